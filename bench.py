@@ -1,0 +1,313 @@
+#!/usr/bin/env python3
+"""bench.py — q4_0 mul_mat on MI355X: decode tok/s (+ prefill GB/s), LLaMA-7B shapes.
+
+Metric (BASELINE.json): "q4_0 mul_mat: decode tok/s + prefill GB/s, LLaMA-7B shapes, 1/2/4/8 GPU".
+
+One step = one decode token through the q4_0 matmuls of LLaMA-7B: 32 layers x 7 mul_mats
+(wq, wk, wv, wo: 4096->4096; w1, w3: 4096->11008; w2: 11008->4096), each including the q8_0
+quantize of its activation row.  The weight stack (3.64 GB of
+block_q4_0 rows, distinct memory per layer) is resident in HBM and larger than the 256 MB
+Infinity Cache.  The 224 launches of a step are captured once in a HIP graph and replayed.
+
+N GPUs (torchrun, one process per GPU): every matrix is row-sharded N ways (the reference's
+GGML_BACKEND_GPU_SPLIT) and each mul_mat ends with an RCCL all-gather of the y slices over
+xGMI; value = tokens/s of the sharded model (strong scaling: total work fixed).
+
+Extra fields: per-kernel roofline of the dominant kernel (the decode GEMV) from HIP events on
+the launch stream, prefill (N=512) GB/s and int8-MFMA TOP/s, and the CPU baseline (the oracle's
+AVX2 restatement of ggml.c's path on this host).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "llama.cpp-q_4_0_amd", "python"))
+
+METRIC = "q4_0 mul_mat: decode tok/s + prefill GB/s, LLaMA-7B shapes, 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+INT8_PEAK_TOPS = 5000.0          # dense int8 MFMA = 2x bf16 per clock (~2.5 PF bf16 dense)
+N_LAYERS = 32
+# (name, K, M) in ggml terms: W [M][K] q4_0, x [N][K], y [N][M]
+LAYER = [("wq", 4096, 4096), ("wk", 4096, 4096), ("wv", 4096, 4096), ("wo", 4096, 4096),
+         ("w1", 4096, 11008), ("w3", 4096, 11008), ("w2", 11008, 4096)]
+
+
+def q4_bytes(K, M):
+    return 18 * K // 32 * M
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------------------------
+def setup_dist(n_gpus):
+    """torchrun env -> (rank, world, local_rank, dist module or None)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or n_gpus > 1:
+        import torch.distributed as dist
+        rank = int(os.environ["RANK"])
+        local = int(os.environ.get("LOCAL_RANK", rank))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        return rank, world, local, dist
+    return 0, 1, 0, None
+
+
+class Stack:
+    """Resident weight stack for one rank: per layer per matrix the rank's row slice."""
+
+    def __init__(self, gh, L, rank, world, layers, seed_base=0x5EED0000):
+        self.mats = []
+        self.bufs = []
+        tmp = gh.DeviceBuffer(max(K * M for _, K, M in LAYER) * 4)
+        total = 0
+        for li in range(layers):
+            row = []
+            for mi, (name, K, M) in enumerate(LAYER):
+                rb = np.zeros(world + 1, np.int64)
+                gh.check(L.ggml_hip_split_rows(M, world, None, rb.ctypes.data_as(ctypes.c_void_p)))
+                m_loc = int(rb[rank + 1] - rb[rank])
+                nbytes = q4_bytes(K, m_loc)
+                buf = gh.DeviceBuffer(max(nbytes, 16))
+                seed = seed_base + li * 16 + mi
+                gh.check(L.ggml_hip_fill_gaussian(tmp.ptr, K * m_loc, seed, 0.0, 0.02, None))
+                gh.check(L.ggml_hip_quantize_q4_0(tmp.ptr, K, m_loc, buf.ptr, None))
+                row.append((name, K, M, m_loc, buf, rb))
+                self.bufs.append(buf)
+                total += nbytes
+            self.mats.append(row)
+        gh.synchronize()
+        tmp.free()
+        self.total_bytes = total
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--layers", type=int, default=N_LAYERS)
+    ap.add_argument("--prefill-tokens", type=int, default=512)
+    ap.add_argument("--no-prefill", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph (launch-per-call)")
+    args = ap.parse_args()
+
+    rank, world, local, dist = setup_dist(args.gpus)
+    import ggml_hip as gh
+    L = gh.load()
+    ndev = L.ggml_hip_device_count()
+    if ndev < 1:
+        raise SystemExit("no HIP device")
+    gh.check(L.ggml_hip_set_device(local % ndev), "set_device")
+    stream = L.ggml_hip_default_stream()
+
+    comm = None
+    if world > 1:
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0:
+            gh.check(L.ggml_hip_comm_unique_id(uid))
+        obj = [uid.raw if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = ctypes.create_string_buffer(obj[0], 128)
+        comm = ctypes.c_void_p()
+        gh.check(L.ggml_hip_comm_init(ctypes.byref(comm), world, rank, uid), "comm_init")
+
+    t0 = time.time()
+    stack = Stack(gh, L, rank, world, args.layers)
+    log(f"[rank {rank}] weight stack {stack.total_bytes / 1e9:.3f} GB resident in {time.time() - t0:.1f}s")
+
+    # activations (one x per K; synthetic N(0,1)) and outputs (one y per M)
+    xs = {}
+    for K in (4096, 11008):
+        b = gh.DeviceBuffer(K * 4 * max(1, args.prefill_tokens))
+        gh.check(L.ggml_hip_fill_gaussian(b.ptr, K * max(1, args.prefill_tokens), 0x5EED1000 + K, 0.0, 1.0, None))
+        xs[K] = b
+    ys = {M: gh.DeviceBuffer(M * 4 * max(1, args.prefill_tokens)) for M in (4096, 11008)}
+    for K in (4096, 11008):
+        gh.check(L.ggml_hip_reserve_workspace(K, max(1, args.prefill_tokens)))
+    gh.synchronize()
+
+    def decode_step():
+        for row in stack.mats:
+            for name, K, M, m_loc, buf, rb in row:
+                if comm is None:
+                    gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, M, xs[K].ptr, 1, ys[M].ptr, M, 0, stream))
+                else:
+                    gh.check(L.ggml_hip_mul_mat_q4_0_split(comm, buf.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
+                                                           xs[K].ptr, 1, ys[M].ptr, stream))
+
+    graph = None
+    if not args.eager:
+        decode_step()                        # first call outside capture (workspace, lazy init)
+        gh.check(L.ggml_hip_stream_synchronize(stream))
+        graph = gh.Graph(stream)
+        with graph:
+            decode_step()
+
+    def run_step():
+        if graph is not None:
+            graph.launch()
+        else:
+            decode_step()
+
+    def barrier():
+        gh.check(L.ggml_hip_device_synchronize())
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        run_step()
+    barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        run_step()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    tok_s = args.steps / elapsed * 32 / args.layers if args.layers else 0.0   # per full 32-layer token
+
+    result = {
+        "metric": METRIC, "value": round(tok_s, 2), "unit": "tok/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "q4_0 x q8_0 (int8 dot, f32 acc)",
+        "data": "synthetic: W ~ N(0,0.02) -> q4_0 (ggml A3 rule, on device), x ~ N(0,1); random-init, no checkpoint",
+        "config": {"workload": "LLaMA-7B q4_0 decode, 32 layers x 7 mul_mats (wq,wk,wv,wo 4096x4096; w1,w3 "
+                               "4096->11008; w2 11008->4096), N=1, q8_0 quantize of x included, lm_head excluded",
+                   "layers": args.layers, "weights_bytes_per_rank": stack.total_bytes,
+                   "graph": graph is not None,
+                   "parallelism": f"row-split x{world} + RCCL all-gather" if world > 1 else "single GPU"},
+    }
+
+    if rank == 0 and world == 1:
+        result["roofline"] = kernel_roofline(gh, L, stack, xs, ys, stream)
+        if not args.no_prefill and args.prefill_tokens > 0:
+            result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens)
+        if not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if comm is not None:
+        L.ggml_hip_comm_destroy(comm)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------------------------
+def kernel_roofline(gh, L, stack, xs, ys, stream, reps=3):
+    """Dominant kernel = the decode GEMV.  Each launch is bracketed by HIP events on its own
+    stream; weights rotate through the whole (>256 MB) stack so every launch streams from HBM.
+    achieved = algorithmic bytes (18MK/32 + 4K + 4M) / mean launch duration."""
+    per_shape = {}
+    evs = [(gh.Event(), gh.Event()) for _ in range(len(stack.mats) * len(LAYER))]
+    for _ in range(reps):
+        i = 0
+        for row in stack.mats:
+            for name, K, M, m_loc, buf, rb in row:
+                a, b = evs[i]
+                a.record(stream)
+                gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, 1, ys[M].ptr, m_loc, 1, stream))
+                b.record(stream)
+                i += 1
+        gh.check(L.ggml_hip_stream_synchronize(stream))
+        i = 0
+        for row in stack.mats:
+            for name, K, M, m_loc, buf, rb in row:
+                a, b = evs[i]
+                per_shape.setdefault((K, m_loc), []).append(a.elapsed_ms(b))
+                i += 1
+    shapes = {}
+    tot_bytes = tot_t = 0.0
+    for (K, M), ts in per_shape.items():
+        t = float(np.mean(ts)) * 1e-3
+        nbytes = q4_bytes(K, M) + 4 * K + 4 * M
+        shapes[f"{K}->{M}"] = {"us": round(t * 1e6, 3), "GBps": round(nbytes / t / 1e9, 1),
+                              "launches": len(ts)}
+        tot_bytes += nbytes * len(ts)
+        tot_t += t * len(ts)
+    achieved = tot_bytes / tot_t / 1e9
+    return {"bound": "hbm", "kernel": "k_gemv_q4_0<1>", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "per_shape": shapes,
+            "bytes_per_launch_def": "18*M*K/32 + 4*K + 4*M (q4_0 weights + f32 x in + f32 y out)"}
+
+
+def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3):
+    """N-token prefill through `layers` layers of the stack (7 mul_mats each, q8_0 quantize +
+    int8-MFMA GEMM).  GB/s = (W + 4KN + 4MN) / t."""
+    mats = [m for row in stack.mats[:layers] for m in row]
+
+    def run():
+        for name, K, M, m_loc, buf, rb in mats:
+            gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, N, ys[M].ptr, m_loc, 2, stream))
+    run()
+    gh.check(L.ggml_hip_stream_synchronize(stream))
+    a, b = gh.Event(), gh.Event()
+    a.record(stream)
+    for _ in range(reps):
+        run()
+    b.record(stream)
+    t = a.elapsed_ms(b) * 1e-3 / reps
+    nbytes = sum(q4_bytes(K, m) + 4 * K * N + 4 * m * N for _, K, M, m, _, _ in mats)
+    ops = sum(2 * K * m * N for _, K, M, m, _, _ in mats)
+    return {"tokens": N, "layers": layers, "ms_per_layer": round(t / layers * 1e3, 4),
+            "GBps": round(nbytes / t / 1e9, 1), "TOPs": round(ops / t / 1e12, 1),
+            "mfma_frac": round(ops / t / 1e12 / INT8_PEAK_TOPS, 4), "peak_TOPs": INT8_PEAK_TOPS,
+            "stack_7B_prefill_ms": round(t / layers * 32 * 1e3, 3)}
+
+
+def cpu_baseline(budget_s):
+    """The oracle's AVX2 restatement of ggml.c's q4_0 mul_mat (quantize_row_q8_0 AVX2 branch +
+    ggml_vec_dot_q4_0_q8_0 AVX2 + row-split threads spawned per call like ggml_graph_compute),
+    timed on this host.  Sample: decode tokens over a rotating set of whole LLaMA-7B layers
+    (> LLC), tok/s = 1 / (32 x layer time)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    nthreads = int(os.environ.get("CPU_BASELINE_THREADS", min(16, os.cpu_count() or 1)))
+    base = []
+    for mi, (name, K, M) in enumerate(LAYER):
+        wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED0000 + mi, 0.0, 0.02).reshape(M, K))
+        base.append((K, wq))
+    n_copies = 6                                   # ~680 MB of weights: beyond any host LLC
+    layers = [[(K, wq.copy()) for K, wq in base] for _ in range(n_copies)]
+    x = {K: O.gaussian(K, 0x5EED1000 + K, 0.0, 1.0).reshape(1, K) for K in (4096, 11008)}
+    O.mul_mat(base[0][1], 4096, x[4096], nthreads=nthreads)   # warm
+    t0 = time.perf_counter()
+    n_layers_run = 0
+    while True:
+        for K, wq in layers[n_layers_run % n_copies]:
+            O.mul_mat(wq, K, x[K], nthreads=nthreads, mode="avx2", pool=False)
+        n_layers_run += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    t = (time.perf_counter() - t0) / n_layers_run
+    import platform
+    cpu = platform.processor() or "x86_64"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(1.0 / (32 * t), 3), "unit": "tok/s", "cores": nthreads, "kind": "port",
+            "sample": f"{n_layers_run} LLaMA-7B decode layers (7 q4_0 GEMVs each, N=1) over {n_copies} rotating "
+                      f"layer copies, {nthreads} threads spawned per mul_mat, AVX2={bool(O.lib().oracle_have_avx2())}, "
+                      f"{budget_s:.0f}s budget; tok/s = 1/(32 x mean layer time)",
+            "ms_per_layer": round(t * 1e3, 3), "cpu": cpu}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,184 @@
+/*
+ * ggml-hip.h — C ABI of the MI355X-native (gfx950) q4_0 mul_mat backend for ggml.
+ *
+ * Drop-in for the reference's GPU backend ABI, ggml-cuda.h:15-36 of
+ * Fcucgvhhhvjv/llama.cpp-q_4_0 (the hook sites in ggml.c / llama.cpp /
+ * arch/arch-util.h call these exactly where they call ggml_cuda_*; see
+ * INTEGRATION.md).  Plain pointers and sizes only; no torch types.
+ *
+ * Scope: GGML_OP_MUL_MAT with src0 = GGML_TYPE_Q4_0, src1 = dst = GGML_TYPE_F32
+ * (the path BASELINE.json names).  Everything else returns "cannot" so ggml's
+ * CPU path runs, exactly as ggml_cuda_can_mul_mat / ggml_cuda_compute_forward
+ * return false for what they do not handle.
+ *
+ * Numerics (pinned by tests/): the q8_0 activation bytes are bit-exact to the
+ * AVX2 branch of quantize_row_q8_0 (ggml.c:1192-1275); y agrees with
+ * ggml_vec_dot_q4_0_q8_0 within 1e-3 relative + fp32 accumulation bound.
+ */
+#ifndef GGML_HIP_H
+#define GGML_HIP_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GGML_HIP_MAX_DEVICES 16   /* GGML_CUDA_MAX_DEVICES, ggml-cuda.h:9 */
+
+struct ggml_tensor;              /* ggml.h:378-414 (mirrored bit-for-bit in csrc/ggml_abi.h) */
+struct ggml_compute_params;      /* ggml.h:459-468 */
+
+/* tensor->extra of device-resident tensors (ggml-cuda.h:11-13): one pointer per
+ * device; for GGML_BACKEND_GPU_SPLIT tensors device i holds its row slice. */
+struct ggml_tensor_extra_gpu {
+    void *data_device[GGML_HIP_MAX_DEVICES];
+};
+
+/* status codes of the tensor-free entry points */
+enum ggml_hip_status {
+    GGML_HIP_OK = 0,
+    GGML_HIP_ERR_INVALID = -1,      /* bad shape / pointer / alignment */
+    GGML_HIP_ERR_UNSUPPORTED = -2,  /* valid request outside the q4_0 path */
+    GGML_HIP_ERR_DEVICE = -3,       /* HIP runtime error (message on stderr) */
+    GGML_HIP_ERR_NOMEM = -4,
+    GGML_HIP_ERR_COMM = -5,         /* RCCL error */
+};
+
+/* ------------------------------------------------------------------------------------------
+ * ggml-cuda.h equivalents (same argument meaning, same error behaviour: HIP errors are
+ * fatal with a message, like CUDA_CHECK in ggml-cuda.cu:22-51).
+ * ---------------------------------------------------------------------------------------- */
+
+/* ggml_init_cublas (ggml-cuda.h:15, ggml-cuda.cu:1826-1861): enumerate devices, default
+ * split proportional to VRAM, one non-blocking stream per device.  Idempotent, thread-safe. */
+void   ggml_init_hip(void);
+/* ggml_cuda_set_tensor_split (ggml-cuda.h:16): per-device fractions (cumulative sums are
+ * normalised, all-zero = keep default). */
+void   ggml_hip_set_tensor_split(const float *tensor_split);
+/* ggml_cuda_can_mul_mat (ggml-cuda.h:19, ggml-cuda.cu:2595-2610). */
+bool   ggml_hip_can_mul_mat(const struct ggml_tensor *src0, const struct ggml_tensor *src1,
+                            struct ggml_tensor *dst);
+/* ggml-cuda.h:20 declares ggml_cuda_mul_mat_get_wsize but ggml-cuda.cu never defines it; ours
+ * returns 0 (no host work buffer is needed). */
+size_t ggml_hip_mul_mat_get_wsize(const struct ggml_tensor *src0, const struct ggml_tensor *src1,
+                                  struct ggml_tensor *dst);
+/* ggml_cuda_mul_mat (ggml-cuda.h:21 / ggml-cuda.cu:2671): dst = src0 x src1 for Q4_0 src0.
+ * Operands may be host (GGML_BACKEND_CPU) or device resident; synchronous on return when dst
+ * is a host tensor. */
+void   ggml_hip_mul_mat(const struct ggml_tensor *src0, const struct ggml_tensor *src1,
+                        struct ggml_tensor *dst);
+/* ggml_cuda_host_malloc / host_free (ggml-cuda.h:24-25): pinned host memory, NULL on failure. */
+void  *ggml_hip_host_malloc(size_t size);
+void   ggml_hip_host_free(void *ptr);
+/* ggml_cuda_transform_tensor (ggml-cuda.h:27, ggml-cuda.cu:2766-2809): upload tensor data
+ * (whole, or the device's row slice for GGML_BACKEND_GPU_SPLIT) and set tensor->extra. */
+void   ggml_hip_transform_tensor(void *data, struct ggml_tensor *tensor);
+/* ggml_cuda_free_data (ggml-cuda.h:29). */
+void   ggml_hip_free_data(struct ggml_tensor *tensor);
+/* ggml_cuda_assign_buffers{,_no_scratch,_force_inplace} (ggml-cuda.h:30-32): give a
+ * graph tensor device storage (scratch ring unless no_scratch). */
+void   ggml_hip_assign_buffers(struct ggml_tensor *tensor);
+void   ggml_hip_assign_buffers_no_scratch(struct ggml_tensor *tensor);
+void   ggml_hip_assign_buffers_force_inplace(struct ggml_tensor *tensor);
+/* ggml_cuda_set_main_device / set_scratch_size / free_scratch (ggml-cuda.h:33-35). */
+void   ggml_hip_set_main_device(int main_device);
+void   ggml_hip_set_scratch_size(size_t scratch_size);
+void   ggml_hip_free_scratch(void);
+/* ggml_cuda_compute_forward (ggml-cuda.h:36, ggml-cuda.cu:2933-3021): returns true when the
+ * node was taken by the backend (the CPU op is then skipped, ggml.c:15645-15652).  Only thread
+ * ith == 0 in the COMPUTE phase launches; the other threads/phases return true immediately. */
+bool   ggml_hip_compute_forward(struct ggml_compute_params *params, struct ggml_tensor *tensor);
+/* ggml_cpu_has_cublas (ggml.c:19465-19470) equivalent: 1 when a HIP device is usable. */
+int    ggml_cpu_has_hipblas(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Tensor-free entry points (device pointers, stream-ordered on `stream` = hipStream_t or NULL
+ * for the backend's stream on the current device).  Return enum ggml_hip_status.
+ * Layouts: ggml's.  W = block_q4_0 rows (18*K/32 bytes per row), x = f32 [N][K] row-major,
+ * y = f32 [N][M] row-major (y[n*M + m], i.e. ggml dst with ne0 = M, ne1 = N).
+ * Pointers must be 16-byte aligned; K % 64 == 0 (ggml.c:2344 asserts nb % 2 == 0).
+ * ---------------------------------------------------------------------------------------- */
+
+/* q8_0 quantize of N activation rows, ggml block_q8_0 output (34*K/32 bytes per row);
+ * bit-exact to quantize_row_q8_0's AVX2 branch (ggml.c:1192-1275). */
+int ggml_hip_quantize_q8_0(const float *dev_x, int64_t K, int64_t N, void *dev_xq, void *stream);
+/* q4_0 weight quantizer, bit-exact to quantize_row_q4_0_reference (ggml.c:918-953). */
+int ggml_hip_quantize_q4_0(const float *dev_w, int64_t K, int64_t M, void *dev_wq, void *stream);
+/* dequantize_row_q4_0 (ggml.c:1500-1518). */
+int ggml_hip_dequantize_q4_0(const void *dev_wq, int64_t K, int64_t M, float *dev_w, void *stream);
+
+/* y = W x (ggml_compute_forward_mul_mat_q_f32, ggml.c:11226-11424, INIT + COMPUTE fused):
+ * N <= 8: fused quantize + GEMV (one wave64 per weight row); N > 8: q8_0 quantize + int8-MFMA
+ * GEMM.  Uses the backend's device workspace for N > 8 (grown outside stream capture by
+ * ggml_hip_reserve_workspace or the first call). */
+int ggml_hip_mul_mat_q4_0(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N,
+                          float *dev_y, void *stream);
+/* Same with an explicit algorithm: 0 auto, 1 GEMV (N <= 8), 2 MFMA GEMM; and output stride ldy. */
+int ggml_hip_mul_mat_q4_0_ex(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N,
+                             float *dev_y, int64_t ldy, int algo, void *stream);
+/* Ensure the current device's workspace can serve mul_mat for N tokens of K (call before
+ * capturing a HIP graph). */
+int ggml_hip_reserve_workspace(int64_t K, int64_t N);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-GPU, one process per GPU (torch.distributed-style ranks), RCCL over xGMI.
+ * The reference row-splits weights across devices (GGML_BACKEND_GPU_SPLIT, ggml-cuda.cu:
+ * 2361-2368, 2773-2806) and gathers each device's dst rows with cudaMemcpyAsync
+ * (ggml-cuda.cu:2514-2539); here every rank holds rows [row_begin[rank], row_begin[rank+1])
+ * and the slices are exchanged with one ncclAllGather.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct ggml_hip_comm ggml_hip_comm;
+
+#define GGML_HIP_UNIQUE_ID_BYTES 128
+/* rank 0 creates the id and ships it to the other ranks (e.g. torch.distributed broadcast). */
+int ggml_hip_comm_unique_id(char out[GGML_HIP_UNIQUE_ID_BYTES]);
+int ggml_hip_comm_init(ggml_hip_comm **comm, int nranks, int rank, const char id[GGML_HIP_UNIQUE_ID_BYTES]);
+int ggml_hip_comm_destroy(ggml_hip_comm *comm);
+/* Row split of M rows over nranks by cumulative fractions (NULL = equal split), the same
+ * rule as the reference's tensor_split (ggml-cuda.cu:1863-1882, 2361-2368).  row_begin has
+ * nranks+1 entries. */
+int ggml_hip_split_rows(int64_t M, int nranks, const float *tensor_split, int64_t *row_begin);
+/* y_full[N][M_total] = W_full x on every rank; this rank holds W rows
+ * [row_begin[rank], row_begin[rank+1]) in dev_w_local (block_q4_0 rows).  Equal splits with
+ * N == 1 gather straight into y_full; otherwise through a padded slab + compaction. */
+int ggml_hip_mul_mat_q4_0_split(ggml_hip_comm *comm, const void *dev_w_local, int64_t K, int64_t M_total,
+                                const int64_t *row_begin, const float *dev_x, int64_t N, float *dev_y_full,
+                                void *stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Device plumbing for bindings (ctypes / cgo / JNI) that have no HIP headers.
+ * ---------------------------------------------------------------------------------------- */
+int    ggml_hip_device_count(void);
+int    ggml_hip_set_device(int device);
+int    ggml_hip_get_device(void);
+void  *ggml_hip_dev_malloc(size_t size);
+void   ggml_hip_dev_free(void *ptr);
+int    ggml_hip_memcpy_h2d(void *dst, const void *src, size_t size, void *stream);
+int    ggml_hip_memcpy_d2h(void *dst, const void *src, size_t size, void *stream);
+int    ggml_hip_memcpy_d2d(void *dst, const void *src, size_t size, void *stream);
+int    ggml_hip_memset(void *dst, int value, size_t size, void *stream);
+int    ggml_hip_stream_synchronize(void *stream);
+int    ggml_hip_device_synchronize(void);
+void  *ggml_hip_default_stream(void);          /* the backend's stream on the current device */
+int    ggml_hip_fill_gaussian(float *dev_dst, int64_t n, uint64_t seed, float mean, float stdv, void *stream);
+/* timing and HIP-graph capture on a stream (bench harness; launch-bound decode chains) */
+void  *ggml_hip_event_create(void);
+int    ggml_hip_event_record(void *event, void *stream);
+float  ggml_hip_event_elapsed_ms(void *start, void *stop);   /* waits for stop */
+void   ggml_hip_event_destroy(void *event);
+typedef struct ggml_hip_graph ggml_hip_graph;
+int    ggml_hip_graph_begin(void *stream);
+int    ggml_hip_graph_end(void *stream, ggml_hip_graph **graph);
+int    ggml_hip_graph_launch(ggml_hip_graph *graph, void *stream);
+int    ggml_hip_graph_destroy(ggml_hip_graph *graph);
+const char *ggml_hip_last_error(void);
+const char *ggml_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GGML_HIP_H */

@@ -1,0 +1,51 @@
+// q4_0_kernels.h — launchers for the gfx950 q4_0 x q8_0 kernels (internal to libggml_hip.so).
+//
+// Data layouts in HBM:
+//   W   : ggml block_q4_0 rows, verbatim (ggml.c:870-875): row m at W + m*rowbytes,
+//         rowbytes = 18*K/32; block = fp16 d + 16 bytes of nibbles (elem j: low nibble
+//         of qs[j], elem j+16: high nibble).  Never repacked.
+//   x   : f32 [N][K] (ggml src1, nb10 == 4).
+//   y   : f32 [N][ldy] (ggml dst, y[n*ldy + m]).
+//   xq8 : ggml block_q8_0 rows (ggml.c:902-907), AoS, 34*K/32 bytes per token — the
+//         reference's INIT wdata layout; produced by quantize_q8_0_aos.
+//   xs  : internal GEMM operand: int8 qs [N][K] + f32 d [N][K/32] (fp32 value of the
+//         fp16-rounded scale), produced by quantize_q8_0_soa from the same device
+//         quantizer; bit-identical q8_0 values.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ghip {
+
+struct DeviceInfo {
+    int num_cus;
+};
+
+// A5 (AVX2 branch semantics, bit-exact): x f32 [N][K] -> block_q8_0 AoS [N][K/32].
+hipError_t quantize_q8_0_aos(const float *x, int64_t K, int64_t N, void *xq8, hipStream_t s);
+// Same quantizer, GEMM operand layout.
+hipError_t quantize_q8_0_soa(const float *x, int64_t K, int64_t N, int8_t *qs, float *d, hipStream_t s);
+// A3 (quantize_row_q4_0_reference semantics, bit-exact): w f32 [M][K] -> block_q4_0 rows.
+hipError_t quantize_q4_0(const float *w, int64_t K, int64_t M, void *wq, hipStream_t s);
+// A4: block_q4_0 rows -> f32 [M][K].
+hipError_t dequantize_q4_0(const void *wq, int64_t K, int64_t M, float *w, hipStream_t s);
+
+// Decode / small-batch path: fused q8_0 quantize of x (in LDS) + q4_0.q8_0 GEMV.
+// N <= gemv_max_tokens(K).
+int gemv_max_tokens(int64_t K);
+hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_t N,
+                     float *y, int64_t ldy, const DeviceInfo &dev, hipStream_t s);
+
+// Prefill path: int8 MFMA (v_mfma_i32_32x32x32_i8, K=32 = one q4_0 block) GEMM on the
+// pre-quantized activations xs (quantize_q8_0_soa).
+hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd,
+                     int64_t N, float *y, int64_t ldy, hipStream_t s);
+
+// Multi-GPU helper: y[n*ldy + row0[r] + i] = slab[r][n][i] for i < rows[r] (gather compaction).
+hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const int64_t *row_begin_dev,
+                         int64_t N, float *y, int64_t ldy, hipStream_t s);
+
+// Synthetic inputs for the bench (splitmix64 + Box-Muller on device).
+hipError_t fill_gaussian(float *dst, int64_t n, uint64_t seed, float mean, float std, hipStream_t s);
+
+}  // namespace ghip

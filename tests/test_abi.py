@@ -1,0 +1,104 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library builds, loads and exports every
+symbol include/ggml-hip.h declares; the ggml_tensor mirror matches ggml.h; host-only logic
+(row split, can_mul_mat rule) behaves like the reference.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from hip_env import LIB_PATH, PKG, ggml_hip
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", PKG, "-j4"])
+    return ggml_hip.load()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    declared = ggml_hip.declared_symbols()
+    assert len(declared) >= 50
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [s for s in declared if s not in exported]
+    assert not missing, missing
+    for s in declared:
+        assert hasattr(lib, s)
+
+
+def test_library_targets_gfx950_only():
+    out = subprocess.check_output(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", LIB_PATH], text=True,
+                                  stderr=subprocess.STDOUT) if False else ""
+    blob = open(LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+    for other in (b"gfx942", b"gfx90a", b"gfx1100"):
+        assert other not in blob
+
+
+def test_no_oracle_linkage():
+    """The product must never route through the oracle / a CPU fallback."""
+    out = subprocess.check_output(["nm", "-D", LIB_PATH], text=True)
+    assert "oracle_" not in out
+    deps = subprocess.check_output(["readelf", "-d", LIB_PATH], text=True)
+    assert "oracle" not in deps
+    assert "libamdhip64" in deps and "librccl" in deps
+
+
+def test_ggml_tensor_mirror_layout():
+    T = ggml_hip.GgmlTensor
+    assert ctypes.sizeof(T) == 240
+    off = {name: getattr(T, name).offset for name, _ in T._fields_}
+    assert (off["ne"], off["nb"], off["op"], off["src0"], off["src1"], off["n_tasks"], off["data"],
+            off["name"], off["extra"]) == (16, 48, 80, 96, 104, 144, 168, 176, 224)
+    assert ctypes.sizeof(ggml_hip.GgmlComputeParams) == 32
+
+
+@pytest.mark.parametrize("M,n", [(4096, 8), (11008, 8), (5120, 8), (13824, 8), (4672, 3), (7, 4), (0, 2)])
+def test_split_rows_equal(lib, M, n):
+    rb = np.zeros(n + 1, np.int64)
+    ggml_hip.check(lib.ggml_hip_split_rows(M, n, None, rb.ctypes.data_as(ctypes.c_void_p)))
+    assert rb[0] == 0 and rb[-1] == M and np.all(np.diff(rb) >= 0)
+    assert np.diff(rb).max() - np.diff(rb).min() <= 1
+
+
+def test_split_rows_fractions_match_reference_rule(lib):
+    """ggml-cuda.cu:1863-1882 normalises cumulative fractions; rows = (int)(nrows*split[id])."""
+    ts = np.array([3.0, 1.0, 2.0, 2.0], np.float32)
+    M = 11008
+    rb = np.zeros(5, np.int64)
+    ggml_hip.check(lib.ggml_hip_split_rows(M, 4, ts.ctypes.data_as(ctypes.c_void_p), rb.ctypes.data_as(ctypes.c_void_p)))
+    cum = np.concatenate([[0], np.cumsum(ts)[:-1]]).astype(np.float32) / np.float32(ts.sum())
+    expect = [0] + [int(np.float32(M) * c) for c in cum[1:]] + [M]
+    assert list(rb) == expect
+
+
+def test_can_mul_mat_rule(lib):
+    """Q4_0 x F32 -> F32 with ne0, ne1, ne10 >= 32 (ggml-cuda.cu:2595-2610); other types: no."""
+    K, M = 4096, 64
+    for N, expect in ((32, True), (31, False), (512, True)):
+        w = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_Q4_0, (K, M))
+        x = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (K, N))
+        y = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (M, N))
+        assert lib.ggml_hip_can_mul_mat(ctypes.byref(w), ctypes.byref(x), ctypes.byref(y)) == expect
+    wf = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (K, M))
+    assert not lib.ggml_hip_can_mul_mat(ctypes.byref(wf), ctypes.byref(x), ctypes.byref(y))
+    w96 = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_Q4_0, (96, M))     # K % 64 != 0 -> CPU path
+    x96 = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (96, 64))
+    y96 = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (M, 64))
+    assert not lib.ggml_hip_can_mul_mat(ctypes.byref(w96), ctypes.byref(x96), ctypes.byref(y96))
+    assert lib.ggml_hip_mul_mat_get_wsize(ctypes.byref(w), ctypes.byref(x), ctypes.byref(y)) == 0
+
+
+def test_compute_forward_declines_other_ops_without_device(lib):
+    """Non-MUL_MAT nodes are never taken (ggml.c falls through to its CPU op)."""
+    t = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (64, 64))
+    t.op = 5   # not MUL_MAT
+    p = ggml_hip.GgmlComputeParams(ggml_hip.GGML_TASK_COMPUTE, 0, 1, 0, None)
+    assert not lib.ggml_hip_compute_forward(ctypes.byref(p), ctypes.byref(t))
+
+
+def test_version(lib):
+    assert b"gfx950" in lib.ggml_hip_version()

@@ -1,0 +1,288 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bar (BASELINE.json north_star): q8_0 activation bytes bit-exact to the reference's AVX2
+branch; y within 1e-3 relative on the fp32 accumulator, with the cancellation-safe bound of
+tests/parity.py (|dy| <= 1e-3|y| + atol_blocks * sum_b |d_w d_x sumi|).  q4_0 weight
+quantization and dequantization are bit-exact.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_io import load
+from hip_env import ggml_hip, gpu_available
+from parity import block_terms, check_y
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs a HIP device and libggml_hip.so")]
+
+DB = ggml_hip.DeviceBuffer
+RTOL, ATOL_BLOCKS = 1e-3, 1e-5
+
+
+def gpu_q8(x):
+    x = np.ascontiguousarray(x, np.float32)
+    N, K = x.shape
+    xd = DB.from_array(x)
+    xq = DB(N * K // 32 * 34)
+    ggml_hip.quantize_q8_0(xd, K, N, xq)
+    return xq.download((N, K // 32 * 34), np.uint8)
+
+
+def gpu_mul_mat(wq, K, x, algo=0, ldy=None):
+    x = np.ascontiguousarray(x, np.float32)
+    N = x.shape[0]
+    M = wq.shape[0]
+    ldy = M if ldy is None else ldy
+    wd, xd = DB.from_array(wq), DB.from_array(x)
+    yd = DB(max(N, 1) * ldy * 4)
+    ggml_hip.load().ggml_hip_memset(yd.ptr, 0x7F, yd.nbytes, None)
+    ggml_hip.mul_mat(wd, K, M, xd, N, yd, algo=algo, ldy=ldy)
+    y = yd.download((max(N, 1), ldy), np.float32)
+    return y[:N, :M], y
+
+
+def upper_s_abs(wq, xq, K):
+    """sum_b |d_w d_x sumi| <= |W_deq| @ |X_deq|^T (cheap at full size)."""
+    dw = O.dequantize_q4_0(wq, K).astype(np.float64)
+    from parity import split_q8_0
+    d, q = split_q8_0(xq, K)
+    xdq = (q.astype(np.float64) * d[:, :, None]).reshape(xq.shape[0], K)
+    return np.abs(xdq) @ np.abs(dw).T
+
+
+def make_case(K, M, N, seed, wstd=0.02, xscale=1.0):
+    wf = O.gaussian(M * K, 0x5EED0000 + seed, 0.0, wstd).reshape(M, K)
+    wq, _ = O.quantize_q4_0(wf)
+    x = O.gaussian(N * K, 0x5EED1000 + seed, 0.0, xscale).reshape(N, K)
+    return wq, x
+
+
+# ------------------------------------------------------------------------------- q8_0 (A5)
+def test_q8_0_bitexact_golden():
+    x = load("avx2", "x4096_f32")
+    assert np.array_equal(gpu_q8(x), load("avx2", "x4096_q8_0"))
+    t = load("avx2", "tie_x_f32").reshape(1, -1)
+    assert np.array_equal(gpu_q8(t).reshape(8, 34), load("avx2", "tie_q8_0"))
+
+
+@pytest.mark.parametrize("K,N", [(64, 1), (4096, 7), (4544, 3), (11008, 5), (13824, 2)])
+def test_q8_0_bitexact_random_scales(K, N):
+    rng = np.random.default_rng(K + N)
+    x = (rng.standard_normal((N, K)) * np.exp(rng.uniform(-12, 10, (N, K // 32))).repeat(32, 1)).astype(np.float32)
+    x[0, :32] = 0.0                                   # amax == 0 block
+    x[-1, 32:64] = np.float32(1e-30)                  # d underflows fp16
+    assert np.array_equal(gpu_q8(x), O.quantize_q8_0(x, "avx2"))
+
+
+def test_q8_0_half_integer_ties_round_to_even():
+    """Blocks with amax = 127 (id = 1 exactly) and half-integer values: every element is a tie."""
+    K = 128
+    x = np.zeros((1, K), np.float32)
+    for b in range(3):
+        x[0, 32 * b:32 * b + 32] = (np.arange(32) - 16).astype(np.float32) + 0.5 * (b + 1) % 2 + 0.5 * (b == 1)
+        x[0, 32 * b + 7] = 127.0 if b != 1 else -127.0
+    x[0, 96:128] = np.linspace(-126.5, 126.5, 32).astype(np.float32)
+    x[0, 100] = 127.0
+    assert np.array_equal(gpu_q8(x), O.quantize_q8_0(x, "avx2"))
+    assert not np.array_equal(O.quantize_q8_0(x, "avx2"), O.quantize_q8_0(x, "ref"))   # ties do differ
+
+
+# ------------------------------------------------------------------------------- q4_0 (A3/A4)
+@pytest.mark.parametrize("K,M", [(128, 1), (4096, 64), (4544, 8)])
+def test_q4_0_quantize_bitexact(K, M):
+    w = O.gaussian(M * K, 0x5EED0001 if (K, M) == (4096, 64) else 77 + K, 0.0, 0.02).reshape(M, K)
+    wd = DB.from_array(w)
+    qd = DB(M * K // 32 * 18)
+    ggml_hip.quantize_q4_0(wd, K, M, qd)
+    got = qd.download((M, K // 32 * 18), np.uint8)
+    ref, _ = O.quantize_q4_0(w)
+    assert np.array_equal(got, ref)
+    if (K, M) == (4096, 64):
+        assert np.array_equal(got, load("avx2", "w4096_q4_0"))
+
+
+def test_q4_0_quantize_ties_golden():
+    w = load("avx2", "q4tie_w_f32").reshape(1, 128)
+    wd = DB.from_array(w)
+    qd = DB(4 * 18)
+    ggml_hip.quantize_q4_0(wd, 128, 1, qd)
+    assert np.array_equal(qd.download((4, 18), np.uint8), load("avx2", "q4tie_q4_0"))
+
+
+def test_dequantize_bitexact_golden():
+    wq = load("avx2", "w4096_q4_0")[:2]
+    qd = DB.from_array(wq)
+    od = DB(2 * 4096 * 4)
+    ggml_hip.dequantize_q4_0(qd, 4096, 2, od)
+    got = od.download((2, 4096), np.float32)
+    assert np.array_equal(got.view(np.uint32), load("avx2", "w4096_dequant_rows01").view(np.uint32))
+
+
+# ------------------------------------------------------------------------------- mul_mat vs golden
+@pytest.mark.parametrize("algo", [1, 2])
+def test_mul_mat_golden_llama_slice(algo):
+    wq, x = load("avx2", "w4096_q4_0"), load("avx2", "x4096_f32")
+    y, _ = gpu_mul_mat(wq, 4096, x, algo=algo)
+    y_ref = load("avx2", "y4096_mul_mat")
+    _, s_abs = block_terms(wq, load("avx2", "x4096_q8_0"), 4096)
+    rel, _ = check_y(y, y_ref, s_abs, RTOL, ATOL_BLOCKS)
+    assert rel < 1e-3
+
+
+@pytest.mark.parametrize("algo", [1, 2])
+def test_mul_mat_golden_falcon_k4544(algo):
+    wq, x = load("avx2", "w4544_q4_0"), load("avx2", "x4544_f32")
+    y, _ = gpu_mul_mat(wq, 4544, x, algo=algo)
+    xq = O.quantize_q8_0(x, "avx2")
+    _, s_abs = block_terms(wq, xq, 4544)
+    check_y(y, load("avx2", "y4544_mul_mat"), s_abs, RTOL, ATOL_BLOCKS)
+
+
+# ------------------------------------------------------------------------------- mul_mat vs oracle
+@pytest.mark.parametrize("K,M,N", [
+    (64, 1, 1), (64, 33, 3), (128, 100, 8), (4096, 257, 2), (4544, 4672 // 8, 1), (11008, 96, 4),
+    (64, 130, 9), (256, 129, 31), (4096, 128, 33), (4544, 200, 65), (11008, 130, 64), (4096, 64, 100),
+])
+def test_mul_mat_vs_oracle_edges(K, M, N):
+    wq, x = make_case(K, M, N, seed=K * 7 + M + N)
+    y, yfull = gpu_mul_mat(wq, K, x)
+    xq = O.quantize_q8_0(x, "avx2")
+    y_ref = O.mul_mat(wq, K, x, nthreads=4)
+    _, s_abs = block_terms(wq, xq, K)
+    check_y(y, y_ref, s_abs, RTOL, ATOL_BLOCKS)
+
+
+@pytest.mark.parametrize("N", [1, 2, 5, 8])
+def test_gemv_and_gemm_agree(N):
+    wq, x = make_case(4096, 192, N, seed=N)
+    y1, _ = gpu_mul_mat(wq, 4096, x, algo=1)
+    y2, _ = gpu_mul_mat(wq, 4096, x, algo=2)
+    _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), 4096)
+    check_y(y1, y2, s_abs, RTOL, ATOL_BLOCKS)
+
+
+def test_ldy_stride_and_no_out_of_bounds_writes():
+    wq, x = make_case(4096, 100, 3, seed=5)
+    for algo in (1, 2):
+        y, yfull = gpu_mul_mat(wq, 4096, x, algo=algo, ldy=128)
+        assert np.all(yfull[:, 100:].view(np.uint32) == 0x7F7F7F7F), "wrote outside [0, M) of a row"
+        y_ref = O.mul_mat(wq, 4096, x)
+        _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), 4096)
+        check_y(y, y_ref, s_abs, RTOL, ATOL_BLOCKS)
+
+
+def test_zero_and_extreme_activations():
+    K, M = 4096, 64
+    wq, _ = make_case(K, M, 1, seed=9)
+    x = np.zeros((4, K), np.float32)
+    x[1] = 1e-20
+    x[2, ::7] = 3e4
+    x[3] = O.gaussian(K, 3, 0.0, 1.0) * np.float32(1e-3)
+    y, _ = gpu_mul_mat(wq, K, x)
+    assert np.all(y[0] == 0.0)
+    _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
+    check_y(y, O.mul_mat(wq, K, x), s_abs, RTOL, ATOL_BLOCKS)
+
+
+def test_invalid_arguments_fail_loudly():
+    L = ggml_hip.load()
+    wq, x = make_case(128, 4, 1, seed=1)
+    wd, xd, yd = DB.from_array(wq), DB.from_array(x), DB(4 * 4)
+    assert L.ggml_hip_mul_mat_q4_0(wd.ptr, 96, 4, xd.ptr, 1, yd.ptr, None) == ggml_hip.ERR_INVALID
+    assert L.ggml_hip_mul_mat_q4_0(wd.ptr + 4, 128, 4, xd.ptr, 1, yd.ptr, None) == ggml_hip.ERR_INVALID
+    assert L.ggml_hip_mul_mat_q4_0_ex(wd.ptr, 128, 4, xd.ptr, 9, yd.ptr, 4, 1, None) == ggml_hip.ERR_INVALID
+    assert L.ggml_hip_mul_mat_q4_0(wd.ptr, 128, 4, xd.ptr, 0, yd.ptr, None) == ggml_hip.OK   # N == 0: no-op
+
+
+# ------------------------------------------------------------------------------- full LLaMA shapes
+@pytest.mark.parametrize("K,M", [(4096, 4096), (4096, 11008), (11008, 4096)])
+def test_llama7b_decode_full_shape(K, M):
+    wq, x = make_case(K, M, 1, seed=K + M)
+    y, _ = gpu_mul_mat(wq, K, x)
+    y_ref = O.mul_mat(wq, K, x, nthreads=8, mode="avx2", pool=False)
+    xq = O.quantize_q8_0(x, "avx2")
+    assert np.array_equal(gpu_q8(x), xq)
+    check_y(y, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
+
+
+@pytest.mark.parametrize("K,M", [(4096, 4096), (4096, 11008)])
+def test_llama7b_prefill_512_full_shape(K, M):
+    wq, x = make_case(K, M, 512, seed=3 * K + M)
+    y, _ = gpu_mul_mat(wq, K, x)
+    y_ref = O.mul_mat(wq, K, x, nthreads=8, mode="avx2", pool=True)
+    xq = O.quantize_q8_0(x, "avx2")
+    rel, _ = check_y(y, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
+    assert rel < 1e-3
+    # size-independent property: linearity in x (x -> 2x doubles q8 scales exactly)
+    y2, _ = gpu_mul_mat(wq, K, 2 * x[:64])
+    assert np.array_equal(y2.view(np.uint32), (2 * y[:64]).view(np.uint32))
+
+
+# ------------------------------------------------------------------------------- tensor ABI (host tensors)
+def test_tensor_abi_compute_forward_host_tensors():
+    """ggml.c:15645-15652 hook: node taken, only ith == 0 / COMPUTE computes; batch dim ne2 = 2."""
+    L = ggml_hip.load()
+    K, M, N = 4096, 96, 40
+    wq, x = make_case(K, M * 2, N * 2, seed=11)
+    w_np = np.ascontiguousarray(wq)
+    x_np = np.ascontiguousarray(x)
+    y_np = np.zeros((2, N, M), np.float32)
+    w = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_Q4_0, (K, M, 2), w_np)
+    xt = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (K, N, 2), x_np)
+    y = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (M, N, 2), y_np)
+    y.op = ggml_hip.GGML_OP_MUL_MAT
+    y.src0 = ctypes.pointer(w)
+    y.src1 = ctypes.pointer(xt)
+    for phase, ith in ((ggml_hip.GGML_TASK_INIT, 0), (ggml_hip.GGML_TASK_COMPUTE, 1)):
+        p = ggml_hip.GgmlComputeParams(phase, ith, 2, 0, None)
+        assert L.ggml_hip_compute_forward(ctypes.byref(p), ctypes.byref(y))
+    assert np.all(y_np == 0.0)                      # nothing computed yet
+    p = ggml_hip.GgmlComputeParams(ggml_hip.GGML_TASK_COMPUTE, 0, 2, 0, None)
+    assert L.ggml_hip_compute_forward(ctypes.byref(p), ctypes.byref(y))
+    for b in range(2):
+        wb = w_np[b * M:(b + 1) * M]
+        xb = x_np[b * N:(b + 1) * N]
+        _, s_abs = block_terms(wb, O.quantize_q8_0(xb, "avx2"), K)
+        check_y(y_np[b], O.mul_mat(wb, K, xb), s_abs, RTOL, ATOL_BLOCKS)
+
+
+def test_tensor_abi_transform_tensor_resident_weights():
+    """ggml_cuda_transform_tensor equivalent: upload once, extra->data_device[main]; decode N=1."""
+    L = ggml_hip.load()
+    K, M = 4096, 256
+    wq, x = make_case(K, M, 1, seed=12)
+    w_np, x_np = np.ascontiguousarray(wq), np.ascontiguousarray(x)
+    y_np = np.zeros((1, M), np.float32)
+    w = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_Q4_0, (K, M), w_np, backend=ggml_hip.GGML_BACKEND_GPU)
+    L.ggml_hip_transform_tensor(w_np.ctypes.data_as(ctypes.c_void_p), ctypes.byref(w))
+    assert w.extra
+    xt = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (K, 1), x_np)
+    y = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (M, 1), y_np)
+    y.op = ggml_hip.GGML_OP_MUL_MAT
+    y.src0 = ctypes.pointer(w)
+    y.src1 = ctypes.pointer(xt)
+    p = ggml_hip.GgmlComputeParams(ggml_hip.GGML_TASK_COMPUTE, 0, 1, 0, None)
+    assert L.ggml_hip_compute_forward(ctypes.byref(p), ctypes.byref(y))   # any_on_device -> taken at N=1
+    _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
+    check_y(y_np, O.mul_mat(wq, K, x), s_abs, RTOL, ATOL_BLOCKS)
+    L.ggml_hip_free_data(ctypes.byref(w))
+    assert not w.extra
+
+
+def test_graph_capture_replays_gemv():
+    K, M = 4096, 512
+    wq, x = make_case(K, M, 1, seed=13)
+    wd, xd, yd = DB.from_array(wq), DB.from_array(x), DB(M * 4)
+    L = ggml_hip.load()
+    s = L.ggml_hip_default_stream()
+    g = ggml_hip.Graph(s)
+    with g:
+        ggml_hip.mul_mat(wd, K, M, xd, 1, yd, stream=s)
+    L.ggml_hip_memset(yd.ptr, 0, M * 4, s)
+    g.launch()
+    y = yd.download((1, M), np.float32, stream=s)
+    _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
+    check_y(y, O.mul_mat(wq, K, x), s_abs, RTOL, ATOL_BLOCKS)

@@ -19,6 +19,7 @@
 #include "q4_0_kernels.h"
 
 #include <climits>
+#include <cstdlib>
 
 namespace ghip {
 
@@ -151,8 +152,9 @@ __global__ __launch_bounds__(256) void k_quantize_q4_0(const float *__restrict__
         uint32_t b2 = 0;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
-            int q0 = (int)(signed char)(int)(v[j + t] * id + 8.5f);
-            int q1 = (int)(signed char)(int)(v[j + t + QK / 2] * id + 8.5f);
+            // separate rounding of v*id and +8.5 (no FMA contraction), as the C reference
+            int q0 = (int)(signed char)(int)(__fmul_rn(v[j + t], id) + 8.5f);
+            int q1 = (int)(signed char)(int)(__fmul_rn(v[j + t + QK / 2], id) + 8.5f);
             q0 = q0 > 15 ? 15 : q0;
             q1 = q1 > 15 ? 15 : q1;
             b2 |= (uint32_t)((q0 & 0xFF) | ((q1 & 0xFF) << 4)) << (8 * t);
@@ -194,17 +196,22 @@ hipError_t dequantize_q4_0(const void *wq, int64_t K, int64_t M, float *w, hipSt
 // ---------------------------------------------------------------------------------------------
 // GEMV (decode, N <= 8).
 //
-// Lane p of a wave owns block pairs p, p+64, ... of one weight row.  A pair is 36 bytes
+// Lane p of a wave owns block pair p of a 64-pair chunk of one weight row.  A pair is 36 bytes
 // (9 dwords): the 18-byte blocks of a row start 4-byte aligned every second block, so a pair
-// is always dword aligned and the 64 lanes of one load instruction read 2,304 contiguous
-// bytes of the row (all of a K=4096 row).  Loads are buffer_load_dwordx4/x4/x1 with the
-// row's descriptor (out-of-row lanes read 0, no fault).  The even block's qs are re-aligned
-// with v_alignbyte_b32.  x is quantized once per workgroup into LDS (q8_0 ints + fp32 d +
+// is always dword aligned and the 64 lanes of one load read 2,304 contiguous bytes (a whole
+// K=4096 row).  Loads are buffer_load_dwordx4/x4/x1 through the row's descriptor
+// (out-of-row lanes read 0, no fault).  The even block's qs are re-aligned with
+// v_alignbyte_b32.  x is quantized once per workgroup into LDS (q8_0 ints + fp32 d +
 // 8*sum(q)); the q4_0 nibbles enter v_dot4c_i32_i8 unsigned (0..15) and the -8 offset is
 // applied once per block as -8*sum(q):  sum((n-8)*q) = sum(n*q) - 8*sum(q).
+//
+// Schedule: the activation loads are issued first, then the wave's first weight chunk, so
+// the q8_0 prologue overlaps the first HBM round trip; after the prologue each wave walks its
+// (row, chunk) items with the next chunk's loads in flight while the current one computes.
 
 static constexpr int GEMV_THREADS = 1024;
 static constexpr int GEMV_LDS_MAX = 64 * 1024;
+static constexpr int GEMV_PRO = 4;          // activation float4 loads in flight per thread
 
 __device__ __forceinline__ int dot_q4_q8(uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3,
                                          const uint32_t *__restrict__ xb) {
@@ -223,6 +230,20 @@ __device__ __forceinline__ int dot_q4_q8(uint32_t q0, uint32_t q1, uint32_t q2, 
     return s;
 }
 
+struct PairRegs {
+    u32x4 a, b;
+    uint32_t c;
+};
+
+__device__ __forceinline__ PairRegs load_pair(const uint8_t *row, int64_t rowbytes, int p) {
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(row, (uint32_t)rowbytes);
+    PairRegs v;
+    v.a = __builtin_amdgcn_raw_buffer_load_b128(r, 36 * p, 0, 0);
+    v.b = __builtin_amdgcn_raw_buffer_load_b128(r, 36 * p + 16, 0, 0);
+    v.c = __builtin_amdgcn_raw_buffer_load_b32(r, 36 * p + 32, 0, 0);
+    return v;
+}
+
 template <int NT>
 __global__ __launch_bounds__(GEMV_THREADS) void k_gemv_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes,
                                                              int nb, int M, const float *__restrict__ x, int K,
@@ -237,80 +258,105 @@ __global__ __launch_bounds__(GEMV_THREADS) void k_gemv_q4_0(const uint8_t *__res
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nwaves = GEMV_THREADS / 64;
     const int npairs = nb >> 1;
+    const int nchunk = (npairs + 63) >> 6;
     const int rstride = gridDim.x * nwaves;
-    int row = blockIdx.x * nwaves + wave;
+    const int row0 = blockIdx.x * nwaves + wave;
+    const int nrows_w = row0 < M ? (M - 1 - row0) / rstride + 1 : 0;
+    const int nitems = nrows_w * nchunk;                            // (row, chunk) items of this wave
 
-    // Issue the first row's first pair-chunk before the activation prologue so the HBM
-    // stream starts at kernel entry.
-    u32x4 pa = {0, 0, 0, 0}, pb = {0, 0, 0, 0};
-    uint32_t pc = 0;
-    if (row < M) {
-        const __amdgpu_buffer_rsrc_t r = make_rsrc(W + (int64_t)row * rowbytes, (uint32_t)rowbytes);
-        pa = __builtin_amdgcn_raw_buffer_load_b128(r, 36 * lane, 0, 0);
-        pb = __builtin_amdgcn_raw_buffer_load_b128(r, 36 * lane + 16, 0, 0);
-        pc = __builtin_amdgcn_raw_buffer_load_b32(r, 36 * lane + 32, 0, 0);
-    }
-
-    // INIT: q8_0 of the NT activation rows into LDS (bit-exact AVX2 semantics).
-    for (int t = tid; t < NT * nb * 8; t += GEMV_THREADS) {
-        const int n = t / (nb * 8);
-        const int r = t - n * (nb * 8);
-        const float4 v = *reinterpret_cast<const float4 *>(x + (int64_t)n * K + 4 * r);
-        uint32_t d16;
-        int qsum;
-        const uint32_t packed = q8_block_lane(v, d16, qsum);
-        xq[n * nb * 8 + r] = packed;
-        if ((r & 7) == 0) {
-            xd[n * nb + (r >> 3)] = h2f(d16);
-            xs[n * nb + (r >> 3)] = 8 * qsum;
+    // ---- INIT: q8_0 of the NT activation rows into LDS, first weight chunk issued in between.
+    // x of the NT tokens is contiguous ([NT][K] f32), so thread t's float4 is at byte 16*t.  All
+    // loads are unconditional buffer loads (out-of-range -> 0, no traffic) so the compiler can
+    // count vmcnt exactly: the q8_0 math waits for the activations only, not the weights.
+    const int total = NT * nb * 8;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, (uint32_t)total * 16u);
+    auto quantize_into_lds = [&](const u32x4 &raw, int t) {
+        if (t < total) {                                            // whole 8-lane groups agree
+            const float4 v = make_float4(__uint_as_float(raw.x), __uint_as_float(raw.y),
+                                         __uint_as_float(raw.z), __uint_as_float(raw.w));
+            uint32_t d16;
+            int qsum;
+            const uint32_t packed = q8_block_lane(v, d16, qsum);
+            xq[t] = packed;
+            if ((t & 7) == 0) {
+                xd[t >> 3] = h2f(d16);
+                xs[t >> 3] = 8 * qsum;
+            }
         }
+    };
+    u32x4 xv[GEMV_PRO];
+#pragma unroll
+    for (int i = 0; i < GEMV_PRO; i++)
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * GEMV_THREADS), 0, 0);
+    PairRegs cur = load_pair(W + (int64_t)(nitems > 0 ? row0 : 0) * rowbytes, nitems > 0 ? rowbytes : 0, lane);
+#pragma unroll
+    for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], tid + i * GEMV_THREADS);
+    for (int base = GEMV_PRO * GEMV_THREADS; base < total; base += GEMV_PRO * GEMV_THREADS) {
+#pragma unroll
+        for (int i = 0; i < GEMV_PRO; i++)
+            xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * GEMV_THREADS), 0, 0);
+#pragma unroll
+        for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], base + tid + i * GEMV_THREADS);
     }
     __syncthreads();
 
-    for (bool first = true; row < M; row += rstride, first = false) {
-        const __amdgpu_buffer_rsrc_t r = make_rsrc(W + (int64_t)row * rowbytes, (uint32_t)rowbytes);
-        float acc[NT];
+    // ---- COMPUTE: stream the wave's (row, chunk) items with one item in flight.  Two named
+    // register sets (no register copies: a copy would force a wait on the in-flight loads).
+    float acc[NT];
 #pragma unroll
-        for (int n = 0; n < NT; n++) acc[n] = 0.0f;
-        for (int p = lane; p < npairs; p += 64) {
-            u32x4 a, b;
-            uint32_t c;
-            if (first && p == lane) {
-                a = pa; b = pb; c = pc;
-            } else {
-                a = __builtin_amdgcn_raw_buffer_load_b128(r, 36 * p, 0, 0);
-                b = __builtin_amdgcn_raw_buffer_load_b128(r, 36 * p + 16, 0, 0);
-                c = __builtin_amdgcn_raw_buffer_load_b32(r, 36 * p + 32, 0, 0);
-            }
+    for (int n = 0; n < NT; n++) acc[n] = 0.0f;
+    auto item_row = [&](int it) { return row0 + (it / nchunk) * rstride; };
+    auto issue = [&](int it) {
+        const bool valid = it < nitems;                             // past the end: zero-size descriptor
+        const int r = valid ? item_row(it) : row0;
+        return load_pair(W + (int64_t)r * rowbytes, valid ? rowbytes : 0, 64 * (it % nchunk) + lane);
+    };
+    auto process = [&](const PairRegs &v, int it) {
+        const int chunk = it % nchunk;
+        const int p = 64 * chunk + lane;
+        if (p < npairs) {
             // even block 2p: d = a.x[15:0], qs = bytes 2..17 ; odd block 2p+1: d = b.x[31:16], qs = b.y..c
-            const float dA = h2f(a.x & 0xFFFFu);
-            const float dB = h2f(b.x >> 16);
-            const uint32_t qA0 = __builtin_amdgcn_alignbyte(a.y, a.x, 2);
-            const uint32_t qA1 = __builtin_amdgcn_alignbyte(a.z, a.y, 2);
-            const uint32_t qA2 = __builtin_amdgcn_alignbyte(a.w, a.z, 2);
-            const uint32_t qA3 = __builtin_amdgcn_alignbyte(b.x, a.w, 2);
+            const float dA = h2f(v.a.x & 0xFFFFu);
+            const float dB = h2f(v.b.x >> 16);
+            const uint32_t qA0 = __builtin_amdgcn_alignbyte(v.a.y, v.a.x, 2);
+            const uint32_t qA1 = __builtin_amdgcn_alignbyte(v.a.z, v.a.y, 2);
+            const uint32_t qA2 = __builtin_amdgcn_alignbyte(v.a.w, v.a.z, 2);
+            const uint32_t qA3 = __builtin_amdgcn_alignbyte(v.b.x, v.a.w, 2);
 #pragma unroll
             for (int n = 0; n < NT; n++) {
                 const int bA = n * nb + 2 * p;
-                const int sA = dot_q4_q8(qA0, qA1, qA2, qA3, xq + bA * 8) - xs[bA];
-                const int sB = dot_q4_q8(b.y, b.z, b.w, c, xq + bA * 8 + 8) - xs[bA + 1];
-                acc[n] = fmaf((float)sA, dA * xd[bA], acc[n]);
-                acc[n] = fmaf((float)sB, dB * xd[bA + 1], acc[n]);
+                const float2 dx = *reinterpret_cast<const float2 *>(xd + bA);
+                const int2 sx = *reinterpret_cast<const int2 *>(xs + bA);
+                const int sA = dot_q4_q8(qA0, qA1, qA2, qA3, xq + bA * 8) - sx.x;
+                const int sB = dot_q4_q8(v.b.y, v.b.z, v.b.w, v.c, xq + bA * 8 + 8) - sx.y;
+                acc[n] = fmaf((float)sA, dA * dx.x, acc[n]);
+                acc[n] = fmaf((float)sB, dB * dx.y, acc[n]);
             }
         }
-        float out = 0.0f;
+        if (chunk == nchunk - 1) {                                  // row complete: reduce + store
+            float out = 0.0f;
 #pragma unroll
-        for (int n = 0; n < NT; n++) {
-            float v = acc[n];
-            v += __shfl_xor(v, 32);
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 8);
-            v += __shfl_xor(v, 4);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 1);
-            out = (lane == n) ? v : out;
+            for (int n = 0; n < NT; n++) {
+                float t = acc[n];
+                t += __shfl_xor(t, 32);
+                t += __shfl_xor(t, 16);
+                t += __shfl_xor(t, 8);
+                t += __shfl_xor(t, 4);
+                t += __shfl_xor(t, 2);
+                t += __shfl_xor(t, 1);
+                out = (lane == n) ? t : out;
+                acc[n] = 0.0f;
+            }
+            if (lane < NT) y[(int64_t)lane * ldy + item_row(it)] = out;
         }
-        if (lane < NT) y[(int64_t)lane * ldy + row] = out;
+    };
+    PairRegs nxt;
+    for (int it = 0; it < nitems; it += 2) {
+        nxt = issue(it + 1);
+        process(cur, it);
+        if (it + 1 >= nitems) break;
+        cur = issue(it + 2);
+        process(nxt, it + 1);
     }
 }
 
@@ -321,14 +367,21 @@ int gemv_max_tokens(int64_t K) {
     return nt;
 }
 
+static int g_gemv_wg_per_cu = 0;
+
 template <int NT>
 static hipError_t launch_gemv(const void *W, int64_t K, int64_t M, const float *x, float *y, int64_t ldy,
                               const DeviceInfo &dev, hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     const size_t lds = (size_t)NT * nb * 40;
+    if (g_gemv_wg_per_cu == 0) {
+        const char *e = getenv("GGML_HIP_GEMV_WG_PER_CU");
+        g_gemv_wg_per_cu = e ? atoi(e) : 2;
+        if (g_gemv_wg_per_cu < 1) g_gemv_wg_per_cu = 1;
+    }
     const int64_t need = (M + GEMV_THREADS / 64 - 1) / (GEMV_THREADS / 64);
-    const int64_t cap = (int64_t)dev.num_cus * 2;
+    const int64_t cap = (int64_t)dev.num_cus * g_gemv_wg_per_cu;
     const unsigned grid = (unsigned)(need < cap ? need : cap);
     hipLaunchKernelGGL(k_gemv_q4_0<NT>, dim3(grid), dim3(GEMV_THREADS), lds, s, (const uint8_t *)W, rowbytes, nb,
                        (int)M, x, (int)K, y, ldy);

@@ -98,6 +98,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (launch-per-call)")
+    ap.add_argument("--no-batch-siblings", action="store_true",
+                    help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
     args = ap.parse_args()
 
     rank, world, local, dist = setup_dist(args.gpus)
@@ -135,14 +137,34 @@ def main():
         gh.check(L.ggml_hip_reserve_workspace(K, max(1, args.prefill_tokens)))
     gh.synchronize()
 
+    batch = comm is None and not args.no_batch_siblings
+    # sibling groups that share src1 in the LLaMA graph: (wq, wk, wv) and (w1, w3)
+    groups = [[0, 1, 2], [3], [4, 5], [6]] if batch else [[i] for i in range(len(LAYER))]
+    yb = {i: gh.DeviceBuffer(LAYER[i][2] * 4) for i in range(len(LAYER))}
+    launch_args = []
+    for row in stack.mats:
+        for g in groups:
+            if len(g) == 1 or not batch:
+                launch_args.append(("one", row[g[0]]))
+            else:
+                n = len(g)
+                wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
+                yp = (ctypes.c_void_p * n)(*[yb[i].ptr for i in g])
+                mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
+                launch_args.append(("multi", (n, wp, mp, row[g[0]][1], yp)))
+
     def decode_step():
-        for row in stack.mats:
-            for name, K, M, m_loc, buf, rb in row:
-                if comm is None:
-                    gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, M, xs[K].ptr, 1, ys[M].ptr, M, 0, stream))
-                else:
-                    gh.check(L.ggml_hip_mul_mat_q4_0_split(comm, buf.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
-                                                           xs[K].ptr, 1, ys[M].ptr, stream))
+        for kind, a in launch_args:
+            if kind == "multi":
+                n, wp, mp, K, yp = a
+                gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, 1, yp, stream))
+                continue
+            name, K, M, m_loc, buf, rb = a
+            if comm is None:
+                gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, M, xs[K].ptr, 1, ys[M].ptr, M, 0, stream))
+            else:
+                gh.check(L.ggml_hip_mul_mat_q4_0_split(comm, buf.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
+                                                       xs[K].ptr, 1, ys[M].ptr, stream))
 
     graph = None
     if not args.eager:
@@ -187,7 +209,8 @@ def main():
         "config": {"workload": "LLaMA-7B q4_0 decode, 32 layers x 7 mul_mats (wq,wk,wv,wo 4096x4096; w1,w3 "
                                "4096->11008; w2 11008->4096), N=1, q8_0 quantize of x included, lm_head excluded",
                    "layers": args.layers, "weights_bytes_per_rank": stack.total_bytes,
-                   "graph": graph is not None,
+                   "graph": graph is not None, "launches_per_layer": len(groups),
+                   "sibling_batching": "wq|wk|wv and w1|w3 share src1 -> one launch each" if batch else "off",
                    "parallelism": f"row-split x{world} + RCCL all-gather" if world > 1 else "single GPU"},
     }
 

@@ -119,6 +119,12 @@ int ggml_hip_mul_mat_q4_0(const void *dev_w, int64_t K, int64_t M, const float *
 /* Same with an explicit algorithm: 0 auto, 1 GEMV (N <= 8), 2 MFMA GEMM; and output stride ldy. */
 int ggml_hip_mul_mat_q4_0_ex(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N,
                              float *dev_y, int64_t ldy, int algo, void *stream);
+/* Sibling mul_mats that share the activation x (ggml graphs issue wq/wk/wv and w1/w3 on the same
+ * src1): n <= 4 weight matrices of the same K, y_i = W_i x with y_i f32 [N][M_i].  One launch for
+ * N <= 8 (rows concatenated); for N > 8 x is quantized once and each W_i runs the GEMM.  Results
+ * are identical to n separate ggml_hip_mul_mat_q4_0 calls. */
+int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *M, int64_t K, const float *dev_x,
+                                int64_t N, float *const *dev_y, void *stream);
 /* Ensure the current device's workspace can serve mul_mat for N tokens of K (call before
  * capturing a HIP graph). */
 int ggml_hip_reserve_workspace(int64_t K, int64_t N);

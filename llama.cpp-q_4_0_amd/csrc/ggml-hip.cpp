@@ -542,6 +542,36 @@ int ggml_hip_mul_mat_q4_0_ex(const void *dev_w, int64_t K, int64_t M, const floa
     return mul_mat_dev(dev_w, K, M, dev_x, N, dev_y, ldy, algo, resolve_stream(stream));
 }
 
+int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *M, int64_t K, const float *dev_x,
+                                int64_t N, float *const *dev_y, void *stream) {
+    ensure_init();
+    if (n < 1 || n > ghip::GEMV_MULTI_MAX || !dev_w || !M || !dev_y)
+        return fail(GGML_HIP_ERR_INVALID, "n must be 1..4 with non-null arrays");
+    hipStream_t s = resolve_stream(stream);
+    int64_t total = 0;
+    for (int i = 0; i < n; i++) {
+        if (!dev_w[i] || !dev_y[i] || M[i] <= 0) return fail(GGML_HIP_ERR_INVALID, "null matrix or M <= 0");
+        if (!aligned(dev_w[i], 16) || !aligned(dev_y[i], 4)) return fail(GGML_HIP_ERR_INVALID, "misaligned W or y");
+        total += M[i];
+    }
+    if (N == 0) return GGML_HIP_OK;
+    if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30)) {
+        for (int i = 0; i < n; i++) {       // GEMM path (x re-quantized per matrix: prefill is MFMA-bound)
+            int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 2, s);
+            if (rc != GGML_HIP_OK) return rc;
+        }
+        return GGML_HIP_OK;
+    }
+    // validate the shared shape once through the single-matrix checks
+    if (!dev_x || K <= 0 || K % 64 != 0 || !aligned(dev_x, 16)) return fail(GGML_HIP_ERR_INVALID, "bad x or K");
+    for (int i = 0; i < n; i++)
+        if (M[i] * (K / QK) * Q4B >= ((int64_t)1 << 31)) return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large");
+    int64_t ldy[ghip::GEMV_MULTI_MAX];
+    for (int i = 0; i < n; i++) ldy[i] = M[i];
+    HIP_RET(ghip::gemv_q4_0_multi(n, dev_w, M, K, dev_x, N, dev_y, ldy, g_dev[current_device()].info, s));
+    return GGML_HIP_OK;
+}
+
 int ggml_hip_reserve_workspace(int64_t K, int64_t N) {
     ensure_init();
     if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
@@ -803,6 +833,12 @@ int ggml_hip_graph_destroy(ggml_hip_graph *g) {
 }
 
 const char *ggml_hip_last_error(void) { return g_last_error.c_str(); }
+
+// diagnostic hook (not in the public header): GEMV phase stamps, see q4_0_kernels.hip
+int ggml_hip_debug_gemv_stamps(unsigned long long *host, int n) {
+    HIP_RET(ghip::gemv_read_stamps(host, n));
+    return GGML_HIP_OK;
+}
 
 const char *ggml_hip_version(void) { return "ggml-hip q4_0 gfx950 r1"; }
 

@@ -36,6 +36,14 @@ int gemv_max_tokens(int64_t K);
 hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_t N,
                      float *y, int64_t ldy, const DeviceInfo &dev, hipStream_t s);
 
+// Sibling mul_mats sharing x (e.g. wq/wk/wv): up to 4 matrices of the same K in one launch.
+constexpr int GEMV_MULTI_MAX = 4;
+hipError_t gemv_q4_0_multi(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *x, int64_t N,
+                           float *const *y, const int64_t *ldy, const DeviceInfo &dev, hipStream_t s);
+
+// diagnostic: copy the per-wave phase stamps of the last GGML_HIP_GEMV_DIAG=7 launch
+hipError_t gemv_read_stamps(unsigned long long *host, int n);
+
 // Prefill path: int8 MFMA (v_mfma_i32_32x32x32_i8, K=32 = one q4_0 block) GEMM on the
 // pre-quantized activations xs (quantize_q8_0_soa).
 hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd,

@@ -40,6 +40,9 @@ __device__ __forceinline__ float h2f(uint32_t bits) {
 }
 
 __device__ __forceinline__ uint32_t f2h(float f) {
+    // opaque barrier: keeps hipcc from folding a preceding multiply into v_fma_mix with a +0
+    // addend, which turns -0.0 into +0.0 (ggml stores fp16(-0.0) = 0x8000 for all-zero blocks)
+    asm volatile("" : "+v"(f));
     const _Float16 h = (_Float16)f;        // v_cvt_f16_f32, round-to-nearest-even
     uint16_t b;
     __builtin_memcpy(&b, &h, 2);
@@ -58,23 +61,55 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, RSRC_FLAGS);
 }
 
+// ---- cross-lane reductions on DPP (no LDS round trip) -------------------------------------
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {      // lanes outside ROW_MASK read 0
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_QUAD_XOR1 = 0xB1;     // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;     // quad_perm [2,3,0,1]
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;
+constexpr int DPP_ROW_MIRROR = 0x140;
+constexpr int DPP_ROW_BCAST15 = 0x142;
+constexpr int DPP_ROW_BCAST31 = 0x143;
+
+// max / sum over each group of 8 consecutive lanes (every lane of the group gets the result)
+__device__ __forceinline__ float group8_max(float v) {
+    v = fmaxf(v, dpp_f<DPP_QUAD_XOR1>(v));
+    v = fmaxf(v, dpp_f<DPP_QUAD_XOR2>(v));
+    return fmaxf(v, dpp_f<DPP_ROW_HALF_MIRROR>(v));
+}
+__device__ __forceinline__ int group8_sum(int v) {
+    v += dpp_i<DPP_QUAD_XOR1>(v);
+    v += dpp_i<DPP_QUAD_XOR2>(v);
+    return v + dpp_i<DPP_ROW_HALF_MIRROR>(v);
+}
+// sum over the 64 lanes; the total is valid in lane 63 (fixed order -> deterministic)
+__device__ __forceinline__ float wave_sum_lane63(float v) {
+    v += dpp_f<DPP_QUAD_XOR1>(v);
+    v += dpp_f<DPP_QUAD_XOR2>(v);
+    v += dpp_f<DPP_ROW_HALF_MIRROR>(v);
+    v += dpp_f<DPP_ROW_MIRROR>(v);
+    v += dpp_f<DPP_ROW_BCAST15, 0xA>(v);
+    v += dpp_f<DPP_ROW_BCAST31, 0xC>(v);
+    return v;
+}
+
 // One q8_0 block spread over 8 consecutive lanes, 4 floats each (lane group g = lane>>3).
 // Returns the packed int8x4 of this lane; d16 = fp16(amax/127.f); qsum = sum of the 32 q.
 __device__ __forceinline__ uint32_t q8_block_lane(float4 v, uint32_t &d16, int &qsum) {
     float a = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
-    a = fmaxf(a, __shfl_xor(a, 1));
-    a = fmaxf(a, __shfl_xor(a, 2));
-    a = fmaxf(a, __shfl_xor(a, 4));
+    a = group8_max(a);
     const float d = a / 127.f;                         // correctly rounded (no fast-math)
     const float id = (a != 0.0f) ? 127.f / a : 0.0f;
     d16 = f2h(d);
     const int q0 = q8_round_sat(v.x * id), q1 = q8_round_sat(v.y * id);
     const int q2 = q8_round_sat(v.z * id), q3 = q8_round_sat(v.w * id);
-    int s = q0 + q1 + q2 + q3;
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 4);
-    qsum = s;
+    qsum = group8_sum(q0 + q1 + q2 + q3);
     return (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) | ((uint32_t)(q2 & 0xFF) << 16) |
            ((uint32_t)(q3 & 0xFF) << 24);
 }
@@ -152,9 +187,9 @@ __global__ __launch_bounds__(256) void k_quantize_q4_0(const float *__restrict__
         uint32_t b2 = 0;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
-            // separate rounding of v*id and +8.5 (no FMA contraction), as the C reference
-            int q0 = (int)(signed char)(int)(__fmul_rn(v[j + t], id) + 8.5f);
-            int q1 = (int)(signed char)(int)(__fmul_rn(v[j + t + QK / 2], id) + 8.5f);
+            // separate rounding of v*id and +8.5 (built with -ffp-contract=off), as the C reference
+            int q0 = (int)(signed char)(int)(v[j + t] * id + 8.5f);
+            int q1 = (int)(signed char)(int)(v[j + t + QK / 2] * id + 8.5f);
             q0 = q0 > 15 ? 15 : q0;
             q1 = q1 > 15 ? 15 : q1;
             b2 |= (uint32_t)((q0 & 0xFF) | ((q1 & 0xFF) << 4)) << (8 * t);
@@ -209,9 +244,18 @@ hipError_t dequantize_q4_0(const void *wq, int64_t K, int64_t M, float *w, hipSt
 // the q8_0 prologue overlaps the first HBM round trip; after the prologue each wave walks its
 // (row, chunk) items with the next chunk's loads in flight while the current one computes.
 
-static constexpr int GEMV_THREADS = 1024;
 static constexpr int GEMV_LDS_MAX = 64 * 1024;
+// diagnostic build (GGML_HIP_GEMV_DIAG=7): per-wave s_memrealtime stamps of the phases
+__device__ unsigned long long g_gemv_stamps[8192 * 8];
+#define GEMV_STAMP(slot)                                                                         \
+    do {                                                                                         \
+        if (DIAG == 7 && lane == 0) {                                                            \
+            const int wid_ = blockIdx.x * WAVES + wave;                                          \
+            if (wid_ < 8192) g_gemv_stamps[wid_ * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                        \
+    } while (0)
 static constexpr int GEMV_PRO = 4;          // activation float4 loads in flight per thread
+static constexpr int GEMV_MAXMAT = 4;       // sibling matrices per launch
 
 __device__ __forceinline__ int dot_q4_q8(uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3,
                                          const uint32_t *__restrict__ xb) {
@@ -244,10 +288,19 @@ __device__ __forceinline__ PairRegs load_pair(const uint8_t *row, int64_t rowbyt
     return v;
 }
 
-template <int NT>
-__global__ __launch_bounds__(GEMV_THREADS) void k_gemv_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes,
-                                                             int nb, int M, const float *__restrict__ x, int K,
-                                                             float *__restrict__ y, int64_t ldy) {
+// Up to GEMV_MAXMAT weight matrices that share the activation x ("siblings": wq/wk/wv, w1/w3)
+// run as one launch; their rows are concatenated and each (row, chunk) item looks up its matrix.
+struct GemvMats {
+    const uint8_t *W[GEMV_MAXMAT];
+    float *y[GEMV_MAXMAT];
+    int64_t ldy[GEMV_MAXMAT];
+    int row_begin[GEMV_MAXMAT + 1];       // prefix sums of M; row_begin[n] = total rows
+    int n;
+};
+
+template <int NT, int DIAG, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, int64_t rowbytes, int nb,
+                                                          const float *__restrict__ x, int K) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t *xq = lds;                                             // [NT][nb][8] int8x4
     float *xd = reinterpret_cast<float *>(lds + NT * nb * 8);      // [NT][nb]
@@ -256,13 +309,21 @@ __global__ __launch_bounds__(GEMV_THREADS) void k_gemv_q4_0(const uint8_t *__res
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nwaves = GEMV_THREADS / 64;
+    const int M = mats.row_begin[mats.n];
     const int npairs = nb >> 1;
     const int nchunk = (npairs + 63) >> 6;
-    const int rstride = gridDim.x * nwaves;
-    const int row0 = blockIdx.x * nwaves + wave;
+    const int rstride = gridDim.x * WAVES;
+    const int row0 = blockIdx.x * WAVES + wave;
     const int nrows_w = row0 < M ? (M - 1 - row0) / rstride + 1 : 0;
     const int nitems = nrows_w * nchunk;                            // (row, chunk) items of this wave
+    GEMV_STAMP(0);
+
+    auto row_ptr = [&](int r) {                                     // wave-uniform
+        int mi = 0;
+#pragma unroll
+        for (int i = 1; i < GEMV_MAXMAT; i++) mi += (i < mats.n && r >= mats.row_begin[i]) ? 1 : 0;
+        return mats.W[mi] + (int64_t)(r - mats.row_begin[mi]) * rowbytes;
+    };
 
     // ---- INIT: q8_0 of the NT activation rows into LDS, first weight chunk issued in between.
     // x of the NT tokens is contiguous ([NT][K] f32), so thread t's float4 is at byte 16*t.  All
@@ -287,18 +348,21 @@ __global__ __launch_bounds__(GEMV_THREADS) void k_gemv_q4_0(const uint8_t *__res
     u32x4 xv[GEMV_PRO];
 #pragma unroll
     for (int i = 0; i < GEMV_PRO; i++)
-        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * GEMV_THREADS), 0, 0);
-    PairRegs cur = load_pair(W + (int64_t)(nitems > 0 ? row0 : 0) * rowbytes, nitems > 0 ? rowbytes : 0, lane);
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * (WAVES * 64)), 0, 0);
+    PairRegs cur = load_pair(row_ptr(nitems > 0 ? row0 : 0), nitems > 0 ? rowbytes : 0, lane);
+    GEMV_STAMP(1);
 #pragma unroll
-    for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], tid + i * GEMV_THREADS);
-    for (int base = GEMV_PRO * GEMV_THREADS; base < total; base += GEMV_PRO * GEMV_THREADS) {
+    for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], tid + i * (WAVES * 64));
+    GEMV_STAMP(2);
+    for (int base = GEMV_PRO * (WAVES * 64); base < total; base += GEMV_PRO * (WAVES * 64)) {
 #pragma unroll
         for (int i = 0; i < GEMV_PRO; i++)
-            xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * GEMV_THREADS), 0, 0);
+            xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * (WAVES * 64)), 0, 0);
 #pragma unroll
-        for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], base + tid + i * GEMV_THREADS);
+        for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], base + tid + i * (WAVES * 64));
     }
     __syncthreads();
+    GEMV_STAMP(3);
 
     // ---- COMPUTE: stream the wave's (row, chunk) items with one item in flight.  Two named
     // register sets (no register copies: a copy would force a wait on the in-flight loads).
@@ -309,7 +373,7 @@ __global__ __launch_bounds__(GEMV_THREADS) void k_gemv_q4_0(const uint8_t *__res
     auto issue = [&](int it) {
         const bool valid = it < nitems;                             // past the end: zero-size descriptor
         const int r = valid ? item_row(it) : row0;
-        return load_pair(W + (int64_t)r * rowbytes, valid ? rowbytes : 0, 64 * (it % nchunk) + lane);
+        return load_pair(row_ptr(valid ? r : 0), valid ? rowbytes : 0, 64 * (it % nchunk) + lane);
     };
     auto process = [&](const PairRegs &v, int it) {
         const int chunk = it % nchunk;
@@ -334,30 +398,37 @@ __global__ __launch_bounds__(GEMV_THREADS) void k_gemv_q4_0(const uint8_t *__res
             }
         }
         if (chunk == nchunk - 1) {                                  // row complete: reduce + store
+            const int r = item_row(it);
+            int mi = 0;
+#pragma unroll
+            for (int i = 1; i < GEMV_MAXMAT; i++) mi += (i < mats.n && r >= mats.row_begin[i]) ? 1 : 0;
+            float *yo = mats.y[mi] + (r - mats.row_begin[mi]);
+            const int64_t ld = mats.ldy[mi];
             float out = 0.0f;
 #pragma unroll
             for (int n = 0; n < NT; n++) {
-                float t = acc[n];
-                t += __shfl_xor(t, 32);
-                t += __shfl_xor(t, 16);
-                t += __shfl_xor(t, 8);
-                t += __shfl_xor(t, 4);
-                t += __shfl_xor(t, 2);
-                t += __shfl_xor(t, 1);
-                out = (lane == n) ? t : out;
+                const float t = wave_sum_lane63(acc[n]);
+                const float tn = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 63));
+                out = (lane == n) ? tn : out;
                 acc[n] = 0.0f;
             }
-            if (lane < NT) y[(int64_t)lane * ldy + item_row(it)] = out;
+            if (lane < NT) yo[(int64_t)lane * ld] = out;
         }
     };
     PairRegs nxt;
     for (int it = 0; it < nitems; it += 2) {
         nxt = issue(it + 1);
+        if (it == 0 && DIAG == 7) {                                 // when the first weights have landed
+            asm volatile("" ::"v"(cur.a), "v"(cur.b), "v"(cur.c));
+            GEMV_STAMP(4);
+        }
         process(cur, it);
+        if (it == 0) GEMV_STAMP(5);
         if (it + 1 >= nitems) break;
         cur = issue(it + 2);
         process(nxt, it + 1);
     }
+    GEMV_STAMP(6);
 }
 
 int gemv_max_tokens(int64_t K) {
@@ -367,71 +438,125 @@ int gemv_max_tokens(int64_t K) {
     return nt;
 }
 
-static int g_gemv_wg_per_cu = 0;
+static int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
 
-template <int NT>
-static hipError_t launch_gemv(const void *W, int64_t K, int64_t M, const float *x, float *y, int64_t ldy,
-                              const DeviceInfo &dev, hipStream_t s) {
+template <int NT, int DIAG, int WAVES>
+static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     const size_t lds = (size_t)NT * nb * 40;
-    if (g_gemv_wg_per_cu == 0) {
-        const char *e = getenv("GGML_HIP_GEMV_WG_PER_CU");
-        g_gemv_wg_per_cu = e ? atoi(e) : 2;
-        if (g_gemv_wg_per_cu < 1) g_gemv_wg_per_cu = 1;
-    }
-    const int64_t need = (M + GEMV_THREADS / 64 - 1) / (GEMV_THREADS / 64);
-    const int64_t cap = (int64_t)dev.num_cus * g_gemv_wg_per_cu;
+    static const int wg_per_cu = env_int("GGML_HIP_GEMV_WG_PER_CU", 2048 / (WAVES * 64));
+    const int64_t M = m.row_begin[m.n];
+    const int64_t need = (M + WAVES - 1) / WAVES;
+    const int64_t cap = (int64_t)dev.num_cus * (wg_per_cu < 1 ? 1 : wg_per_cu);
     const unsigned grid = (unsigned)(need < cap ? need : cap);
-    hipLaunchKernelGGL(k_gemv_q4_0<NT>, dim3(grid), dim3(GEMV_THREADS), lds, s, (const uint8_t *)W, rowbytes, nb,
-                       (int)M, x, (int)K, y, ldy);
+    hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES>), dim3(grid), dim3(WAVES * 64), lds, s, m, rowbytes, nb, x,
+                       (int)K);
     return hipGetLastError();
 }
 
-hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_t N, float *y, int64_t ldy,
-                     const DeviceInfo &dev, hipStream_t s) {
+template <int NT>
+static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
+    // GGML_HIP_GEMV_DIAG=7: diagnostic build with per-wave phase stamps (gemv_read_stamps)
+    static const int diag = env_int("GGML_HIP_GEMV_DIAG", 0);
+    static const int waves = env_int("GGML_HIP_GEMV_WAVES", 16);
+    if (NT == 1 && diag == 7) return launch_gemv_w<NT, 7, 16>(m, K, x, dev, s);
+    if (waves == 8) return launch_gemv_w<NT, 0, 8>(m, K, x, dev, s);
+    return launch_gemv_w<NT, 0, 16>(m, K, x, dev, s);
+}
+
+hipError_t gemv_read_stamps(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemv_stamps), sizeof(unsigned long long) * n, 0,
+                               hipMemcpyDeviceToHost);
+}
+
+hipError_t gemv_q4_0_multi(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *x, int64_t N,
+                           float *const *y, const int64_t *ldy, const DeviceInfo &dev, hipStream_t s) {
+    if (nmat < 1 || nmat > GEMV_MAXMAT) return hipErrorInvalidValue;
+    GemvMats m{};
+    m.n = nmat;
+    m.row_begin[0] = 0;
+    for (int i = 0; i < nmat; i++) {
+        m.W[i] = (const uint8_t *)W[i];
+        m.y[i] = y[i];
+        m.ldy[i] = ldy[i];
+        m.row_begin[i + 1] = m.row_begin[i] + (int)M[i];
+    }
+    for (int i = nmat; i < GEMV_MAXMAT; i++) {
+        m.W[i] = m.W[0];
+        m.y[i] = m.y[0];
+        m.ldy[i] = m.ldy[0];
+        m.row_begin[i + 1] = m.row_begin[i];
+    }
     switch (N) {
-        case 1: return launch_gemv<1>(W, K, M, x, y, ldy, dev, s);
-        case 2: return launch_gemv<2>(W, K, M, x, y, ldy, dev, s);
-        case 3: return launch_gemv<3>(W, K, M, x, y, ldy, dev, s);
-        case 4: return launch_gemv<4>(W, K, M, x, y, ldy, dev, s);
-        case 5: return launch_gemv<5>(W, K, M, x, y, ldy, dev, s);
-        case 6: return launch_gemv<6>(W, K, M, x, y, ldy, dev, s);
-        case 7: return launch_gemv<7>(W, K, M, x, y, ldy, dev, s);
-        case 8: return launch_gemv<8>(W, K, M, x, y, ldy, dev, s);
+        case 1: return launch_gemv<1>(m, K, x, dev, s);
+        case 2: return launch_gemv<2>(m, K, x, dev, s);
+        case 3: return launch_gemv<3>(m, K, x, dev, s);
+        case 4: return launch_gemv<4>(m, K, x, dev, s);
+        case 5: return launch_gemv<5>(m, K, x, dev, s);
+        case 6: return launch_gemv<6>(m, K, x, dev, s);
+        case 7: return launch_gemv<7>(m, K, x, dev, s);
+        case 8: return launch_gemv<8>(m, K, x, dev, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// GEMM (prefill): workgroup tile = 128 weight rows x 64 tokens, 4 waves as 2 (rows) x 2 (tokens);
-// each wave owns two 32x32 MFMA tiles (64 rows x 32 tokens).  K advances 4 blocks per stage.
-//
-// MFMA roles: A = activations (token = MFMA row), B = weights (weight row = MFMA column), so
-// D[token][wrow] has the weight row on the lane and the output store y[token][m0 + lane] is a
-// contiguous 128-byte segment per register.  Lane (c, h) = (lane&31, lane>>5) supplies k-half h
-// of its row/column: activations bytes 16h..16h+15 of the q8_0 block, weights the low (h=0) or
-// high (h=1) nibbles of the 16 qs bytes = elements 16h..16h+15.  The i32 result of one MFMA is
-// the exact block sum; the epilogue applies d_x[token]*d_w[row] in fp32.
+hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_t N, float *y, int64_t ldy,
+                     const DeviceInfo &dev, hipStream_t s) {
+    return gemv_q4_0_multi(1, &W, &M, K, x, N, &y, &ldy, dev, s);
+}
 
-static constexpr int GM_BM = 128, GM_BN = 64, GM_KB = 4;
-static constexpr int GM_WSTR = GM_KB * Q4B + 4;     // 76 B: 19 dwords (odd) -> conflict-free b32 reads
-static constexpr int GM_XSTR = GM_KB * QK + 16;     // 144 B: conflict-free ds_read_b128 per 16-lane group
-static constexpr int GM_WDW = GM_KB * Q4B / 4;      // 18 dwords of raw weights per row per stage
+// ---------------------------------------------------------------------------------------------
+// GEMM (prefill): int8 MFMA v_mfma_i32_32x32x32_i8, K = 32 = one q4_0/q8_0 block per MFMA.
+//
+// Workgroup = 4 waves, tile 64 weight rows x 64 tokens, each wave one 32x32 MFMA tile (2x2).
+// K advances GM_KB = 8 blocks (256 values) per stage through a double-buffered LDS ring with
+// one barrier per stage; the next stage's global loads are issued before the current stage's
+// MFMAs and converted/stored after them.
+//
+// Staging converts every weight element once per workgroup: thread t owns (row t/4, block pair
+// t%4) of the stage, loads the pair's 36 raw bytes (dword aligned, as in the GEMV), turns the
+// nibbles into int8 (n-8) and writes [block][row][32 B] + fp32 d_w.  Activations arrive already
+// q8_0-quantized (int8 qs [N][K] + fp32 d_x, from k_quantize_q8_0<false>).  LDS rows are 32 B;
+// the two 16-byte halves of row r are swapped when (r>>3)&1 so that the ds_read_b128 of 32
+// consecutive rows hits 16 distinct bank slots per lane group.
+//
+// MFMA roles: A = activations (token = MFMA row), B = weights (weight row = MFMA column): lane
+// (c, h) = (lane&31, lane>>5) supplies k-half h (elements 16h..16h+15) of token c (A) and of
+// weight row c (B).  D[token][row] has the weight row on the lane, so each output register is
+// a 128-byte contiguous store and d_w is one value per lane.  The i32 MFMA result is the exact
+// block sum; the epilogue applies d_x[token] * d_w[row] in fp32 (fmaf per block).
+
+static constexpr int GM_BM = 64, GM_BN = 64, GM_KB = 8;
+static constexpr int GM_STAGE_W = GM_KB * GM_BM * 32;          // int8 weights  [KB][BM][32]
+static constexpr int GM_STAGE_X = GM_KB * GM_BN * 32;          // int8 acts     [KB][BN][32]
+static constexpr int GM_STAGE_WD = GM_KB * GM_BM * 4;          // f32 d_w       [KB][BM]
+static constexpr int GM_STAGE_XD = GM_KB * GM_BN * 4;          // f32 d_x       [KB][BN]
+static constexpr int GM_STAGE = GM_STAGE_W + GM_STAGE_X + GM_STAGE_WD + GM_STAGE_XD;   // 36 KB
 
 __device__ __forceinline__ uint32_t nib_to_i8x4(uint32_t q, int shift) {
     const uint32_t n = (q >> shift) & 0x0F0F0F0Fu;                 // 0..15 per byte
     return ((n | 0x80808080u) - 0x08080808u) ^ 0x80808080u;      // n - 8 as int8, no cross-byte borrow
 }
 
+__device__ __forceinline__ int gm_half_off(int r, int half) {    // byte offset of a 16-B half in a 32-B row
+    return r * 32 + 16 * (half ^ ((r >> 3) & 1));
+}
+
+struct GmStageRegs {
+    u32x4 wa, wb;
+    uint32_t wc;
+    u32x4 x[4];
+    float xd[2];
+};
+
 __global__ __launch_bounds__(256) void k_gemm_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes, int nb, int M,
                                                    const int8_t *__restrict__ xqs, const float *__restrict__ xd,
                                                    int N, int K, float *__restrict__ y, int64_t ldy) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[GM_BM * GM_WSTR + GM_BN * GM_XSTR + GM_KB * GM_BN * 4];
-    uint8_t *wl = smem;                                    // [BM][WSTR] raw block_q4_0 bytes
-    uint8_t *xl = smem + GM_BM * GM_WSTR;                  // [BN][XSTR] int8 activations
-    float *dl = reinterpret_cast<float *>(xl + GM_BN * GM_XSTR);   // [KB][BN] d_x
-
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -440,118 +565,111 @@ __global__ __launch_bounds__(256) void k_gemm_q4_0(const uint8_t *__restrict__ W
     const int m0 = blockIdx.x * GM_BM;
     const int n0 = blockIdx.y * GM_BN;
 
-    // whole-operand descriptors: out-of-range rows / tokens read as 0
-    const int64_t wbytes = (int64_t)M * rowbytes;
-    const __amdgpu_buffer_rsrc_t wr_rsrc = make_rsrc(W + (int64_t)m0 * rowbytes,
-                                                     (uint32_t)(wbytes - (int64_t)m0 * rowbytes));
-    const __amdgpu_buffer_rsrc_t xr_rsrc = make_rsrc(xqs + (int64_t)n0 * K,
-                                                     (uint32_t)((int64_t)(N - n0) * K));
+    // out-of-range rows / tokens read as 0 through the descriptors' bounds
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W + (int64_t)m0 * rowbytes, (uint32_t)((int64_t)(M - m0) * rowbytes));
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)(N - n0) * K));
 
-    // staging registers (prefetch of stage s+1 while stage s computes)
-    uint32_t wreg[9];
-    u32x4 xreg[2];
-    float dreg;
+    // staging roles: weights (row sr, block pair sp), activations (token t, 16-byte part)
+    const int sr = tid >> 2, sp = tid & 3;
 
-    auto load_stage = [&](int kb0) {
+    auto load_stage = [&](int kb0, GmStageRegs &g) {
+        const int woff = (int)(sr * rowbytes) + (kb0 + 2 * sp) * Q4B;
+        g.wa = __builtin_amdgcn_raw_buffer_load_b128(wrs, woff, 0, 0);
+        g.wb = __builtin_amdgcn_raw_buffer_load_b128(wrs, woff + 16, 0, 0);
+        g.wc = __builtin_amdgcn_raw_buffer_load_b32(wrs, woff + 32, 0, 0);
 #pragma unroll
-        for (int i = 0; i < 9; i++) {
-            const int idx = tid + 256 * i;                 // 0 .. 128*18-1
-            const int r = idx / GM_WDW, dw = idx - r * GM_WDW;
-            wreg[i] = __builtin_amdgcn_raw_buffer_load_b32(wr_rsrc, (int)(r * rowbytes + kb0 * Q4B + 4 * dw), 0, 0);
+        for (int i = 0; i < 4; i++) {
+            const int idx = tid + 256 * i;                 // 0 .. 64 tokens * 16 parts
+            const int t = idx >> 4, part = idx & 15;
+            g.x[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, t * K + kb0 * QK + 16 * part, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < 2; i++) {
-            const int idx = tid + 256 * i;                 // 0 .. 64*8-1
-            const int t = idx >> 3, part = idx & 7;
-            xreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, t * K + kb0 * QK + 16 * part, 0, 0);
-        }
-        {
-            const int b = tid >> 6, t = tid & 63;          // KB*BN == 256
-            dreg = (n0 + t < N && kb0 + b < nb) ? xd[(int64_t)(n0 + t) * nb + kb0 + b] : 0.0f;
+            const int idx = tid + 256 * i;                 // 0 .. KB * BN
+            const int b = idx >> 6, t = idx & 63;
+            g.xd[i] = (n0 + t < N && kb0 + b < nb) ? xd[(int64_t)(n0 + t) * nb + kb0 + b] : 0.0f;
         }
     };
-    auto store_stage = [&]() {
+    auto store_stage = [&](int kb0, const GmStageRegs &g, uint8_t *st) {
+        uint8_t *ws = st;
+        uint8_t *xs = st + GM_STAGE_W;
+        float *wds = reinterpret_cast<float *>(st + GM_STAGE_W + GM_STAGE_X);
+        float *xds = reinterpret_cast<float *>(st + GM_STAGE_W + GM_STAGE_X + GM_STAGE_WD);
+        // weights: block 2sp (d = wa.x[15:0], qs = bytes 2..17) and 2sp+1 (d = wb.x[31:16], qs = wb.y..wc)
+        const bool vA = kb0 + 2 * sp < nb, vB = kb0 + 2 * sp + 1 < nb;
+        const uint32_t qa[4] = {__builtin_amdgcn_alignbyte(g.wa.y, g.wa.x, 2), __builtin_amdgcn_alignbyte(g.wa.z, g.wa.y, 2),
+                                __builtin_amdgcn_alignbyte(g.wa.w, g.wa.z, 2), __builtin_amdgcn_alignbyte(g.wb.x, g.wa.w, 2)};
+        const uint32_t qb[4] = {g.wb.y, g.wb.z, g.wb.w, g.wc};
 #pragma unroll
-        for (int i = 0; i < 9; i++) {
+        for (int half = 0; half < 2; half++) {
+            u32x4 ta, tb;
+            ta.x = nib_to_i8x4(qa[0], 4 * half); ta.y = nib_to_i8x4(qa[1], 4 * half);
+            ta.z = nib_to_i8x4(qa[2], 4 * half); ta.w = nib_to_i8x4(qa[3], 4 * half);
+            tb.x = nib_to_i8x4(qb[0], 4 * half); tb.y = nib_to_i8x4(qb[1], 4 * half);
+            tb.z = nib_to_i8x4(qb[2], 4 * half); tb.w = nib_to_i8x4(qb[3], 4 * half);
+            *reinterpret_cast<u32x4 *>(ws + (2 * sp) * GM_BM * 32 + gm_half_off(sr, half)) = ta;
+            *reinterpret_cast<u32x4 *>(ws + (2 * sp + 1) * GM_BM * 32 + gm_half_off(sr, half)) = tb;
+        }
+        wds[(2 * sp) * GM_BM + sr] = vA ? h2f(g.wa.x & 0xFFFFu) : 0.0f;
+        wds[(2 * sp + 1) * GM_BM + sr] = vB ? h2f(g.wb.x >> 16) : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
             const int idx = tid + 256 * i;
-            const int r = idx / GM_WDW, dw = idx - r * GM_WDW;
-            *reinterpret_cast<uint32_t *>(wl + r * GM_WSTR + 4 * dw) = wreg[i];
+            const int t = idx >> 4, part = idx & 15;       // part: block part >> 1, half part & 1
+            *reinterpret_cast<u32x4 *>(xs + (part >> 1) * GM_BN * 32 + gm_half_off(t, part & 1)) = g.x[i];
         }
 #pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const int idx = tid + 256 * i;
-            const int t = idx >> 3, part = idx & 7;
-            *reinterpret_cast<u32x4 *>(xl + t * GM_XSTR + 16 * part) = xreg[i];
-        }
-        dl[tid] = dreg;
+        for (int i = 0; i < 2; i++) xds[tid + 256 * i] = g.xd[i];
     };
 
-    float acc[2][16];
+    float acc[16];
 #pragma unroll
-    for (int ct = 0; ct < 2; ct++)
-#pragma unroll
-        for (int i = 0; i < 16; i++) acc[ct][i] = 0.0f;
+    for (int i = 0; i < 16; i++) acc[i] = 0.0f;
 
-    load_stage(0);
-    for (int kb0 = 0; kb0 < nb; kb0 += GM_KB) {
-        __syncthreads();                                   // previous stage's LDS reads done
-        store_stage();
-        __syncthreads();
-        if (kb0 + GM_KB < nb) load_stage(kb0 + GM_KB);     // in flight during this stage's MFMAs
+    GmStageRegs g;
+    load_stage(0, g);
+    store_stage(0, g, smem);
+    __syncthreads();
+    const int nstages = (nb + GM_KB - 1) / GM_KB;
+    const int tok = 32 * wt + c;             // A row (token) of this lane
+    const int wrow = 32 * wr + c;            // B column (weight row) of this lane
+    for (int s = 0; s < nstages; s++) {
+        uint8_t *st = smem + (s & 1) * GM_STAGE;
+        const int kb0 = s * GM_KB;
+        const bool more = s + 1 < nstages;
+        if (more) load_stage(kb0 + GM_KB, g);            // in flight during this stage's MFMAs
+        const uint8_t *ws = st;
+        const uint8_t *xs = st + GM_STAGE_W;
+        const float *wds = reinterpret_cast<const float *>(st + GM_STAGE_W + GM_STAGE_X);
+        const float *xds = reinterpret_cast<const float *>(st + GM_STAGE_W + GM_STAGE_X + GM_STAGE_WD);
 #pragma unroll
         for (int b = 0; b < GM_KB; b++) {
             if (kb0 + b >= nb) break;
-            const int tok = 32 * wt + c;
-            const u32x4 af = *reinterpret_cast<const u32x4 *>(xl + tok * GM_XSTR + 32 * b + 16 * h);
-            // d_x of the 16 tokens this lane's accumulator registers hold: 8q + 4h + {0..3}
+            const i32x4 af = *reinterpret_cast<const i32x4 *>(xs + b * GM_BN * 32 + gm_half_off(tok, h));
+            const i32x4 bf = *reinterpret_cast<const i32x4 *>(ws + b * GM_BM * 32 + gm_half_off(wrow, h));
+            const float dw = wds[b * GM_BM + wrow];
             float dx[16];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const float4 f = *reinterpret_cast<const float4 *>(dl + b * GM_BN + 32 * wt + 8 * q + 4 * h);
+                const float4 f = *reinterpret_cast<const float4 *>(xds + b * GM_BN + 32 * wt + 8 * q + 4 * h);
                 dx[4 * q] = f.x; dx[4 * q + 1] = f.y; dx[4 * q + 2] = f.z; dx[4 * q + 3] = f.w;
             }
+            const i32x16 cz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            const i32x16 cv = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, bf, cz, 0, 0, 0);
 #pragma unroll
-            for (int ct = 0; ct < 2; ct++) {
-                const int wrow = 64 * wr + 32 * ct + c;
-                const uint32_t *wp = reinterpret_cast<const uint32_t *>(wl + wrow * GM_WSTR);
-                uint32_t q0, q1, q2, q3, dbits;
-                if ((b & 1) == 0) {                        // block starts dword aligned: d | qs0 qs1
-                    const int o = (9 * b) / 2;
-                    const uint32_t d0 = wp[o], d1 = wp[o + 1], d2 = wp[o + 2], d3 = wp[o + 3], d4 = wp[o + 4];
-                    dbits = d0 & 0xFFFFu;
-                    q0 = __builtin_amdgcn_alignbyte(d1, d0, 2);
-                    q1 = __builtin_amdgcn_alignbyte(d2, d1, 2);
-                    q2 = __builtin_amdgcn_alignbyte(d3, d2, 2);
-                    q3 = __builtin_amdgcn_alignbyte(d4, d3, 2);
-                } else {                                   // d in the upper half of the previous dword
-                    const int o = (9 * b + 1) / 2;
-                    dbits = wp[o - 1] >> 16;
-                    q0 = wp[o]; q1 = wp[o + 1]; q2 = wp[o + 2]; q3 = wp[o + 3];
-                }
-                const int sh = 4 * h;
-                i32x4 bf;
-                bf.x = (int)nib_to_i8x4(q0, sh);
-                bf.y = (int)nib_to_i8x4(q1, sh);
-                bf.z = (int)nib_to_i8x4(q2, sh);
-                bf.w = (int)nib_to_i8x4(q3, sh);
-                i32x16 cz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-                const i32x16 cv = __builtin_amdgcn_mfma_i32_32x32x32_i8((i32x4)af, bf, cz, 0, 0, 0);
-                const float dw = h2f(dbits);
-#pragma unroll
-                for (int i = 0; i < 16; i++) acc[ct][i] = fmaf((float)cv[i], dw * dx[i], acc[ct][i]);
-            }
+            for (int i = 0; i < 16; i++) acc[i] = fmaf((float)cv[i], dw * dx[i], acc[i]);
         }
+        if (more) store_stage(kb0 + GM_KB, g, smem + ((s + 1) & 1) * GM_STAGE);
+        __syncthreads();
     }
 
-    // epilogue: acc[ct][i] = y[token(i)][row]; token(i) = 32wt + (i&3) + 8(i>>2) + 4h
-#pragma unroll
-    for (int ct = 0; ct < 2; ct++) {
-        const int row = m0 + 64 * wr + 32 * ct + c;
-        if (row >= M) continue;
+    // epilogue: acc[i] = y[token(i)][row]; token(i) = 32wt + (i&3) + 8(i>>2) + 4h
+    const int row = m0 + wrow;
+    if (row < M) {
 #pragma unroll
         for (int i = 0; i < 16; i++) {
-            const int tok = n0 + 32 * wt + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (tok < N) y[(int64_t)tok * ldy + row] = acc[ct][i];
+            const int t = n0 + 32 * wt + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (t < N) y[(int64_t)t * ldy + row] = acc[i];
         }
     }
 }
@@ -561,8 +679,15 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     dim3 grid((unsigned)((M + GM_BM - 1) / GM_BM), (unsigned)((N + GM_BN - 1) / GM_BN));
-    hipLaunchKernelGGL(k_gemm_q4_0, grid, dim3(256), 0, s, (const uint8_t *)W, rowbytes, nb, (int)M, xqs, xd,
-                       (int)N, (int)K, y, ldy);
+    static bool attr_set = false;       // > 64 KB of dynamic LDS (gfx950 has 160 KB per CU)
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_gemm_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           2 * GM_STAGE);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_gemm_q4_0, grid, dim3(256), 2 * GM_STAGE, s, (const uint8_t *)W, rowbytes, nb, (int)M, xqs,
+                       xd, (int)N, (int)K, y, ldy);
     return hipGetLastError();
 }
 

@@ -55,6 +55,7 @@ def _bind(L):
         "ggml_hip_mul_mat_q4_0": ([vp, i64, i64, vp, i64, vp, vp], i32),
         "ggml_hip_mul_mat_q4_0_ex": ([vp, i64, i64, vp, i64, vp, i64, i32, vp], i32),
         "ggml_hip_reserve_workspace": ([i64, i64], i32),
+        "ggml_hip_mul_mat_q4_0_multi": ([i32, vp, vp, i64, vp, i64, vp, vp], i32),
         "ggml_hip_comm_unique_id": ([vp], i32),
         "ggml_hip_comm_init": ([vp, i32, i32, vp], i32),
         "ggml_hip_comm_destroy": ([vp], i32),
@@ -187,6 +188,16 @@ def mul_mat(w_dev, K, M, x_dev, N, y_dev, algo=0, ldy=None, stream=None, w_off=0
     yp = y_dev if isinstance(y_dev, int) else y_dev.ptr
     check(load().ggml_hip_mul_mat_q4_0_ex(wp + w_off, K, M, xp + x_off, N, yp + y_off, M if ldy is None else ldy,
                                           algo, stream), "mul_mat_q4_0")
+
+
+def mul_mat_multi(ws, Ms, K, x_dev, N, ys, stream=None):
+    """Sibling mul_mats sharing x: ws / ys are DeviceBuffers (or raw pointers)."""
+    n = len(ws)
+    wp = (ctypes.c_void_p * n)(*[w if isinstance(w, int) else w.ptr for w in ws])
+    yp = (ctypes.c_void_p * n)(*[y if isinstance(y, int) else y.ptr for y in ys])
+    mp = (ctypes.c_int64 * n)(*Ms)
+    xp = x_dev if isinstance(x_dev, int) else x_dev.ptr
+    check(load().ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xp, N, yp, stream), "mul_mat_q4_0_multi")
 
 
 def synchronize():

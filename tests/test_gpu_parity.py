@@ -164,6 +164,23 @@ def test_gemv_and_gemm_agree(N):
     check_y(y1, y2, s_abs, RTOL, ATOL_BLOCKS)
 
 
+@pytest.mark.parametrize("N", [1, 3, 8, 20])
+def test_multi_matrix_siblings_match_single_calls(N):
+    """wq|wk|wv-style sibling batch (shared x, different M) == separate calls, bitwise."""
+    K = 4096
+    Ms = [256, 128, 300]
+    cases = [make_case(K, M, N, seed=40 + i) for i, M in enumerate(Ms)]
+    x = cases[0][1]
+    wds = [DB.from_array(c[0]) for c in cases]
+    xd = DB.from_array(x)
+    ys = [DB(N * M * 4) for M in Ms]
+    ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
+    for (wq, _), yd, M, wd in zip(cases, ys, Ms, wds):
+        got = yd.download((N, M), np.float32)
+        single, _ = gpu_mul_mat(wq, K, x)
+        assert np.array_equal(got.view(np.uint32), single.view(np.uint32))
+
+
 def test_ldy_stride_and_no_out_of_bounds_writes():
     wq, x = make_case(4096, 100, 3, seed=5)
     for algo in (1, 2):

@@ -789,9 +789,14 @@ int ggml_hip_event_record(void *event, void *stream) {
 }
 
 float ggml_hip_event_elapsed_ms(void *start, void *stop) {
-    if (hipEventSynchronize((hipEvent_t)stop) != hipSuccess) return -1.0f;
     float ms = -1.0f;
-    if (hipEventElapsedTime(&ms, (hipEvent_t)start, (hipEvent_t)stop) != hipSuccess) return -1.0f;
+    hipError_t e = hipEventSynchronize((hipEvent_t)stop);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, (hipEvent_t)start, (hipEvent_t)stop);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();      // do not leave a sticky error for the next launch check
+        g_last_error = std::string("hipEventElapsedTime: ") + hipGetErrorString(e);
+        return -1.0f;
+    }
     return ms;
 }
 

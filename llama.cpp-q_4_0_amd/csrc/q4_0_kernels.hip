@@ -145,6 +145,7 @@ hipError_t quantize_q8_0_aos(const float *x, int64_t K, int64_t N, void *xq8, hi
     const int64_t total8 = N * (K / QK) * 8;
     if (total8 == 0) return hipSuccess;
     const int64_t grid = (total8 + 255) / 256;
+    (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL(k_quantize_q8_0<true>, dim3((unsigned)grid), dim3(256), 0, s, x, K, total8,
                        (uint8_t *)xq8, (int8_t *)nullptr, (float *)nullptr);
     return hipGetLastError();
@@ -154,6 +155,7 @@ hipError_t quantize_q8_0_soa(const float *x, int64_t K, int64_t N, int8_t *qs, f
     const int64_t total8 = N * (K / QK) * 8;
     if (total8 == 0) return hipSuccess;
     const int64_t grid = (total8 + 255) / 256;
+    (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL(k_quantize_q8_0<false>, dim3((unsigned)grid), dim3(256), 0, s, x, K, total8,
                        (uint8_t *)nullptr, qs, d);
     return hipGetLastError();
@@ -201,6 +203,7 @@ __global__ __launch_bounds__(256) void k_quantize_q4_0(const float *__restrict__
 hipError_t quantize_q4_0(const float *w, int64_t K, int64_t M, void *wq, hipStream_t s) {
     const int64_t nblocks = M * (K / QK);
     if (nblocks == 0) return hipSuccess;
+    (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL(k_quantize_q4_0, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, s, w, nblocks,
                        (uint8_t *)wq);
     return hipGetLastError();
@@ -223,6 +226,7 @@ __global__ __launch_bounds__(256) void k_dequantize_q4_0(const uint8_t *__restri
 hipError_t dequantize_q4_0(const void *wq, int64_t K, int64_t M, float *w, hipStream_t s) {
     const int64_t nblocks = M * (K / QK);
     if (nblocks == 0) return hipSuccess;
+    (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL(k_dequantize_q4_0, dim3((unsigned)((nblocks * 16 + 255) / 256)), dim3(256), 0, s,
                        (const uint8_t *)wq, nblocks, w);
     return hipGetLastError();
@@ -453,6 +457,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     const int64_t need = (M + WAVES - 1) / WAVES;
     const int64_t cap = (int64_t)dev.num_cus * (wg_per_cu < 1 ? 1 : wg_per_cu);
     const unsigned grid = (unsigned)(need < cap ? need : cap);
+    (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES>), dim3(grid), dim3(WAVES * 64), lds, s, m, rowbytes, nb, x,
                        (int)K);
     return hipGetLastError();
@@ -512,16 +517,17 @@ hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_
 // ---------------------------------------------------------------------------------------------
 // GEMM (prefill): int8 MFMA v_mfma_i32_32x32x32_i8, K = 32 = one q4_0/q8_0 block per MFMA.
 //
-// Workgroup = 4 waves, tile 64 weight rows x 64 tokens, each wave one 32x32 MFMA tile (2x2).
-// K advances GM_KB = 8 blocks (256 values) per stage through a double-buffered LDS ring with
-// one barrier per stage; the next stage's global loads are issued before the current stage's
-// MFMAs and converted/stored after them.
+// Workgroup = 8 waves, tile 64 weight rows x 128 tokens; wave (wr, wt) in 2 x 4 owns one 32x32
+// MFMA tile.  K advances GM_KB = 4 blocks (128 values) per stage through a double-buffered LDS
+// ring with one barrier per stage.  Global loads run TWO stages ahead in two named register
+// sets (HBM latency under load is ~2 us, longer than one stage of MFMAs); two workgroups per
+// CU (16 waves) cover the rest.
 //
-// Staging converts every weight element once per workgroup: thread t owns (row t/4, block pair
-// t%4) of the stage, loads the pair's 36 raw bytes (dword aligned, as in the GEMV), turns the
-// nibbles into int8 (n-8) and writes [block][row][32 B] + fp32 d_w.  Activations arrive already
-// q8_0-quantized (int8 qs [N][K] + fp32 d_x, from k_quantize_q8_0<false>).  LDS rows are 32 B;
-// the two 16-byte halves of row r are swapped when (r>>3)&1 so that the ds_read_b128 of 32
+// Staging converts every weight element once per workgroup: thread t < 128 owns (row t/2,
+// block pair t%2) of the stage, loads the pair's 36 raw bytes (dword aligned, as in the GEMV),
+// turns the nibbles into int8 (n-8) and writes [block][row][32 B] + fp32 d_w.  Activations arrive
+// already q8_0-quantized (int8 qs [N][K] + fp32 d_x, from k_quantize_q8_0<false>).  LDS rows are
+// 32 B; the two 16-byte halves of row r are swapped when (r>>3)&1 so that the ds_read_b128 of 32
 // consecutive rows hits 16 distinct bank slots per lane group.
 //
 // MFMA roles: A = activations (token = MFMA row), B = weights (weight row = MFMA column): lane
@@ -530,12 +536,15 @@ hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_
 // a 128-byte contiguous store and d_w is one value per lane.  The i32 MFMA result is the exact
 // block sum; the epilogue applies d_x[token] * d_w[row] in fp32 (fmaf per block).
 
-static constexpr int GM_BM = 64, GM_BN = 64, GM_KB = 8;
+static constexpr int GM_BM = 64, GM_BN = 128, GM_KB = 4, GM_WAVES = 8, GM_THREADS = GM_WAVES * 64;
 static constexpr int GM_STAGE_W = GM_KB * GM_BM * 32;          // int8 weights  [KB][BM][32]
 static constexpr int GM_STAGE_X = GM_KB * GM_BN * 32;          // int8 acts     [KB][BN][32]
 static constexpr int GM_STAGE_WD = GM_KB * GM_BM * 4;          // f32 d_w       [KB][BM]
 static constexpr int GM_STAGE_XD = GM_KB * GM_BN * 4;          // f32 d_x       [KB][BN]
-static constexpr int GM_STAGE = GM_STAGE_W + GM_STAGE_X + GM_STAGE_WD + GM_STAGE_XD;   // 36 KB
+static constexpr int GM_STAGE = GM_STAGE_W + GM_STAGE_X + GM_STAGE_WD + GM_STAGE_XD;   // 27 KB
+static_assert(GM_BM * GM_KB / 2 <= GM_THREADS, "one weight block pair per staging thread");
+static_assert(GM_BN * GM_KB * 2 == 2 * GM_THREADS, "two 16-byte activation pieces per thread");
+static_assert(GM_BN * GM_KB == GM_THREADS, "one d_x per thread");
 
 __device__ __forceinline__ uint32_t nib_to_i8x4(uint32_t q, int shift) {
     const uint32_t n = (q >> shift) & 0x0F0F0F0Fu;                 // 0..15 per byte
@@ -549,18 +558,20 @@ __device__ __forceinline__ int gm_half_off(int r, int half) {    // byte offset 
 struct GmStageRegs {
     u32x4 wa, wb;
     uint32_t wc;
-    u32x4 x[4];
-    float xd[2];
+    u32x4 x[2];
+    float xd;
 };
 
-__global__ __launch_bounds__(256) void k_gemm_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes, int nb, int M,
-                                                   const int8_t *__restrict__ xqs, const float *__restrict__ xd,
-                                                   int N, int K, float *__restrict__ y, int64_t ldy) {
+template <int DIAG>
+__global__ __launch_bounds__(GM_THREADS, 2) void k_gemm_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes,
+                                                              int nb, int M, const int8_t *__restrict__ xqs,
+                                                              const float *__restrict__ xd, int N, int K,
+                                                              float *__restrict__ y, int64_t ldy) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int wr = wave & 1, wt = wave >> 1;
+    const int wr = wave & 1, wt = wave >> 1;                        // 2 row waves x 4 token waves
     const int c = lane & 31, h = lane >> 5;
     const int m0 = blockIdx.x * GM_BM;
     const int n0 = blockIdx.y * GM_BN;
@@ -568,76 +579,77 @@ __global__ __launch_bounds__(256) void k_gemm_q4_0(const uint8_t *__restrict__ W
     // out-of-range rows / tokens read as 0 through the descriptors' bounds
     const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W + (int64_t)m0 * rowbytes, (uint32_t)((int64_t)(M - m0) * rowbytes));
     const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)(N - n0) * K));
+    const __amdgpu_buffer_rsrc_t nul = make_rsrc(W, 0);
 
-    // staging roles: weights (row sr, block pair sp), activations (token t, 16-byte part)
-    const int sr = tid >> 2, sp = tid & 3;
+    // staging roles: weights (row sr, block pair sp) for tid < 128; activations (token, piece)
+    const bool wstager = tid < GM_BM * GM_KB / 2;
+    const int sr = (tid >> 1) & (GM_BM - 1), sp = tid & 1;
 
     auto load_stage = [&](int kb0, GmStageRegs &g) {
+        const bool valid = kb0 < nb && (DIAG != 3 || kb0 == 0);   // past the last stage: no traffic
+        const __amdgpu_buffer_rsrc_t wr_ = (valid && wstager) ? wrs : nul;
         const int woff = (int)(sr * rowbytes) + (kb0 + 2 * sp) * Q4B;
-        g.wa = __builtin_amdgcn_raw_buffer_load_b128(wrs, woff, 0, 0);
-        g.wb = __builtin_amdgcn_raw_buffer_load_b128(wrs, woff + 16, 0, 0);
-        g.wc = __builtin_amdgcn_raw_buffer_load_b32(wrs, woff + 32, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int idx = tid + 256 * i;                 // 0 .. 64 tokens * 16 parts
-            const int t = idx >> 4, part = idx & 15;
-            g.x[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, t * K + kb0 * QK + 16 * part, 0, 0);
-        }
+        g.wa = __builtin_amdgcn_raw_buffer_load_b128(wr_, woff, 0, 0);
+        g.wb = __builtin_amdgcn_raw_buffer_load_b128(wr_, woff + 16, 0, 0);
+        g.wc = __builtin_amdgcn_raw_buffer_load_b32(wr_, woff + 32, 0, 0);
+        const __amdgpu_buffer_rsrc_t xr_ = valid ? xrs : nul;
 #pragma unroll
         for (int i = 0; i < 2; i++) {
-            const int idx = tid + 256 * i;                 // 0 .. KB * BN
-            const int b = idx >> 6, t = idx & 63;
-            g.xd[i] = (n0 + t < N && kb0 + b < nb) ? xd[(int64_t)(n0 + t) * nb + kb0 + b] : 0.0f;
+            const int idx = tid + GM_THREADS * i;          // 0 .. 128 tokens * 8 pieces
+            const int t = idx >> 3, piece = idx & 7;       // piece: block piece>>1, half piece&1
+            g.x[i] = __builtin_amdgcn_raw_buffer_load_b128(xr_, t * K + kb0 * QK + 16 * piece, 0, 0);
+        }
+        {
+            const int b = tid >> 7, t = tid & 127;         // KB * BN == threads
+            g.xd = (valid && n0 + t < N && kb0 + b < nb) ? xd[(int64_t)(n0 + t) * nb + kb0 + b] : 0.0f;
         }
     };
     auto store_stage = [&](int kb0, const GmStageRegs &g, uint8_t *st) {
+        if (DIAG == 4 && kb0 > 0) {                        // diagnostic: keep the loads live, skip LDS
+            asm volatile("" ::"v"(g.wa), "v"(g.wb), "v"(g.wc), "v"(g.x[0]), "v"(g.x[1]), "v"(g.xd));
+            return;
+        }
         uint8_t *ws = st;
         uint8_t *xs = st + GM_STAGE_W;
         float *wds = reinterpret_cast<float *>(st + GM_STAGE_W + GM_STAGE_X);
         float *xds = reinterpret_cast<float *>(st + GM_STAGE_W + GM_STAGE_X + GM_STAGE_WD);
-        // weights: block 2sp (d = wa.x[15:0], qs = bytes 2..17) and 2sp+1 (d = wb.x[31:16], qs = wb.y..wc)
-        const bool vA = kb0 + 2 * sp < nb, vB = kb0 + 2 * sp + 1 < nb;
-        const uint32_t qa[4] = {__builtin_amdgcn_alignbyte(g.wa.y, g.wa.x, 2), __builtin_amdgcn_alignbyte(g.wa.z, g.wa.y, 2),
-                                __builtin_amdgcn_alignbyte(g.wa.w, g.wa.z, 2), __builtin_amdgcn_alignbyte(g.wb.x, g.wa.w, 2)};
-        const uint32_t qb[4] = {g.wb.y, g.wb.z, g.wb.w, g.wc};
+        if (wstager) {
+            // block 2sp (d = wa.x[15:0], qs = bytes 2..17) and 2sp+1 (d = wb.x[31:16], qs = wb.y..wc)
+            const bool vA = kb0 + 2 * sp < nb, vB = kb0 + 2 * sp + 1 < nb;
+            const uint32_t qa[4] = {__builtin_amdgcn_alignbyte(g.wa.y, g.wa.x, 2),
+                                    __builtin_amdgcn_alignbyte(g.wa.z, g.wa.y, 2),
+                                    __builtin_amdgcn_alignbyte(g.wa.w, g.wa.z, 2),
+                                    __builtin_amdgcn_alignbyte(g.wb.x, g.wa.w, 2)};
+            const uint32_t qb[4] = {g.wb.y, g.wb.z, g.wb.w, g.wc};
 #pragma unroll
-        for (int half = 0; half < 2; half++) {
-            u32x4 ta, tb;
-            ta.x = nib_to_i8x4(qa[0], 4 * half); ta.y = nib_to_i8x4(qa[1], 4 * half);
-            ta.z = nib_to_i8x4(qa[2], 4 * half); ta.w = nib_to_i8x4(qa[3], 4 * half);
-            tb.x = nib_to_i8x4(qb[0], 4 * half); tb.y = nib_to_i8x4(qb[1], 4 * half);
-            tb.z = nib_to_i8x4(qb[2], 4 * half); tb.w = nib_to_i8x4(qb[3], 4 * half);
-            *reinterpret_cast<u32x4 *>(ws + (2 * sp) * GM_BM * 32 + gm_half_off(sr, half)) = ta;
-            *reinterpret_cast<u32x4 *>(ws + (2 * sp + 1) * GM_BM * 32 + gm_half_off(sr, half)) = tb;
-        }
-        wds[(2 * sp) * GM_BM + sr] = vA ? h2f(g.wa.x & 0xFFFFu) : 0.0f;
-        wds[(2 * sp + 1) * GM_BM + sr] = vB ? h2f(g.wb.x >> 16) : 0.0f;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int idx = tid + 256 * i;
-            const int t = idx >> 4, part = idx & 15;       // part: block part >> 1, half part & 1
-            *reinterpret_cast<u32x4 *>(xs + (part >> 1) * GM_BN * 32 + gm_half_off(t, part & 1)) = g.x[i];
+            for (int half = 0; half < 2; half++) {
+                u32x4 ta, tb;
+                ta.x = nib_to_i8x4(qa[0], 4 * half); ta.y = nib_to_i8x4(qa[1], 4 * half);
+                ta.z = nib_to_i8x4(qa[2], 4 * half); ta.w = nib_to_i8x4(qa[3], 4 * half);
+                tb.x = nib_to_i8x4(qb[0], 4 * half); tb.y = nib_to_i8x4(qb[1], 4 * half);
+                tb.z = nib_to_i8x4(qb[2], 4 * half); tb.w = nib_to_i8x4(qb[3], 4 * half);
+                *reinterpret_cast<u32x4 *>(ws + (2 * sp) * GM_BM * 32 + gm_half_off(sr, half)) = ta;
+                *reinterpret_cast<u32x4 *>(ws + (2 * sp + 1) * GM_BM * 32 + gm_half_off(sr, half)) = tb;
+            }
+            wds[(2 * sp) * GM_BM + sr] = vA ? h2f(g.wa.x & 0xFFFFu) : 0.0f;
+            wds[(2 * sp + 1) * GM_BM + sr] = vB ? h2f(g.wb.x >> 16) : 0.0f;
         }
 #pragma unroll
-        for (int i = 0; i < 2; i++) xds[tid + 256 * i] = g.xd[i];
+        for (int i = 0; i < 2; i++) {
+            const int idx = tid + GM_THREADS * i;
+            const int t = idx >> 3, piece = idx & 7;
+            *reinterpret_cast<u32x4 *>(xs + (piece >> 1) * GM_BN * 32 + gm_half_off(t, piece & 1)) = g.x[i];
+        }
+        xds[tid] = g.xd;
     };
 
     float acc[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) acc[i] = 0.0f;
-
-    GmStageRegs g;
-    load_stage(0, g);
-    store_stage(0, g, smem);
-    __syncthreads();
-    const int nstages = (nb + GM_KB - 1) / GM_KB;
     const int tok = 32 * wt + c;             // A row (token) of this lane
     const int wrow = 32 * wr + c;            // B column (weight row) of this lane
-    for (int s = 0; s < nstages; s++) {
-        uint8_t *st = smem + (s & 1) * GM_STAGE;
-        const int kb0 = s * GM_KB;
-        const bool more = s + 1 < nstages;
-        if (more) load_stage(kb0 + GM_KB, g);            // in flight during this stage's MFMAs
+
+    auto compute_stage = [&](int kb0, const uint8_t *st) {
         const uint8_t *ws = st;
         const uint8_t *xs = st + GM_STAGE_W;
         const float *wds = reinterpret_cast<const float *>(st + GM_STAGE_W + GM_STAGE_X);
@@ -655,11 +667,43 @@ __global__ __launch_bounds__(256) void k_gemm_q4_0(const uint8_t *__restrict__ W
                 dx[4 * q] = f.x; dx[4 * q + 1] = f.y; dx[4 * q + 2] = f.z; dx[4 * q + 3] = f.w;
             }
             const i32x16 cz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-            const i32x16 cv = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, bf, cz, 0, 0, 0);
+            i32x16 cv;
+            if (DIAG == 2) {                                // diagnostic: no MFMA
+                cv = cz;
+                cv[0] = af.x ^ bf.y;
+            } else {
+                cv = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, bf, cz, 0, 0, 0);
+            }
+            if (DIAG == 1) {                                // diagnostic: integer epilogue only
 #pragma unroll
-            for (int i = 0; i < 16; i++) acc[i] = fmaf((float)cv[i], dw * dx[i], acc[i]);
+                for (int i = 0; i < 16; i++) acc[i] = __int_as_float(__float_as_int(acc[i]) + cv[i]);
+                asm volatile("" ::"v"(dw), "v"(dx[0]), "v"(dx[15]));
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; i++) acc[i] = fmaf((float)cv[i], dw * dx[i], acc[i]);
+            }
         }
-        if (more) store_stage(kb0 + GM_KB, g, smem + ((s + 1) & 1) * GM_STAGE);
+    };
+
+    // ring: LDS buffers 0/1 alternate per stage; register sets gA/gB hold stages s+1 / s+2
+    const int nstages = (nb + GM_KB - 1) / GM_KB;
+    GmStageRegs gA, gB;
+    load_stage(0, gA);
+    load_stage(GM_KB, gB);
+    store_stage(0, gA, smem);
+    __syncthreads();
+    for (int s = 0; s < nstages; s += 2) {
+        // even stage s in LDS buffer 0, gB holds stage s+1
+        load_stage((s + 2) * GM_KB, gA);
+        compute_stage(s * GM_KB, smem);
+        if (s + 1 >= nstages) break;
+        store_stage((s + 1) * GM_KB, gB, smem + GM_STAGE);
+        __syncthreads();
+        // odd stage s+1 in LDS buffer 1, gA holds stage s+2
+        load_stage((s + 3) * GM_KB, gB);
+        compute_stage((s + 1) * GM_KB, smem + GM_STAGE);
+        if (s + 2 >= nstages) break;
+        store_stage((s + 2) * GM_KB, gA, smem);
         __syncthreads();
     }
 
@@ -679,15 +723,23 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     dim3 grid((unsigned)((M + GM_BM - 1) / GM_BM), (unsigned)((N + GM_BN - 1) / GM_BN));
-    static bool attr_set = false;       // > 64 KB of dynamic LDS (gfx950 has 160 KB per CU)
+    // GGML_HIP_GEMM_DIAG (diagnostic builds): 1 integer epilogue, 2 no MFMA, 3 no global loads,
+    // 4 no LDS staging
+    static const int diag = env_int("GGML_HIP_GEMM_DIAG", 0);
+    auto kern = diag == 1 ? k_gemm_q4_0<1> : diag == 2 ? k_gemm_q4_0<2> : diag == 3 ? k_gemm_q4_0<3>
+              : diag == 4 ? k_gemm_q4_0<4> : k_gemm_q4_0<0>;
+    static bool attr_set = false;       // up to 2 x 27 KB of dynamic LDS
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_gemm_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           2 * GM_STAGE);
-        if (e != hipSuccess) return e;
+        for (auto k : {k_gemm_q4_0<0>, k_gemm_q4_0<1>, k_gemm_q4_0<2>, k_gemm_q4_0<3>, k_gemm_q4_0<4>}) {
+            hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * GM_STAGE);
+            if (e != hipSuccess) return e;
+        }
         attr_set = true;
     }
-    hipLaunchKernelGGL(k_gemm_q4_0, grid, dim3(256), 2 * GM_STAGE, s, (const uint8_t *)W, rowbytes, nb, (int)M, xqs,
-                       xd, (int)N, (int)K, y, ldy);
+    (void)hipGetLastError();  // report only this launch's error
+    hipLaunchKernelGGL(kern, grid, dim3(GM_THREADS), 2 * GM_STAGE, s, (const uint8_t *)W, rowbytes, nb,
+                       (int)M, xqs, xd, (int)N, (int)K, y, ldy);
     return hipGetLastError();
 }
 
@@ -711,6 +763,7 @@ hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const
                          float *y, int64_t ldy, hipStream_t s) {
     const int64_t total = (int64_t)nranks * N * max_rows;
     if (total == 0) return hipSuccess;
+    (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL(k_scatter_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, slabs, nranks,
                        max_rows, row_begin_dev, N, y, ldy);
     return hipGetLastError();
@@ -743,6 +796,7 @@ __global__ __launch_bounds__(256) void k_fill_gaussian(float *__restrict__ dst, 
 hipError_t fill_gaussian(float *dst, int64_t n, uint64_t seed, float mean, float stdv, hipStream_t s) {
     const int64_t pairs = (n + 1) / 2;
     if (pairs == 0) return hipSuccess;
+    (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL(k_fill_gaussian, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, dst, n, seed, mean,
                        stdv);
     return hipGetLastError();

@@ -98,6 +98,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (launch-per-call)")
+    ap.add_argument("--force-split", action="store_true",
+                    help="run the multi-GPU code path (row split + RCCL all-gather) even with one rank")
     ap.add_argument("--no-batch-siblings", action="store_true",
                     help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
     args = ap.parse_args()
@@ -112,13 +114,14 @@ def main():
     stream = L.ggml_hip_default_stream()
 
     comm = None
-    if world > 1:
+    if world > 1 or args.force_split:
         uid = ctypes.create_string_buffer(128)
         if rank == 0:
             gh.check(L.ggml_hip_comm_unique_id(uid))
-        obj = [uid.raw if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = ctypes.create_string_buffer(obj[0], 128)
+        if dist is not None:
+            obj = [uid.raw if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = ctypes.create_string_buffer(obj[0], 128)
         comm = ctypes.c_void_p()
         gh.check(L.ggml_hip_comm_init(ctypes.byref(comm), world, rank, uid), "comm_init")
 
@@ -204,7 +207,7 @@ def main():
     result = {
         "metric": METRIC, "value": round(tok_s, 2), "unit": "tok/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "q4_0 x q8_0 (int8 dot, f32 acc)",
+        "scaling": "strong", "vs_baseline": None, "dtype": "q4_0 x q8_0 (int8 dot, f32 acc)",
         "data": "synthetic: W ~ N(0,0.02) -> q4_0 (ggml A3 rule, on device), x ~ N(0,1); random-init, no checkpoint",
         "config": {"workload": "LLaMA-7B q4_0 decode, 32 layers x 7 mul_mats (wq,wk,wv,wo 4096x4096; w1,w3 "
                                "4096->11008; w2 11008->4096), N=1, q8_0 quantize of x included, lm_head excluded",
@@ -214,7 +217,7 @@ def main():
                    "parallelism": f"row-split x{world} + RCCL all-gather" if world > 1 else "single GPU"},
     }
 
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and comm is None:
         result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
         if not args.no_prefill and args.prefill_tokens > 0:
             result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens)
@@ -267,9 +270,18 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
         tot_t += t * len(sel)
         nlaunch += len(sel)
     achieved = tot_bytes / tot_t / 1e9
+    traffic, src = None, None
+    pmc = os.path.join(ROOT, "profiles", "r01_gemv_pmc_traffic.json")
+    if os.path.exists(pmc):          # measured by tools/pmc_traffic.sh (rocprofv3 --pmc passes)
+        try:
+            traffic = round(json.load(open(pmc))["traffic_bytes_per_launch_mean"])
+            src = "profiles/r01_gemv_pmc_traffic.json: 2*FETCH_SIZE+WRITE_SIZE (x1024) per GEMV launch, mean"
+        except Exception:
+            traffic = None
     return {"bound": "hbm", "kernel": "k_gemv_q4_0<1,0,16> (fused q8_0 quantize + q4_0.q8_0 GEMV)",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": src,
+            "algorithmic_bytes_per_launch_mean": round(tot_bytes / nlaunch),
             "avg_launch_us": round(tot_t / nlaunch * 1e6, 3), "per_shape": shapes,
             "timing": "HIP events around graph replays of each launch position's 32 back-to-back launches",
             "bytes_per_launch_def": "sum over the launch's matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y)"}

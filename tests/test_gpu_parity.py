@@ -303,3 +303,28 @@ def test_graph_capture_replays_gemv():
     y = yd.download((1, M), np.float32, stream=s)
     _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
     check_y(y, O.mul_mat(wq, K, x), s_abs, RTOL, ATOL_BLOCKS)
+
+
+# ------------------------------------------------------------------------------- RCCL split path (1 rank)
+@pytest.mark.parametrize("N", [1, 3, 12])
+def test_split_path_single_rank_rccl(N):
+    """ggml_hip_mul_mat_q4_0_split through a real 1-rank RCCL communicator: the in-place
+    all-gather (N=1) and the padded-slab + compaction path (N>1) equal the plain mul_mat."""
+    L = ggml_hip.load()
+    uid = ctypes.create_string_buffer(128)
+    ggml_hip.check(L.ggml_hip_comm_unique_id(uid))
+    comm = ctypes.c_void_p()
+    ggml_hip.check(L.ggml_hip_comm_init(ctypes.byref(comm), 1, 0, uid), "comm_init")
+    try:
+        K, M = 4096, 320
+        wq, x = make_case(K, M, N, seed=77 + N)
+        wd, xd, yd = DB.from_array(wq), DB.from_array(x), DB(N * M * 4)
+        rb = np.array([0, M], np.int64)
+        ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split(comm, wd.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
+                                                     xd.ptr, N, yd.ptr, None), "split")
+        ggml_hip.check(L.ggml_hip_stream_synchronize(None))
+        y = yd.download((N, M), np.float32)
+        single, _ = gpu_mul_mat(wq, K, x)
+        assert np.array_equal(y.view(np.uint32), single.view(np.uint32))
+    finally:
+        L.ggml_hip_comm_destroy(comm)

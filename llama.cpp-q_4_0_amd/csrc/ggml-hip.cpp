@@ -845,6 +845,11 @@ int ggml_hip_debug_gemv_stamps(unsigned long long *host, int n) {
     return GGML_HIP_OK;
 }
 
+int ggml_hip_debug_gemm_stamps(unsigned long long *host, int n) {
+    HIP_RET(ghip::gemm_read_stamps(host, n));
+    return GGML_HIP_OK;
+}
+
 const char *ggml_hip_version(void) { return "ggml-hip q4_0 gfx950 r1"; }
 
 }  // extern "C"

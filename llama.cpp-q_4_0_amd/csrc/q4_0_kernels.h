@@ -43,6 +43,7 @@ hipError_t gemv_q4_0_multi(int nmat, const void *const *W, const int64_t *M, int
 
 // diagnostic: copy the per-wave phase stamps of the last GGML_HIP_GEMV_DIAG=7 launch
 hipError_t gemv_read_stamps(unsigned long long *host, int n);
+hipError_t gemm_read_stamps(unsigned long long *host, int n);
 
 // Prefill path: int8 MFMA (v_mfma_i32_32x32x32_i8, K=32 = one q4_0 block) GEMM on the
 // pre-quantized activations xs (quantize_q8_0_soa).

@@ -555,6 +555,8 @@ __device__ __forceinline__ int gm_half_off(int r, int half) {    // byte offset 
     return r * 32 + 16 * (half ^ ((r >> 3) & 1));
 }
 
+__device__ unsigned long long g_gemm_stamps[16384 * 4];
+
 struct GmStageRegs {
     u32x4 wa, wb;
     uint32_t wc;
@@ -582,7 +584,9 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm_q4_0(const uint8_t *__re
     const __amdgpu_buffer_rsrc_t nul = make_rsrc(W, 0);
 
     // staging roles: weights (row sr, block pair sp) for tid < 128; activations (token, piece)
-    const bool wstager = tid < GM_BM * GM_KB / 2;
+    // wave-uniform (readfirstlane): a per-lane descriptor choice makes hipcc wrap every buffer
+    // load in a waterfall loop
+    const bool wstager = __builtin_amdgcn_readfirstlane(tid >> 6) < (GM_BM * GM_KB / 2) / 64;
     const int sr = (tid >> 1) & (GM_BM - 1), sp = tid & 1;
 
     auto load_stage = [&](int kb0, GmStageRegs &g) {
@@ -686,25 +690,58 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm_q4_0(const uint8_t *__re
     };
 
     // ring: LDS buffers 0/1 alternate per stage; register sets gA/gB hold stages s+1 / s+2
+    // (DIAG 5: per-wave s_memtime sums of compute / staging / barrier segments)
+    unsigned long long t_c = 0, t_s = 0, t_b = 0, t_mark = 0, t_begin = 0;
+    auto mark = [&](unsigned long long &acc_t) {
+        if (DIAG == 5) {
+            __builtin_amdgcn_sched_barrier(0);
+            unsigned long long t;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            acc_t += t - t_mark;
+            t_mark = t;
+        }
+    };
+    if (DIAG == 5) {
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_mark)::"memory");
+        t_begin = t_mark;
+    }
     const int nstages = (nb + GM_KB - 1) / GM_KB;
     GmStageRegs gA, gB;
     load_stage(0, gA);
     load_stage(GM_KB, gB);
     store_stage(0, gA, smem);
+    mark(t_s);
     __syncthreads();
+    mark(t_b);
     for (int s = 0; s < nstages; s += 2) {
         // even stage s in LDS buffer 0, gB holds stage s+1
         load_stage((s + 2) * GM_KB, gA);
         compute_stage(s * GM_KB, smem);
+        mark(t_c);
         if (s + 1 >= nstages) break;
         store_stage((s + 1) * GM_KB, gB, smem + GM_STAGE);
+        mark(t_s);
         __syncthreads();
+        mark(t_b);
         // odd stage s+1 in LDS buffer 1, gA holds stage s+2
         load_stage((s + 3) * GM_KB, gB);
         compute_stage((s + 1) * GM_KB, smem + GM_STAGE);
+        mark(t_c);
         if (s + 2 >= nstages) break;
         store_stage((s + 2) * GM_KB, gA, smem);
+        mark(t_s);
         __syncthreads();
+        mark(t_b);
+    }
+    if (DIAG == 5 && lane == 0) {
+        const int wid = (blockIdx.y * gridDim.x + blockIdx.x) * GM_WAVES + wave;
+        if (wid < 16384) {
+            g_gemm_stamps[wid * 4 + 0] = t_mark - t_begin;
+            g_gemm_stamps[wid * 4 + 1] = t_c;
+            g_gemm_stamps[wid * 4 + 2] = t_s;
+            g_gemm_stamps[wid * 4 + 3] = t_b;
+        }
     }
 
     // epilogue: acc[i] = y[token(i)][row]; token(i) = 32wt + (i&3) + 8(i>>2) + 4h
@@ -727,10 +764,11 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
     // 4 no LDS staging
     static const int diag = env_int("GGML_HIP_GEMM_DIAG", 0);
     auto kern = diag == 1 ? k_gemm_q4_0<1> : diag == 2 ? k_gemm_q4_0<2> : diag == 3 ? k_gemm_q4_0<3>
-              : diag == 4 ? k_gemm_q4_0<4> : k_gemm_q4_0<0>;
+              : diag == 4 ? k_gemm_q4_0<4> : diag == 5 ? k_gemm_q4_0<5> : k_gemm_q4_0<0>;
     static bool attr_set = false;       // up to 2 x 27 KB of dynamic LDS
     if (!attr_set) {
-        for (auto k : {k_gemm_q4_0<0>, k_gemm_q4_0<1>, k_gemm_q4_0<2>, k_gemm_q4_0<3>, k_gemm_q4_0<4>}) {
+        for (auto k : {k_gemm_q4_0<0>, k_gemm_q4_0<1>, k_gemm_q4_0<2>, k_gemm_q4_0<3>, k_gemm_q4_0<4>,
+                       k_gemm_q4_0<5>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * GM_STAGE);
             if (e != hipSuccess) return e;
@@ -800,6 +838,11 @@ hipError_t fill_gaussian(float *dst, int64_t n, uint64_t seed, float mean, float
     hipLaunchKernelGGL(k_fill_gaussian, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, dst, n, seed, mean,
                        stdv);
     return hipGetLastError();
+}
+
+hipError_t gemm_read_stamps(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), sizeof(unsigned long long) * n, 0,
+                               hipMemcpyDeviceToHost);
 }
 
 }  // namespace ghip

@@ -15,7 +15,7 @@ import sys
 import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "libggml_hip.so")
+LIB_PATH = os.environ.get("GGML_HIP_LIB") or os.path.join(PKG, "libggml_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "ggml-hip.h")
 
 OK = 0

@@ -320,45 +320,74 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3):
             "stack_7B_prefill_ms": round(t / layers * 32 * 1e3, 3)}
 
 
-def cpu_baseline(budget_s):
-    """The oracle's AVX2 restatement of ggml.c's q4_0 mul_mat (quantize_row_q8_0 AVX2 branch +
-    ggml_vec_dot_q4_0_q8_0 AVX2 + row-split threads spawned per call like ggml_graph_compute),
-    timed on this host.  Sample: decode tokens over a rotating set of whole LLaMA-7B layers
-    (> LLC), tok/s = 1 / (32 x layer time)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    nthreads = int(os.environ.get("CPU_BASELINE_THREADS", min(16, os.cpu_count() or 1)))
-    base = []
-    for mi, (name, K, M) in enumerate(LAYER):
-        wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED0000 + mi, 0.0, 0.02).reshape(M, K))
-        base.append((K, wq))
-    n_copies = 6                                   # ~680 MB of weights: beyond any host LLC
-    layers = [[(K, wq.copy()) for K, wq in base] for _ in range(n_copies)]
-    x = {K: O.gaussian(K, 0x5EED1000 + K, 0.0, 1.0).reshape(1, K) for K in (4096, 11008)}
-    O.mul_mat(base[0][1], 4096, x[4096], nthreads=nthreads)   # warm
-    t0 = time.perf_counter()
-    n_layers_run = 0
-    while True:
-        for K, wq in layers[n_layers_run % n_copies]:
-            O.mul_mat(wq, K, x[K], nthreads=nthreads, mode="avx2", pool=False)
-        n_layers_run += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    t = (time.perf_counter() - t0) / n_layers_run
+def _cpu_name():
     import platform
     cpu = platform.processor() or "x86_64"
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": round(1.0 / (32 * t), 3), "unit": "tok/s", "cores": nthreads, "kind": "port",
-            "sample": f"{n_layers_run} LLaMA-7B decode layers (7 q4_0 GEMVs each, N=1) over {n_copies} rotating "
-                      f"layer copies, {nthreads} threads spawned per mul_mat, AVX2={bool(O.lib().oracle_have_avx2())}, "
-                      f"{budget_s:.0f}s budget; tok/s = 1/(32 x mean layer time)",
-            "ms_per_layer": round(t * 1e3, 3), "cpu": cpu}
+    return cpu
+
+
+def cpu_baseline(budget_s):
+    """CPU path timed beside the GPU path on this host, decode tokens over a rotating set of whole
+    LLaMA-7B layers (> LLC), tok/s = 1 / (32 x layer time).
+
+    kind "reference": the reference's own ggml.c (oracle/_ref, compiled from /root/reference by
+    oracle/Makefile, AVX2/FMA/F16C branches) driven through ggml_mul_mat + ggml_graph_compute per
+    matmul (oracle/ref_bench.c).  kind "port" (only when oracle/_ref was not built): the oracle's
+    AVX2 restatement with the same row split and per-call thread spawn."""
+    nthreads = int(os.environ.get("CPU_BASELINE_THREADS", min(16, os.cpu_count() or 1)))
+    n_copies = 6                                   # ~680 MB of weights: beyond any host LLC
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_bench.so")
+    if os.path.exists(ref_so) and os.environ.get("CPU_BASELINE_KIND", "reference") == "reference":
+        import ctypes
+        R = ctypes.CDLL(ref_so)
+        R.ref_layers_create.restype = ctypes.c_void_p
+        R.ref_layers_create.argtypes = [ctypes.c_int, ctypes.c_int]
+        R.ref_layer_run.restype = ctypes.c_double
+        R.ref_layer_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        R.ref_layers_destroy.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        h = R.ref_layers_create(n_copies, 1)
+        R.ref_layer_run(h, 0, nthreads)            # warm
+        total, n_layers_run = 0.0, 0
+        while total < budget_s:
+            total += R.ref_layer_run(h, n_layers_run % n_copies, nthreads)
+            n_layers_run += 1
+        R.ref_layers_destroy(h, n_copies)
+        t = total / n_layers_run
+        kind = "reference"
+        what = ("reference ggml.c (oracle/_ref, -march=x86-64-v3) ggml_mul_mat + ggml_graph_compute per "
+                f"matmul, n_threads={nthreads}")
+    else:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        base = []
+        for mi, (name, K, M) in enumerate(LAYER):
+            wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED0000 + mi, 0.0, 0.02).reshape(M, K))
+            base.append((K, wq))
+        layers = [[(K, wq.copy()) for K, wq in base] for _ in range(n_copies)]
+        x = {K: O.gaussian(K, 0x5EED1000 + K, 0.0, 1.0).reshape(1, K) for K in (4096, 11008)}
+        O.mul_mat(base[0][1], 4096, x[4096], nthreads=nthreads)   # warm
+        t0 = time.perf_counter()
+        n_layers_run = 0
+        while True:
+            for K, wq in layers[n_layers_run % n_copies]:
+                O.mul_mat(wq, K, x[K], nthreads=nthreads, mode="avx2", pool=False)
+            n_layers_run += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        t = (time.perf_counter() - t0) / n_layers_run
+        kind = "port"
+        what = (f"oracle AVX2 restatement, {nthreads} threads spawned per mul_mat, "
+                f"AVX2={bool(O.lib().oracle_have_avx2())}")
+    return {"value": round(1.0 / (32 * t), 3), "unit": "tok/s", "cores": nthreads, "kind": kind,
+            "sample": f"{n_layers_run} LLaMA-7B decode layers (7 q4_0 mul_mats each, N=1) over {n_copies} "
+                      f"rotating layer copies; {what}; {budget_s:.0f}s budget; tok/s = 1/(32 x mean layer time)",
+            "ms_per_layer": round(t * 1e3, 3), "cpu": _cpu_name()}
 
 
 if __name__ == "__main__":

@@ -262,9 +262,7 @@ static constexpr int GEMV_PRO = 4;          // activation float4 loads in flight
 static constexpr int GEMV_MAXMAT = 4;       // sibling matrices per launch
 
 __device__ __forceinline__ int dot_q4_q8(uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3,
-                                         const uint32_t *__restrict__ xb) {
-    const u32x4 xl = *reinterpret_cast<const u32x4 *>(xb);      // elems 0..15
-    const u32x4 xh = *reinterpret_cast<const u32x4 *>(xb + 4);  // elems 16..31
+                                         const u32x4 xl /* elems 0..15 */, const u32x4 xh /* 16..31 */) {
     const uint32_t m = 0x0F0F0F0Fu;
     int s = 0;
     s = __builtin_amdgcn_sdot4((int)(q0 & m), (int)xl.x, s, false);
@@ -292,41 +290,73 @@ __device__ __forceinline__ PairRegs load_pair(const uint8_t *row, int64_t rowbyt
     return v;
 }
 
+// Global-load form: lanes past the row's last pair (and whole past-the-end items) clamp to one
+// address, so they add no traffic; no descriptor setup per item.
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+__device__ __forceinline__ PairRegs load_pair_g(const uint8_t *p36) {
+    PairRegs v;                                     // global_load (not flat: no lgkmcnt coupling)
+    v.a = *(g_u32x4 *)(p36);
+    v.b = *(g_u32x4 *)(p36 + 16);
+    v.c = *(g_u32 *)(p36 + 32);
+    return v;
+}
+
 // Up to GEMV_MAXMAT weight matrices that share the activation x ("siblings": wq/wk/wv, w1/w3)
 // run as one launch; their rows are concatenated and each (row, chunk) item looks up its matrix.
 struct GemvMats {
     const uint8_t *W[GEMV_MAXMAT];
     float *y[GEMV_MAXMAT];
     int64_t ldy[GEMV_MAXMAT];
-    int row_begin[GEMV_MAXMAT + 1];       // prefix sums of M; row_begin[n] = total rows
+    int row_begin[GEMV_MAXMAT + 1];       // prefix sums of M; unused entries = total rows
     int n;
+    int M;                                // total rows (= row_begin[n])
+    int rstride;                          // rows between a wave's consecutive rows = grid * WAVES
 };
+// Every field is read with a constant index: the kernel's kernargs arrive in one batch of scalar
+// loads and the per-row matrix lookup is a chain of s_cselect, not a dependent kernarg load.
 
-template <int NT, int DIAG, int WAVES>
+// VAR bit 0 (GLB): weight loads are plain global loads with clamped lane addresses
+// VAR bit 1 (XSPLIT): only the first XW waves load and quantize x; the other waves issue their
+//                     weight loads at once (the x loads enter the CU's queue first)
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, int64_t rowbytes, int nb,
                                                           const float *__restrict__ x, int K) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t *xq = lds;                                             // [NT][nb][8] int8x4
+    // xq: per token, chunk-major [4][npairs] x 16 B: chunk j = (block & 1) * 2 + word / 4 of pair
+    // p = block / 2, so lane p's four ds_read_b128 are lane-contiguous (no bank conflicts)
+    uint32_t *xq = lds;                                             // [NT][4][npairs][4] int8x4
     float *xd = reinterpret_cast<float *>(lds + NT * nb * 8);      // [NT][nb]
     int *xs = reinterpret_cast<int *>(xd + NT * nb);               // [NT][nb] 8*sum(q)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int M = mats.row_begin[mats.n];
+    // kernargs into scalar locals; the per-row matrix choice is written as sums of deltas
+    // selected by (row >= row_begin[i]) so that it compiles to s_cselect (a ternary chain over
+    // four values is turned into a lookup table in scratch by the optimizer)
+    const int M = mats.M;
+    const int rb1 = mats.row_begin[1], rb2 = mats.row_begin[2], rb3 = mats.row_begin[3];
+    const uint64_t w0 = (uint64_t)mats.W[0], wd1 = (uint64_t)mats.W[1] - (uint64_t)mats.W[0],
+                   wd2 = (uint64_t)mats.W[2] - (uint64_t)mats.W[1], wd3 = (uint64_t)mats.W[3] - (uint64_t)mats.W[2];
+    const uint64_t y0 = (uint64_t)mats.y[0], yd1 = (uint64_t)mats.y[1] - (uint64_t)mats.y[0],
+                   yd2 = (uint64_t)mats.y[2] - (uint64_t)mats.y[1], yd3 = (uint64_t)mats.y[3] - (uint64_t)mats.y[2];
+    const int64_t l0 = mats.ldy[0], ld1 = mats.ldy[1] - mats.ldy[0], ld2 = mats.ldy[2] - mats.ldy[1],
+                  ld3 = mats.ldy[3] - mats.ldy[2];
     const int npairs = nb >> 1;
     const int nchunk = (npairs + 63) >> 6;
-    const int rstride = gridDim.x * WAVES;
+    const int rstride = mats.rstride;
     const int row0 = blockIdx.x * WAVES + wave;
     const int nrows_w = row0 < M ? (M - 1 - row0) / rstride + 1 : 0;
     const int nitems = nrows_w * nchunk;                            // (row, chunk) items of this wave
     GEMV_STAMP(0);
 
-    auto row_ptr = [&](int r) {                                     // wave-uniform
-        int mi = 0;
-#pragma unroll
-        for (int i = 1; i < GEMV_MAXMAT; i++) mi += (i < mats.n && r >= mats.row_begin[i]) ? 1 : 0;
-        return mats.W[mi] + (int64_t)(r - mats.row_begin[mi]) * rowbytes;
+    static_assert(GEMV_MAXMAT == 4, "matrix selection below is written for 4 siblings");
+    auto row_ptr = [&](int r) __attribute__((always_inline)) {     // wave-uniform
+        const bool g1 = r >= rb1, g2 = r >= rb2, g3 = r >= rb3;
+        const uint64_t w = w0 + (g1 ? wd1 : 0) + (g2 ? wd2 : 0) + (g3 ? wd3 : 0);
+        const int rb = (g1 ? rb1 : 0) + (g2 ? rb2 - rb1 : 0) + (g3 ? rb3 - rb2 : 0);
+        return reinterpret_cast<const uint8_t *>(w) + (int64_t)(r - rb) * rowbytes;
     };
 
     // ---- INIT: q8_0 of the NT activation rows into LDS, first weight chunk issued in between.
@@ -335,37 +365,87 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     // count vmcnt exactly: the q8_0 math waits for the activations only, not the weights.
     const int total = NT * nb * 8;
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, (uint32_t)total * 16u);
-    auto quantize_into_lds = [&](const u32x4 &raw, int t) {
+    auto quantize_into_lds = [&](const u32x4 &raw, int t) __attribute__((always_inline)) {
         if (t < total) {                                            // whole 8-lane groups agree
             const float4 v = make_float4(__uint_as_float(raw.x), __uint_as_float(raw.y),
                                          __uint_as_float(raw.z), __uint_as_float(raw.w));
             uint32_t d16;
             int qsum;
             const uint32_t packed = q8_block_lane(v, d16, qsum);
-            xq[t] = packed;
+            {
+                const int n = t / (nb * 8), tw = t - n * (nb * 8);  // token, word within token
+                const int b = tw >> 3, w = tw & 7;
+                xq[n * nb * 8 + ((((b & 1) << 1) | (w >> 2)) * (nb >> 1) + (b >> 1)) * 4 + (w & 3)] = packed;
+            }
             if ((t & 7) == 0) {
                 xd[t >> 3] = h2f(d16);
                 xs[t >> 3] = 8 * qsum;
             }
         }
     };
+    auto item_row = [&](int it) __attribute__((always_inline)) { return row0 + (it / nchunk) * rstride; };
+    constexpr bool GLB = (VAR & 1) != 0, XSPLIT = (VAR & 2) != 0;
+    auto issue = [&](int it) __attribute__((always_inline)) {
+        const bool valid = it < nitems;                             // past the end: zero-size descriptor
+        const int r = valid ? item_row(it) : row0;
+        if constexpr (GLB) {                                        // past the end: one shared address
+            const int pp = 64 * (it % nchunk) + lane;
+            const int pc = valid ? (pp < npairs ? pp : npairs - 1) : 0;
+            return load_pair_g(row_ptr(valid ? r : 0) + 36 * pc);
+        } else {
+            return load_pair(row_ptr(valid ? r : 0), valid ? rowbytes : 0, 64 * (it % nchunk) + lane);
+        }
+    };
+    constexpr bool KO_X = DIAG == 8 || DIAG == 10;      // timing knockouts (results invalid)
+    constexpr bool KO_LDS = DIAG == 9 || DIAG == 10;
     u32x4 xv[GEMV_PRO];
+    PairRegs buf[DEPTH];
+    if constexpr (XSPLIT) {
+        // x-waves: wave < XW load + quantize x (XT threads, PRO float4 each per round), then issue
+        // their weight loads; the other waves only issue weight loads
+        const int XW0 = (total + 64 * GEMV_PRO - 1) / (64 * GEMV_PRO);
+        const int XW = XW0 < WAVES ? XW0 : WAVES;
+        const int XT = XW * 64;
+        if (wave < XW) {
+            for (int base = 0; base < total; base += GEMV_PRO * XT) {
+#pragma unroll
+                for (int i = 0; i < GEMV_PRO; i++)
+                    xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * XT), 0, 0);
+#pragma unroll
+                for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], base + tid + i * XT);
+            }
+            asm volatile("" ::: "memory");                          // weight loads stay behind x
+#pragma unroll
+            for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+        } else {
+#pragma unroll
+            for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+        }
+        GEMV_STAMP(1);
+        GEMV_STAMP(2);
+    } else {
 #pragma unroll
     for (int i = 0; i < GEMV_PRO; i++)
-        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * (WAVES * 64)), 0, 0);
-    PairRegs cur = load_pair(row_ptr(nitems > 0 ? row0 : 0), nitems > 0 ? rowbytes : 0, lane);
+        xv[i] = KO_X ? u32x4{0, 0, 0, 0} : __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * (WAVES * 64)), 0, 0);
+    // the wave's first DEPTH items are in flight across the prologue (a ring of named register
+    // sets, never copied: a copy would force a wait on the loads still in flight)
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
     GEMV_STAMP(1);
+    if (!KO_X) {
 #pragma unroll
     for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], tid + i * (WAVES * 64));
+    }
     GEMV_STAMP(2);
-    for (int base = GEMV_PRO * (WAVES * 64); base < total; base += GEMV_PRO * (WAVES * 64)) {
+    for (int base = GEMV_PRO * (WAVES * 64); !KO_X && base < total; base += GEMV_PRO * (WAVES * 64)) {
 #pragma unroll
         for (int i = 0; i < GEMV_PRO; i++)
             xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * (WAVES * 64)), 0, 0);
 #pragma unroll
         for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], base + tid + i * (WAVES * 64));
     }
-    __syncthreads();
+    }
+    if (!KO_X) __syncthreads();
     GEMV_STAMP(3);
 
     // ---- COMPUTE: stream the wave's (row, chunk) items with one item in flight.  Two named
@@ -373,13 +453,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     float acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) acc[n] = 0.0f;
-    auto item_row = [&](int it) { return row0 + (it / nchunk) * rstride; };
-    auto issue = [&](int it) {
-        const bool valid = it < nitems;                             // past the end: zero-size descriptor
-        const int r = valid ? item_row(it) : row0;
-        return load_pair(row_ptr(valid ? r : 0), valid ? rowbytes : 0, 64 * (it % nchunk) + lane);
-    };
-    auto process = [&](const PairRegs &v, int it) {
+    auto process = [&](const PairRegs &v, int it) __attribute__((always_inline)) {
         const int chunk = it % nchunk;
         const int p = 64 * chunk + lane;
         if (p < npairs) {
@@ -393,21 +467,22 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
 #pragma unroll
             for (int n = 0; n < NT; n++) {
                 const int bA = n * nb + 2 * p;
-                const float2 dx = *reinterpret_cast<const float2 *>(xd + bA);
-                const int2 sx = *reinterpret_cast<const int2 *>(xs + bA);
-                const int sA = dot_q4_q8(qA0, qA1, qA2, qA3, xq + bA * 8) - sx.x;
-                const int sB = dot_q4_q8(v.b.y, v.b.z, v.b.w, v.c, xq + bA * 8 + 8) - sx.y;
+                const float2 dx = KO_LDS ? make_float2(1.0f, 2.0f) : *reinterpret_cast<const float2 *>(xd + bA);
+                const int2 sx = KO_LDS ? make_int2(0, 0) : *reinterpret_cast<const int2 *>(xs + bA);
+                const u32x4 *xc = reinterpret_cast<const u32x4 *>(xq + n * nb * 8) + p;
+                const u32x4 c1{0x01010101u, 0x02020202u, 0x03030303u, (uint32_t)p};
+                const int sA = dot_q4_q8(qA0, qA1, qA2, qA3, KO_LDS ? c1 : xc[0], KO_LDS ? c1 : xc[npairs]) - (KO_LDS ? p : sx.x);
+                const int sB = dot_q4_q8(v.b.y, v.b.z, v.b.w, v.c, KO_LDS ? c1 : xc[2 * npairs], KO_LDS ? c1 : xc[3 * npairs]) - (KO_LDS ? lane : sx.y);
                 acc[n] = fmaf((float)sA, dA * dx.x, acc[n]);
                 acc[n] = fmaf((float)sB, dB * dx.y, acc[n]);
             }
         }
         if (chunk == nchunk - 1) {                                  // row complete: reduce + store
             const int r = item_row(it);
-            int mi = 0;
-#pragma unroll
-            for (int i = 1; i < GEMV_MAXMAT; i++) mi += (i < mats.n && r >= mats.row_begin[i]) ? 1 : 0;
-            float *yo = mats.y[mi] + (r - mats.row_begin[mi]);
-            const int64_t ld = mats.ldy[mi];
+            const bool g1 = r >= rb1, g2 = r >= rb2, g3 = r >= rb3;
+            const int rb = (g1 ? rb1 : 0) + (g2 ? rb2 - rb1 : 0) + (g3 ? rb3 - rb2 : 0);
+            float *yo = reinterpret_cast<float *>(y0 + (g1 ? yd1 : 0) + (g2 ? yd2 : 0) + (g3 ? yd3 : 0)) + (r - rb);
+            const int64_t ld = l0 + (g1 ? ld1 : 0) + (g2 ? ld2 : 0) + (g3 ? ld3 : 0);
             float out = 0.0f;
 #pragma unroll
             for (int n = 0; n < NT; n++) {
@@ -419,18 +494,18 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
             if (lane < NT) yo[(int64_t)lane * ld] = out;
         }
     };
-    PairRegs nxt;
-    for (int it = 0; it < nitems; it += 2) {
-        nxt = issue(it + 1);
-        if (it == 0 && DIAG == 7) {                                 // when the first weights have landed
-            asm volatile("" ::"v"(cur.a), "v"(cur.b), "v"(cur.c));
-            GEMV_STAMP(4);
+    for (int it = 0; it < nitems; it += DEPTH) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; d++) {
+            if (it + d >= nitems) break;
+            if (DIAG == 7 && it + d == 0) {                         // when the first weights have landed
+                asm volatile("" ::"v"(buf[0].a), "v"(buf[0].b), "v"(buf[0].c));
+                GEMV_STAMP(4);
+            }
+            process(buf[d], it + d);
+            if (it + d == 0) GEMV_STAMP(5);
+            buf[d] = issue(it + d + DEPTH);
         }
-        process(cur, it);
-        if (it == 0) GEMV_STAMP(5);
-        if (it + 1 >= nitems) break;
-        cur = issue(it + 2);
-        process(nxt, it + 1);
     }
     GEMV_STAMP(6);
 }
@@ -447,7 +522,7 @@ static int env_int(const char *name, int dflt) {
     return e ? atoi(e) : dflt;
 }
 
-template <int NT, int DIAG, int WAVES>
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0>
 static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
@@ -457,20 +532,36 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     const int64_t need = (M + WAVES - 1) / WAVES;
     const int64_t cap = (int64_t)dev.num_cus * (wg_per_cu < 1 ? 1 : wg_per_cu);
     const unsigned grid = (unsigned)(need < cap ? need : cap);
+    GemvMats ma = m;
+    ma.M = (int)M;
+    ma.rstride = (int)grid * WAVES;
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES>), dim3(grid), dim3(WAVES * 64), lds, s, m, rowbytes, nb, x,
-                       (int)K);
+    hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR>), dim3(grid), dim3(WAVES * 64), lds, s, ma, rowbytes, nb,
+                       x, (int)K);
     return hipGetLastError();
 }
 
 template <int NT>
 static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
-    // GGML_HIP_GEMV_DIAG=7: diagnostic build with per-wave phase stamps (gemv_read_stamps)
+    // Production: VAR 3 (global weight loads + x-wave prologue), ring depth 1 for single-chunk
+    // rows (K <= 4096) and 2 when a row spans several 64-pair chunks (measured per shape,
+    // tools/gemv_ab.sh).  GGML_HIP_GEMV_VAR=0 / GGML_HIP_GEMV_DEPTH=1|2 select the A/B variants;
+    // GGML_HIP_GEMV_DIAG=7 the phase-stamp build, 8/9/10 the timing knockouts (invalid results).
     static const int diag = env_int("GGML_HIP_GEMV_DIAG", 0);
-    static const int waves = env_int("GGML_HIP_GEMV_WAVES", 16);
-    if (NT == 1 && diag == 7) return launch_gemv_w<NT, 7, 16>(m, K, x, dev, s);
-    if (waves == 8) return launch_gemv_w<NT, 0, 8>(m, K, x, dev, s);
-    return launch_gemv_w<NT, 0, 16>(m, K, x, dev, s);
+    static const int var = env_int("GGML_HIP_GEMV_VAR", 3);
+    static const int depth_env = env_int("GGML_HIP_GEMV_DEPTH", 0);
+    const int depth = depth_env ? depth_env : (K / 64 > 64 ? 2 : 1);
+    if constexpr (NT == 1) {
+        if (diag == 7) return depth == 1 ? launch_gemv_w<NT, 7, 16, 1, 3>(m, K, x, dev, s)
+                                         : launch_gemv_w<NT, 7, 16, 2, 3>(m, K, x, dev, s);
+        if (diag == 8) return launch_gemv_w<NT, 8, 16, 1>(m, K, x, dev, s);
+        if (diag == 9) return launch_gemv_w<NT, 9, 16, 1>(m, K, x, dev, s);
+        if (diag == 10) return launch_gemv_w<NT, 10, 16, 1>(m, K, x, dev, s);
+    }
+    if (var == 0) return depth == 1 ? launch_gemv_w<NT, 0, 16, 1, 0>(m, K, x, dev, s)
+                                    : launch_gemv_w<NT, 0, 16, 2, 0>(m, K, x, dev, s);
+    return depth == 1 ? launch_gemv_w<NT, 0, 16, 1, 3>(m, K, x, dev, s)
+                      : launch_gemv_w<NT, 0, 16, 2, 3>(m, K, x, dev, s);
 }
 
 hipError_t gemv_read_stamps(unsigned long long *host, int n) {

@@ -102,3 +102,19 @@ def test_compute_forward_declines_other_ops_without_device(lib):
 
 def test_version(lib):
     assert b"gfx950" in lib.ggml_hip_version()
+
+
+def test_cuda_abi_shim_exports_reference_names():
+    """libggml_hip_cuda.so exports every ggml-cuda.h name declared in include/ggml-hip-cuda-abi.h
+    (the full reference list, ggml-cuda.h:15-36) and forwards to libggml_hip.so."""
+    import re
+    hdr = os.path.join(os.path.dirname(os.path.dirname(LIB_PATH)), "include", "ggml-hip-cuda-abi.h")
+    shim = os.path.join(os.path.dirname(LIB_PATH), "libggml_hip_cuda.so")
+    src = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(ggml_(?:cuda|init_cublas)\w*)\s*\(", src)))
+    assert len(declared) == 17
+    out = subprocess.check_output(["nm", "-D", "--defined-only", shim], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    assert not [s for s in declared if s not in exported]
+    deps = subprocess.check_output(["readelf", "-d", shim], text=True)
+    assert "libggml_hip.so" in deps and "oracle" not in deps

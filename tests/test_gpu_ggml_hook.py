@@ -1,0 +1,98 @@
+"""The reference's own ggml.c drives the MI355X backend through its own GPU hooks.
+
+oracle/_ref/libggml_ref_hip.so is the reference ggml.c compiled unmodified with -DGGML_USE_CUBLAS
+and linked against libggml_hip_cuda.so (include/ggml-hip-cuda-abi.h, the ggml-cuda.h names as
+aliases of ggml-hip.h).  A q4_0 mul_mat graph built and computed by ggml (ggml_init ->
+ggml_init_cublas, planner can_mul_mat, ggml_compute_forward -> ggml_cuda_compute_forward) must:
+  * run on the GPU when the weight is offloaded (llama.cpp's loader: backend = GPU, then
+    ggml_cuda_transform_tensor) or when N >= 32 (can_mul_mat, weights uploaded per call), with y
+    within the north-star bound of the reference's CPU result (the golden vectors / the oracle,
+    which is bit-exact to the reference's AVX2 build);
+  * fall back to ggml's own CPU op, bit-exact to the AVX2 reference, for what the backend
+    declines (a CPU weight with N < 32), exactly like the CUDA backend.
+The library is built in this container from /root/reference (oracle/Makefile `ref`); the test is
+skipped where it was not built.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_io import load
+from hip_env import ROOT, gpu_available
+from parity import block_terms, check_y
+
+LIB = os.path.join(ROOT, "oracle", "_ref", "libggml_ref_hip.so")
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs a HIP device and libggml_hip.so"),
+              pytest.mark.skipif(not os.path.exists(LIB), reason="oracle/_ref/libggml_ref_hip.so not built")]
+
+RTOL, ATOL_BLOCKS = 1e-3, 1e-5
+GGML_BACKEND_CPU = 0
+
+
+@pytest.fixture(scope="module")
+def ref():
+    lib = ctypes.CDLL(LIB)
+    lib.refhip_mul_mat.restype = ctypes.c_int
+    lib.refhip_mul_mat.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    lib.refhip_has_gpublas.restype = ctypes.c_int
+    return lib
+
+
+def ggml_mul_mat(ref, wq, K, x, offload, n_threads):
+    wq = np.ascontiguousarray(wq, np.uint8)
+    x = np.ascontiguousarray(x, np.float32)
+    M, N = wq.shape[0], x.shape[0]
+    y = np.full((N, M), np.nan, np.float32)
+    be = ref.refhip_mul_mat(wq.ctypes.data, K, M, x.ctypes.data, N, y.ctypes.data, offload, n_threads)
+    assert be >= 0
+    return y, be
+
+
+def assert_close(wq, x, K, y, y_ref):
+    xq = O.quantize_q8_0(x)
+    _, s_abs = block_terms(wq, xq, K)
+    rel, _ = check_y(y, y_ref, s_abs, rtol=RTOL, atol_blocks=ATOL_BLOCKS)
+    assert rel < RTOL
+
+
+def test_hooks_present(ref):
+    assert ref.refhip_has_gpublas() == 1          # ggml_cpu_has_cublas(): built with the GPU hooks
+
+
+@pytest.mark.parametrize("n_threads", [1, 4])
+@pytest.mark.parametrize("offload", [1, 2])
+def test_offloaded_weight_golden(ref, offload, n_threads):
+    wq, x = load("avx2", "w4096_q4_0"), load("avx2", "x4096_f32")
+    y, _ = ggml_mul_mat(ref, wq, 4096, x, offload, n_threads)
+    assert np.isfinite(y).all()
+    assert_close(wq, x, 4096, y, load("avx2", "y4096_mul_mat"))
+
+
+def test_offloaded_weight_falcon_golden(ref):
+    wq, x = load("avx2", "w4544_q4_0"), load("avx2", "x4544_f32")
+    y, _ = ggml_mul_mat(ref, wq, 4544, x, 1, 2)
+    assert_close(wq, x, 4544, y, load("avx2", "y4544_mul_mat"))
+
+
+@pytest.mark.parametrize("K,M,N,offload", [(4096, 256, 32, 0), (4096, 512, 64, 0), (11008, 128, 48, 1),
+                                           (4096, 300, 512, 1), (4544, 4672 // 8, 33, 0)])
+def test_prefill_through_ggml(ref, K, M, N, offload):
+    wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED7000 + K + M, 0.0, 0.02).reshape(M, K))
+    x = O.gaussian(N * K, 0x5EED7100 + N, 0.0, 1.0).reshape(N, K)
+    y, _ = ggml_mul_mat(ref, wq, K, x, offload, 4)
+    assert_close(wq, x, K, y, O.mul_mat(wq, K, x))
+
+
+def test_declined_node_runs_reference_cpu_op(ref):
+    """CPU weight and N < 32: can_mul_mat is false, ggml computes it itself (AVX2 vec_dot), so
+    the result is the reference's CPU result bit for bit."""
+    wq, x = load("avx2", "w4096_q4_0"), load("avx2", "x4096_f32")
+    y, be = ggml_mul_mat(ref, wq, 4096, x, 0, 2)
+    assert be == GGML_BACKEND_CPU
+    assert np.array_equal(y.view(np.uint32), load("avx2", "y4096_mul_mat").view(np.uint32))

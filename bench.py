@@ -10,8 +10,9 @@ block_q4_0 rows, distinct memory per layer) is resident in HBM and larger than t
 Infinity Cache.  The 224 launches of a step are captured once in a HIP graph and replayed.
 
 N GPUs (torchrun, one process per GPU): every matrix is row-sharded N ways (the reference's
-GGML_BACKEND_GPU_SPLIT) and each mul_mat ends with an RCCL all-gather of the y slices over
-xGMI; value = tokens/s of the sharded model (strong scaling: total work fixed).
+GGML_BACKEND_GPU_SPLIT); siblings (wq|wk|wv, w1|w3) run as one GEMV launch per rank followed by
+one grouped RCCL all-gather of their y slices over xGMI (4 collectives per layer; SURVEY 8e);
+value = tokens/s of the sharded model (strong scaling: total work fixed).
 
 Extra fields: per-kernel roofline of the dominant kernel (the decode GEMV) from HIP events on
 the launch stream, prefill (N=512) GB/s and int8-MFMA TOP/s, and the CPU baseline (the oracle's
@@ -140,30 +141,48 @@ def main():
         gh.check(L.ggml_hip_reserve_workspace(K, max(1, args.prefill_tokens)))
     gh.synchronize()
 
-    batch = comm is None and not args.no_batch_siblings
+    batch = not args.no_batch_siblings
     # sibling groups that share src1 in the LLaMA graph: (wq, wk, wv) and (w1, w3)
     groups = [[0, 1, 2], [3], [4, 5], [6]] if batch else [[i] for i in range(len(LAYER))]
     yb = {i: gh.DeviceBuffer(LAYER[i][2] * 4) for i in range(len(LAYER))}
-    launch_args = []
-    for row in stack.mats:
-        for g in groups:
-            if len(g) == 1 or not batch:
-                launch_args.append(("one", tuple(row[g[0]]) + (yb[g[0]],)))
-            else:
-                n = len(g)
-                wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
-                yp = (ctypes.c_void_p * n)(*[yb[i].ptr for i in g])
-                mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
-                launch_args.append(("multi", (n, wp, mp, row[g[0]][1], yp)))
+    ysplit = {i: gh.DeviceBuffer(LAYER[i][2] * 4) for i in range(len(LAYER))}   # full-M gathered outputs
+    def build_launch_args(use_comm):
+        out = []
+        for row in stack.mats:
+            for g in groups:
+                if len(g) == 1 or not batch:
+                    out.append(("one" if use_comm else "local", tuple(row[g[0]]) + (yb[g[0]],)))
+                elif not use_comm:
+                    n = len(g)
+                    wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
+                    yp = (ctypes.c_void_p * n)(*[yb[i].ptr for i in g])
+                    mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
+                    out.append(("multi", (n, wp, mp, row[g[0]][1], yp)))
+                else:                # split siblings: one GEMV launch + one grouped all-gather
+                    n = len(g)
+                    wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
+                    mt = (ctypes.c_int64 * n)(*[row[i][2] for i in g])
+                    rp = (ctypes.c_void_p * n)(*[row[i][5].ctypes.data for i in g])
+                    yp = (ctypes.c_void_p * n)(*[ysplit[i].ptr for i in g])
+                    out.append(("split_multi", (n, wp, mt, rp, row[g[0]][1], yp)))
+        return out
 
-    def decode_step():
+    launch_args = build_launch_args(comm is not None)
+
+    def decode_step(launch_args=launch_args):
         for kind, a in launch_args:
             if kind == "multi":
                 n, wp, mp, K, yp = a
                 gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, 1, yp, stream))
                 continue
-            name, K, M, m_loc, buf, rb, _ = a
-            if comm is None:
+            if kind == "split_multi":
+                n, wp, mt, rp, K, yp = a
+                gh.check(L.ggml_hip_mul_mat_q4_0_split_multi(comm, n, wp, mt, rp, K, xs[K].ptr, 1, yp, stream))
+                continue
+            name, K, M, m_loc, buf, rb, ylocal = a
+            if kind == "local":      # this rank's slice only, no collective
+                gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, 1, ylocal.ptr, m_loc, 0, stream))
+            elif comm is None:
                 gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, M, xs[K].ptr, 1, ys[M].ptr, M, 0, stream))
             else:
                 gh.check(L.ggml_hip_mul_mat_q4_0_split(comm, buf.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
@@ -213,9 +232,33 @@ def main():
                                "4096->11008; w2 11008->4096), N=1, q8_0 quantize of x included, lm_head excluded",
                    "layers": args.layers, "weights_bytes_per_rank": stack.total_bytes,
                    "graph": graph is not None, "launches_per_layer": len(groups),
-                   "sibling_batching": "wq|wk|wv and w1|w3 share src1 -> one launch each" if batch else "off",
+                   "sibling_batching": ("wq|wk|wv and w1|w3 share src1 -> one launch each"
+                                        + (" + one grouped all-gather each" if comm is not None else ""))
+                   if batch else "off",
+                   "collectives_per_layer": len(groups) if comm is not None else 0,
                    "parallelism": f"row-split x{world} + RCCL all-gather" if world > 1 else "single GPU"},
     }
+
+    if comm is not None:
+        # same sharded graph without the all-gathers: what the collectives cost
+        g2 = gh.Graph(stream)
+        with g2:
+            decode_step(build_launch_args(False))
+        for _ in range(args.warmup):
+            g2.launch()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g2.launch()
+        barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            import torch
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        result["config"]["compute_only_tok_s"] = round(args.steps / el * 32 / args.layers, 2)
+        result["config"]["collective_us_per_token"] = round((elapsed - el) / args.steps * 1e6 * 32 / args.layers, 1)
 
     if rank == 0 and world == 1 and comm is None:
         result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))

@@ -153,6 +153,15 @@ int ggml_hip_split_rows(int64_t M, int nranks, const float *tensor_split, int64_
 int ggml_hip_mul_mat_q4_0_split(ggml_hip_comm *comm, const void *dev_w_local, int64_t K, int64_t M_total,
                                 const int64_t *row_begin, const float *dev_x, int64_t N, float *dev_y_full,
                                 void *stream);
+/* Sibling form ("fuse QKV (3) and w1/w3 (2) into one all-gather each"): n <= 4
+ * matrices sharing x, matrix i row-split by row_begin[i] (nranks+1 entries each).  With equal
+ * splits and N == 1 this rank's slices are computed by ONE multi-matrix GEMV launch straight into
+ * their places in y_full[i], then ONE grouped RCCL all-gather (ncclGroupStart/End) completes all
+ * n outputs in place.  Other cases run ggml_hip_mul_mat_q4_0_split per matrix.  Results are
+ * identical to n separate split calls. */
+int ggml_hip_mul_mat_q4_0_split_multi(ggml_hip_comm *comm, int n, const void *const *dev_w_local, const int64_t *M_total,
+                                      const int64_t *const *row_begin, int64_t K, const float *dev_x, int64_t N,
+                                      float *const *dev_y_full, void *stream);
 
 /* ------------------------------------------------------------------------------------------
  * Device plumbing for bindings (ctypes / cgo / JNI) that have no HIP headers.

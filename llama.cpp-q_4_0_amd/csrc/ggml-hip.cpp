@@ -704,6 +704,49 @@ int ggml_hip_mul_mat_q4_0_split(ggml_hip_comm *c, const void *dev_w_local, int64
     return GGML_HIP_OK;
 }
 
+int ggml_hip_mul_mat_q4_0_split_multi(ggml_hip_comm *c, int n, const void *const *dev_w_local, const int64_t *M_total,
+                                      const int64_t *const *row_begin, int64_t K, const float *dev_x, int64_t N,
+                                      float *const *dev_y_full, void *stream) {
+    if (!c || n < 1 || n > 4 || !dev_w_local || !M_total || !row_begin || !dev_y_full)
+        return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    const int R = c->nranks;
+    bool equal = N == 1;
+    for (int i = 0; i < n && equal; i++) {
+        if (!row_begin[i] || row_begin[i][0] != 0 || row_begin[i][R] != M_total[i]) equal = false;
+        for (int r = 0; r < R && equal; r++)
+            if (row_begin[i][r + 1] - row_begin[i][r] != row_begin[i][1] - row_begin[i][0] ||
+                row_begin[i][1] - row_begin[i][0] < 1)
+                equal = false;
+    }
+    if (!equal) {
+        for (int i = 0; i < n; i++) {
+            const int rc = ggml_hip_mul_mat_q4_0_split(c, dev_w_local[i], K, M_total[i], row_begin[i], dev_x, N,
+                                                       dev_y_full[i], stream);
+            if (rc != GGML_HIP_OK) return rc;
+        }
+        return GGML_HIP_OK;
+    }
+    hipStream_t s = resolve_stream(stream);
+    int64_t m_loc[4];
+    float *mine[4];
+    for (int i = 0; i < n; i++) {
+        m_loc[i] = row_begin[i][c->rank + 1] - row_begin[i][c->rank];
+        mine[i] = dev_y_full[i] + row_begin[i][c->rank];
+    }
+    const int rc = ggml_hip_mul_mat_q4_0_multi(n, dev_w_local, m_loc, K, dev_x, N, mine, s);
+    if (rc != GGML_HIP_OK) return rc;
+    NCCL_RET(ncclGroupStart());
+    for (int i = 0; i < n; i++) {
+        const ncclResult_t r = ncclAllGather(mine[i], dev_y_full[i], (size_t)m_loc[i], ncclFloat32, c->comm, s);
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            NCCL_RET(r);
+        }
+    }
+    NCCL_RET(ncclGroupEnd());
+    return GGML_HIP_OK;
+}
+
 // ------------------------------------------------------------------------------------------
 // device plumbing
 

@@ -328,3 +328,34 @@ def test_split_path_single_rank_rccl(N):
         assert np.array_equal(y.view(np.uint32), single.view(np.uint32))
     finally:
         L.ggml_hip_comm_destroy(comm)
+
+
+@pytest.mark.parametrize("N,Ms", [(1, (256, 256, 256)), (1, (512, 1376)), (3, (320, 64))])
+def test_split_multi_single_rank_rccl(N, Ms):
+    """ggml_hip_mul_mat_q4_0_split_multi (one multi-matrix GEMV + one grouped all-gather for the
+    siblings; per-matrix split for N > 1) equals separate plain mul_mats bitwise."""
+    L = ggml_hip.load()
+    uid = ctypes.create_string_buffer(128)
+    ggml_hip.check(L.ggml_hip_comm_unique_id(uid))
+    comm = ctypes.c_void_p()
+    ggml_hip.check(L.ggml_hip_comm_init(ctypes.byref(comm), 1, 0, uid), "comm_init")
+    try:
+        K, n = 4096, len(Ms)
+        x = O.gaussian(N * K, 0x5EED2200 + N, 0.0, 1.0).reshape(N, K)
+        cases = [make_case(K, M, N, seed=90 + i)[0] for i, M in enumerate(Ms)]
+        wds = [DB.from_array(w) for w in cases]
+        yds = [DB(N * M * 4) for M in Ms]
+        rbs = [np.array([0, M], np.int64) for M in Ms]
+        xd = DB.from_array(x)
+        wp = (ctypes.c_void_p * n)(*[w.ptr for w in wds])
+        mp = (ctypes.c_int64 * n)(*Ms)
+        rp = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rbs])
+        yp = (ctypes.c_void_p * n)(*[y.ptr for y in yds])
+        ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split_multi(comm, n, wp, mp, rp, K, xd.ptr, N, yp, None),
+                       "split_multi")
+        ggml_hip.check(L.ggml_hip_stream_synchronize(None))
+        for w, M, yd in zip(cases, Ms, yds):
+            single, _ = gpu_mul_mat(w, K, x)
+            assert np.array_equal(yd.download((N, M), np.float32).view(np.uint32), single.view(np.uint32))
+    finally:
+        L.ggml_hip_comm_destroy(comm)

@@ -846,6 +846,243 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm_q4_0(const uint8_t *__re
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// GEMM v6 (default).  Same tile (64 weight rows x 128 tokens, 8 waves, one 32x32 tile per wave,
+// K-stage = 4 blocks, LDS double buffer, global loads two stages ahead), restructured per block:
+//   * the per-block scale d_x[token] * d_w[row] is an exact rank-1 product of two fp16 values, so
+//     one v_mfma_f32_32x32x16_f16 with d_x at k = 0 of A and d_w at k = 0 of B produces all 16
+//     products of a lane in the int8 tile's D layout (fp16 x fp16 is exact in fp32: the same value
+//     as the CPU's fp32(d_x) * fp32(d_w)); the epilogue is cvt + fma per output and block;
+//   * software pipeline over blocks: operands of block b+1 are read from LDS while block b's two
+//     MFMAs run and block b-1's epilogue executes (two named result sets; the last block's
+//     epilogue of a stage runs after the next stage's first MFMAs);
+//   * weight staging is spread over all 512 threads (row, block, half) so that the barrier does
+//     not wait on two staging waves.
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+static constexpr int G6_STAGE_W = GM_KB * GM_BM * 32;           // int8 weights  [KB][BM][32]
+static constexpr int G6_STAGE_X = GM_KB * GM_BN * 32;           // int8 acts     [KB][BN][32]
+static constexpr int G6_STAGE_WD = GM_KB * GM_BM * 2;           // fp16 d_w      [KB][BM]
+static constexpr int G6_STAGE_XD = GM_KB * GM_BN * 2;           // fp16 d_x      [KB][BN]
+static constexpr int G6_STAGE = G6_STAGE_W + G6_STAGE_X + G6_STAGE_WD + G6_STAGE_XD;   // 25.5 KB
+static_assert(GM_BM * GM_KB * 2 == GM_THREADS, "one (row, block, half) of the weights per thread");
+
+struct G6Regs {
+    u32x4 wa, wb;
+    uint32_t wc;
+    u32x4 x[2];
+    float xd;
+};
+struct G6Ops {
+    i32x4 a, b;
+    uint32_t sx, sw;
+};
+
+template <int DIAG>
+__global__ __launch_bounds__(GM_THREADS, 2) void k_gemm6_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes,
+                                                               int nb, int M, const int8_t *__restrict__ xqs,
+                                                               const float *__restrict__ xd, int N, int K,
+                                                               float *__restrict__ y, int64_t ldy) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wr = wave & 1, wt = wave >> 1;                        // 2 row waves x 4 token waves
+    const int c = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.x * GM_BM;
+    const int n0 = blockIdx.y * GM_BN;
+
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W + (int64_t)m0 * rowbytes, (uint32_t)((int64_t)(M - m0) * rowbytes));
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)(N - n0) * K));
+    const __amdgpu_buffer_rsrc_t nul = make_rsrc(W, 0);
+
+    // weight staging role: row sr, block sb of the stage, nibble half sh (all threads).  The 8 lanes
+    // of a row are adjacent (one 72-byte span per row for the global loads).  Measured: the
+    // bank-conflict-free mapping (8-lane groups = 4 rows x 2 halves) removes every LDS conflict but
+    // runs 8 % slower overall (wider global footprint per wave-instruction).
+    const int sr = tid >> 3, sb = (tid >> 1) & 3, sh = tid & 1;
+
+    auto load_stage = [&](int kb0, G6Regs &g) __attribute__((always_inline)) {
+        const bool valid = kb0 < nb && (DIAG != 3 || kb0 == 0);    // past the last stage: no traffic
+        const __amdgpu_buffer_rsrc_t wr_ = valid ? wrs : nul;
+        const int woff = (int)(sr * rowbytes) + (kb0 + (sb & ~1)) * Q4B;   // the pair holding block sb
+        g.wa = __builtin_amdgcn_raw_buffer_load_b128(wr_, woff, 0, 0);
+        g.wb = __builtin_amdgcn_raw_buffer_load_b128(wr_, woff + 16, 0, 0);
+        g.wc = __builtin_amdgcn_raw_buffer_load_b32(wr_, woff + 32, 0, 0);
+        const __amdgpu_buffer_rsrc_t xr_ = valid ? xrs : nul;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {          // piece (token t, block piece>>1, half piece&1): 128 B per token
+            const int idx = tid + GM_THREADS * i;
+            const int t = idx >> 3, piece = idx & 7;
+            g.x[i] = __builtin_amdgcn_raw_buffer_load_b128(xr_, t * K + kb0 * QK + 16 * piece, 0, 0);
+        }
+        {
+            const int b = tid >> 7, t = tid & 127;
+            g.xd = (valid && n0 + t < N && kb0 + b < nb) ? xd[(int64_t)(n0 + t) * nb + kb0 + b] : 0.0f;
+        }
+    };
+    auto store_stage = [&](int kb0, const G6Regs &g, uint8_t *st) __attribute__((always_inline)) {
+        uint8_t *ws = st;
+        uint8_t *xs = st + G6_STAGE_W;
+        uint16_t *wds = reinterpret_cast<uint16_t *>(st + G6_STAGE_W + G6_STAGE_X);
+        uint16_t *xds = reinterpret_cast<uint16_t *>(st + G6_STAGE_W + G6_STAGE_X + G6_STAGE_WD);
+        {
+            const bool odd = sb & 1;
+            const uint32_t q0 = odd ? g.wb.y : __builtin_amdgcn_alignbyte(g.wa.y, g.wa.x, 2);
+            const uint32_t q1 = odd ? g.wb.z : __builtin_amdgcn_alignbyte(g.wa.z, g.wa.y, 2);
+            const uint32_t q2 = odd ? g.wb.w : __builtin_amdgcn_alignbyte(g.wa.w, g.wa.z, 2);
+            const uint32_t q3 = odd ? g.wc : __builtin_amdgcn_alignbyte(g.wb.x, g.wa.w, 2);
+            u32x4 t;
+            t.x = nib_to_i8x4(q0, 4 * sh); t.y = nib_to_i8x4(q1, 4 * sh);
+            t.z = nib_to_i8x4(q2, 4 * sh); t.w = nib_to_i8x4(q3, 4 * sh);
+            *reinterpret_cast<u32x4 *>(ws + sb * GM_BM * 32 + gm_half_off(sr, sh)) = t;
+            if (sh == 0) {
+                const uint32_t d16 = odd ? (g.wb.x >> 16) : (g.wa.x & 0xFFFFu);
+                wds[sb * GM_BM + sr] = (uint16_t)((kb0 + sb < nb) ? d16 : 0u);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int idx = tid + GM_THREADS * i;
+            const int t = idx >> 3, piece = idx & 7;
+            *reinterpret_cast<u32x4 *>(xs + (piece >> 1) * GM_BN * 32 + gm_half_off(t, piece & 1)) = g.x[i];
+        }
+        xds[tid] = (uint16_t)f2h(g.xd);                            // exact: d_x is an fp16 value
+    };
+
+    const int tok = 32 * wt + c;             // A row (token) of this lane
+    const int wrow = 32 * wr + c;            // B column (weight row) of this lane
+    auto ld_ops = [&](const uint8_t *st, int b) __attribute__((always_inline)) {
+        const uint8_t *ws = st;
+        const uint8_t *xs = st + G6_STAGE_W;
+        const uint16_t *wds = reinterpret_cast<const uint16_t *>(st + G6_STAGE_W + G6_STAGE_X);
+        const uint16_t *xds = reinterpret_cast<const uint16_t *>(st + G6_STAGE_W + G6_STAGE_X + G6_STAGE_WD);
+        G6Ops o;
+        o.a = *reinterpret_cast<const i32x4 *>(xs + b * GM_BN * 32 + gm_half_off(tok, h));
+        o.b = *reinterpret_cast<const i32x4 *>(ws + b * GM_BM * 32 + gm_half_off(wrow, h));
+        o.sx = xds[b * GM_BN + tok];
+        o.sw = wds[b * GM_BM + wrow];
+        return o;
+    };
+    const i32x16 iz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // The int8 MFMA accumulates onto 0x4B400000, so S holds the float bits of 12582912 + sumi (exact
+    // for |sumi| < 2^22; here |sumi| <= 32*8*128): float(sumi) = S_f - 12582912 exactly, a full-rate
+    // v_sub_f32 instead of v_cvt_f32_i32 (compute phase -13 %; DIAG 6 keeps the cvt form)
+    constexpr bool MAGIC = DIAG != 6;
+    const int mg = 0x4B400000;
+    const i32x16 im = {mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg};
+    auto mfma2 = [&](const G6Ops &o, i32x16 &S, f32x16 &P) __attribute__((always_inline)) {
+        S = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a, o.b, MAGIC ? im : iz, 0, 0, 0);
+        const u32x4 as = {h == 0 ? o.sx : 0u, 0u, 0u, 0u};
+        const u32x4 bs = {h == 0 ? o.sw : 0u, 0u, 0u, 0u};
+        P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs), fz,
+                                                   0, 0, 0);
+    };
+    float acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+    auto epi = [&](const i32x16 &S, const f32x16 &P) __attribute__((always_inline)) {
+        if (DIAG == 1) {                                            // diagnostic: no epilogue VALU
+            asm volatile("" ::"v"(S[0]), "v"(S[15]), "v"(P[0]), "v"(P[15]));
+            return;
+        }
+        if (MAGIC) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc[i] = fmaf(__int_as_float(S[i]) - 12582912.0f, P[i], acc[i]);
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc[i] = fmaf((float)S[i], P[i], acc[i]);
+    };
+
+    // one stage: blocks 0..3 from LDS buffer st; set 1 holds the previous stage's last block
+    i32x16 S0, S1 = iz;
+    f32x16 P0, P1 = fz;
+    auto compute_stage = [&](const uint8_t *st) __attribute__((always_inline)) {
+        G6Ops o0 = ld_ops(st, 0);
+        G6Ops o1 = ld_ops(st, 1);
+        mfma2(o0, S0, P0);
+        epi(S1, P1);                          // previous stage's block 3 (zeros on the first stage)
+        o0 = ld_ops(st, 2);
+        mfma2(o1, S1, P1);
+        epi(S0, P0);
+        o1 = ld_ops(st, 3);
+        mfma2(o0, S0, P0);
+        epi(S1, P1);
+        mfma2(o1, S1, P1);
+        epi(S0, P0);
+    };
+
+    unsigned long long t_c = 0, t_s = 0, t_b = 0, t_mark = 0, t_begin = 0;
+    auto mark = [&](unsigned long long &acc_t) __attribute__((always_inline)) {
+        if (DIAG == 5) {
+            __builtin_amdgcn_sched_barrier(0);
+            unsigned long long t;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            acc_t += t - t_mark;
+            t_mark = t;
+        }
+    };
+    if (DIAG == 5) {
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_mark)::"memory");
+        t_begin = t_mark;
+    }
+    const int nstages = (nb + GM_KB - 1) / GM_KB;
+    G6Regs gA, gB;
+    load_stage(0, gA);
+    load_stage(GM_KB, gB);
+    store_stage(0, gA, smem);
+    mark(t_s);
+    __syncthreads();
+    mark(t_b);
+    if (DIAG == 6 || DIAG == 7) {             // diagnostic: compute phase only (stage 0 data, no sync;
+                                              // 6 with the cvt epilogue, 7 with the default one)
+        for (int s = 0; s < nstages; s++) {
+            compute_stage(smem);
+            mark(t_c);
+        }
+    }
+    for (int s = 0; DIAG != 6 && DIAG != 7 && s < nstages; s += 2) {
+        load_stage((s + 2) * GM_KB, gA);
+        compute_stage(smem);
+        mark(t_c);
+        if (s + 1 >= nstages) break;
+        store_stage((s + 1) * GM_KB, gB, smem + G6_STAGE);
+        mark(t_s);
+        __syncthreads();
+        mark(t_b);
+        load_stage((s + 3) * GM_KB, gB);
+        compute_stage(smem + G6_STAGE);
+        mark(t_c);
+        if (s + 2 >= nstages) break;
+        store_stage((s + 2) * GM_KB, gA, smem);
+        mark(t_s);
+        __syncthreads();
+        mark(t_b);
+    }
+    epi(S1, P1);                              // the last block
+    if (DIAG == 5 && lane == 0) {
+        const int wid = (blockIdx.y * gridDim.x + blockIdx.x) * GM_WAVES + wave;
+        if (wid < 16384) {
+            g_gemm_stamps[wid * 4 + 0] = t_mark - t_begin;
+            g_gemm_stamps[wid * 4 + 1] = t_c;
+            g_gemm_stamps[wid * 4 + 2] = t_s;
+            g_gemm_stamps[wid * 4 + 3] = t_b;
+        }
+    }
+
+    const int row = m0 + wrow;
+    if (row < M) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int t = n0 + 32 * wt + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (t < N) y[(int64_t)t * ldy + row] = acc[i];
+        }
+    }
+}
+
 hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
                      float *y, int64_t ldy, hipStream_t s) {
     const int nb = (int)(K / QK);
@@ -854,6 +1091,27 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
     // GGML_HIP_GEMM_DIAG (diagnostic builds): 1 integer epilogue, 2 no MFMA, 3 no global loads,
     // 4 no LDS staging
     static const int diag = env_int("GGML_HIP_GEMM_DIAG", 0);
+    static const int ver = env_int("GGML_HIP_GEMM_V", 6);
+    if (ver == 6) {
+        // v6 diagnostics (GGML_HIP_GEMM_DIAG): 1 no epilogue VALU, 3 no global loads, 5 phase stamps,
+        // 6/7 compute phase only (cvt / default epilogue).  GGML_HIP_GEMM_V=5: the previous kernel.
+        auto k6 = diag == 1 ? k_gemm6_q4_0<1> : diag == 3 ? k_gemm6_q4_0<3> : diag == 5 ? k_gemm6_q4_0<5>
+                : diag == 6 ? k_gemm6_q4_0<6> : diag == 7 ? k_gemm6_q4_0<7> : k_gemm6_q4_0<0>;
+        static bool attr6 = false;
+        if (!attr6) {
+            for (auto k : {k_gemm6_q4_0<0>, k_gemm6_q4_0<1>, k_gemm6_q4_0<3>, k_gemm6_q4_0<5>, k_gemm6_q4_0<6>,
+                           k_gemm6_q4_0<7>}) {
+                hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   2 * G6_STAGE);
+                if (e != hipSuccess) return e;
+            }
+            attr6 = true;
+        }
+        (void)hipGetLastError();  // report only this launch's error
+        hipLaunchKernelGGL(k6, grid, dim3(GM_THREADS), 2 * G6_STAGE, s, (const uint8_t *)W, rowbytes, nb, (int)M,
+                           xqs, xd, (int)N, (int)K, y, ldy);
+        return hipGetLastError();
+    }
     auto kern = diag == 1 ? k_gemm_q4_0<1> : diag == 2 ? k_gemm_q4_0<2> : diag == 3 ? k_gemm_q4_0<3>
               : diag == 4 ? k_gemm_q4_0<4> : diag == 5 ? k_gemm_q4_0<5> : k_gemm_q4_0<0>;
     static bool attr_set = false;       // up to 2 x 27 KB of dynamic LDS

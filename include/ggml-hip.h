@@ -116,7 +116,8 @@ int ggml_hip_dequantize_q4_0(const void *dev_wq, int64_t K, int64_t M, float *de
  * ggml_hip_reserve_workspace or the first call). */
 int ggml_hip_mul_mat_q4_0(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N,
                           float *dev_y, void *stream);
-/* Same with an explicit algorithm: 0 auto, 1 GEMV (N <= 8), 2 MFMA GEMM; and output stride ldy. */
+/* Same with an explicit algorithm and output stride ldy: 0 auto (1 for N <= 8, 3 for N <= 128, else
+ * 2), 1 fused GEMV (N <= 8), 2 LDS-staged int8-MFMA GEMM, 3 split-K int8-MFMA GEMM (small N). */
 int ggml_hip_mul_mat_q4_0_ex(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N,
                              float *dev_y, int64_t ldy, int algo, void *stream);
 /* Sibling mul_mats that share the activation x (ggml graphs issue wq/wk/wv and w1/w3 on the same

@@ -199,13 +199,15 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
         return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large for 32-bit buffer offsets; split rows");
     const int id = current_device();
     const int max_nt = ghip::gemv_max_tokens(K);
-    if (algo == 0) algo = (N <= max_nt) ? 1 : 2;
+    // auto: fused GEMV for N <= 8, split-K MFMA for N <= 128, LDS-staged MFMA GEMM above
+    // (crossovers measured with tools/n_sweep.py)
+    if (algo == 0) algo = (N <= max_nt) ? 1 : (N <= 128 ? 3 : 2);
     if (algo == 1) {
         if (N > max_nt) return fail(GGML_HIP_ERR_INVALID, "GEMV path supports N <= gemv_max_tokens(K)");
         HIP_RET(ghip::gemv_q4_0(w, K, M, x, N, y, ldy, g_dev[id].info, s));
         return GGML_HIP_OK;
     }
-    if (algo != 2) return fail(GGML_HIP_ERR_INVALID, "algo must be 0, 1 or 2");
+    if (algo != 2 && algo != 3) return fail(GGML_HIP_ERR_INVALID, "algo must be 0, 1, 2 or 3");
     const size_t need = workspace_bytes(K, N);
     if (g_dev[id].ws_size < need) {
         int rc = reserve_workspace(id, need);
@@ -214,7 +216,10 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
     int8_t *qs = (int8_t *)g_dev[id].ws;
     float *xd = (float *)((char *)g_dev[id].ws + ((size_t)(N * K + 255) & ~(size_t)255));
     HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s));
-    HIP_RET(ghip::gemm_q4_0(w, K, M, qs, xd, N, y, ldy, s));
+    if (algo == 3)
+        HIP_RET(ghip::gemm_sk_q4_0(w, K, M, qs, xd, N, y, ldy, g_dev[id].info.num_cus, s));
+    else
+        HIP_RET(ghip::gemm_q4_0(w, K, M, qs, xd, N, y, ldy, s));
     return GGML_HIP_OK;
 }
 
@@ -557,7 +562,7 @@ int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *
     if (N == 0) return GGML_HIP_OK;
     if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30)) {
         for (int i = 0; i < n; i++) {       // GEMM path (x re-quantized per matrix: prefill is MFMA-bound)
-            int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 2, s);
+            int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 0, s);
             if (rc != GGML_HIP_OK) return rc;
         }
         return GGML_HIP_OK;

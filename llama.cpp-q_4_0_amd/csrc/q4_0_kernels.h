@@ -50,6 +50,10 @@ hipError_t gemm_read_stamps(unsigned long long *host, int n);
 hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd,
                      int64_t N, float *y, int64_t ldy, hipStream_t s);
 
+// Small / medium N (split-K over the waves of a 32x32-tile workgroup, operands straight to registers).
+hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
+                        float *y, int64_t ldy, int num_cus, hipStream_t s);
+
 // Multi-GPU helper: y[n*ldy + row0[r] + i] = slab[r][n][i] for i < rows[r] (gather compaction).
 hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const int64_t *row_begin_dev,
                          int64_t N, float *y, int64_t ldy, hipStream_t s);

@@ -24,6 +24,7 @@
 namespace ghip {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
@@ -1081,6 +1082,140 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm6_q4_0(const uint8_t *__r
             if (t < N) y[(int64_t)t * ldy + row] = acc[i];
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split-K MFMA GEMM for small / medium token counts (9 <= N <= 128 by default).
+//
+// The LDS-staged GEMM above runs (M/64) x ceil(N/128) workgroups that each walk all of K, so for
+// N <= 128 it uses a quarter of the chip and its time is one workgroup's K walk (~36 us at
+// K = 4096).  Here a workgroup owns one 32-row x 32-token output tile and its SK waves split K into
+// contiguous slices: each wave streams its slice's weight pairs (36 B per row) and q8_0 activations
+// straight into registers through a DP-deep ring (no LDS staging, no barriers in the loop), runs
+// the same per-block int8 MFMA + fp16 rank-1 scale MFMA + convert-free epilogue as the GEMM, and
+// the SK partial tiles are summed through LDS in a fixed order (deterministic).  For N <= 32 every
+// weight byte is read once.
+template <int SK, int DP>
+__global__ __launch_bounds__(SK * 64, 1) void k_gemm_sk_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes, int nb,
+                                                              int M, const int8_t *__restrict__ xqs,
+                                                              const float *__restrict__ xd, int N, int K,
+                                                              float *__restrict__ y, int64_t ldy) {
+    extern __shared__ __attribute__((aligned(16))) float red[];    // [SK][16][64] partial tiles
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+    // out-of-range rows / tokens read 0 through the descriptors (rows: d = 0 -> no contribution)
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W + (int64_t)m0 * rowbytes, (uint32_t)((int64_t)min(M - m0, 32) * rowbytes));
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)min(N - n0, 32) * K));
+    const __amdgpu_buffer_rsrc_t drs = make_rsrc(xd + (int64_t)n0 * nb, (uint32_t)((int64_t)min(N - n0, 32) * nb * 4));
+    const int npairs = nb >> 1;
+    const int ppw = (npairs + SK - 1) / SK;                         // pairs per wave
+    const int p_begin = wave * ppw;
+    const int p_end = min(npairs, p_begin + ppw);
+    const int np = max(0, p_end - p_begin);
+
+    struct Ring {
+        u32x4 wa, wb;
+        uint32_t wc;
+        i32x4 x0, x1;
+        float d0, d1;
+    };
+    auto issue = [&](int i) __attribute__((always_inline)) {        // pair p_begin + i (past the end: no traffic)
+        Ring r;
+        const bool v = i < np;
+        const int p = p_begin + (v ? i : 0);
+        const __amdgpu_buffer_rsrc_t w_ = v ? wrs : make_rsrc(W, 0);
+        const __amdgpu_buffer_rsrc_t x_ = v ? xrs : make_rsrc(W, 0);
+        const __amdgpu_buffer_rsrc_t d_ = v ? drs : make_rsrc(W, 0);
+        const int woff = (int)(c * rowbytes) + 36 * p;
+        r.wa = __builtin_amdgcn_raw_buffer_load_b128(w_, woff, 0, 0);
+        r.wb = __builtin_amdgcn_raw_buffer_load_b128(w_, woff + 16, 0, 0);
+        r.wc = __builtin_amdgcn_raw_buffer_load_b32(w_, woff + 32, 0, 0);
+        const int xoff = c * K + 64 * p + 16 * h;
+        r.x0 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(x_, xoff, 0, 0));
+        r.x1 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(x_, xoff + 32, 0, 0));
+        const u32x2 dd = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(d_, (c * nb + 2 * p) * 4, 0, 0));
+        r.d0 = __uint_as_float(dd.x);
+        r.d1 = __uint_as_float(dd.y);
+        return r;
+    };
+    const int mg = 0x4B400000;
+    const i32x16 im = {mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg};
+    const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    float acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+    auto block = [&](const i32x4 &xa, uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3, uint32_t dw16, float dx)
+        __attribute__((always_inline)) {
+        i32x4 wb;
+        wb.x = (int)nib_to_i8x4(q0, 4 * h);
+        wb.y = (int)nib_to_i8x4(q1, 4 * h);
+        wb.z = (int)nib_to_i8x4(q2, 4 * h);
+        wb.w = (int)nib_to_i8x4(q3, 4 * h);
+        const i32x16 S = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa, wb, im, 0, 0, 0);
+        const u32x4 as = {h == 0 ? f2h(dx) : 0u, 0u, 0u, 0u};
+        const u32x4 bs = {h == 0 ? dw16 : 0u, 0u, 0u, 0u};
+        const f32x16 P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as),
+                                                                __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc[i] = fmaf(__int_as_float(S[i]) - 12582912.0f, P[i], acc[i]);
+    };
+    auto process = [&](const Ring &r) __attribute__((always_inline)) {
+        block(r.x0, __builtin_amdgcn_alignbyte(r.wa.y, r.wa.x, 2), __builtin_amdgcn_alignbyte(r.wa.z, r.wa.y, 2),
+              __builtin_amdgcn_alignbyte(r.wa.w, r.wa.z, 2), __builtin_amdgcn_alignbyte(r.wb.x, r.wa.w, 2),
+              r.wa.x & 0xFFFFu, r.d0);
+        block(r.x1, r.wb.y, r.wb.z, r.wb.w, r.wc, r.wb.x >> 16, r.d1);
+    };
+    Ring ring[DP];
+#pragma unroll
+    for (int d = 0; d < DP; d++) ring[d] = issue(d);
+    for (int i = 0; i < np; i += DP) {
+#pragma unroll
+        for (int d = 0; d < DP; d++) {
+            if (i + d >= np) break;
+            process(ring[d]);
+            ring[d] = issue(i + d + DP);
+        }
+    }
+    // fixed-order reduction of the SK partial tiles: red[w][i][lane]
+#pragma unroll
+    for (int i = 0; i < 16; i++) red[(wave * 16 + i) * 64 + lane] = acc[i];
+    __syncthreads();
+    for (int o = tid; o < 1024; o += SK * 64) {
+        const int i = o >> 6, l = o & 63;
+        float v = 0.0f;
+        for (int w = 0; w < SK; w++) v += red[(w * 16 + i) * 64 + l];
+        const int tok = n0 + 8 * (i >> 2) + 4 * (l >> 5) + (i & 3);
+        const int row = m0 + (l & 31);
+        if (tok < N && row < M) y[(int64_t)tok * ldy + row] = v;
+    }
+}
+
+hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N, float *y,
+                        int64_t ldy, int num_cus, hipStream_t s) {
+    const int nb = (int)(K / QK);
+    const int64_t rowbytes = (int64_t)nb * Q4B;
+    dim3 grid((unsigned)((M + 31) / 32), (unsigned)((N + 31) / 32));
+    const int64_t tiles = (int64_t)grid.x * grid.y;
+    static const int sk_env = env_int("GGML_HIP_GEMM_SK", 0);
+    static const int dp = env_int("GGML_HIP_GEMM_SK_DP", 2);
+    const int sk = sk_env ? sk_env : (tiles < 2 * (int64_t)num_cus ? 16 : 8);
+    (void)hipGetLastError();  // report only this launch's error
+    if (sk == 16 && dp == 4)
+        hipLaunchKernelGGL((k_gemm_sk_q4_0<16, 4>), grid, dim3(1024), 16 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
+                           nb, (int)M, xqs, xd, (int)N, (int)K, y, ldy);
+    else if (sk == 8 && dp == 4)
+        hipLaunchKernelGGL((k_gemm_sk_q4_0<8, 4>), grid, dim3(512), 8 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
+                           nb, (int)M, xqs, xd, (int)N, (int)K, y, ldy);
+    else if (sk == 16)
+        hipLaunchKernelGGL((k_gemm_sk_q4_0<16, 2>), grid, dim3(1024), 16 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
+                           nb, (int)M, xqs, xd, (int)N, (int)K, y, ldy);
+    else
+        hipLaunchKernelGGL((k_gemm_sk_q4_0<8, 2>), grid, dim3(512), 8 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
+                           nb, (int)M, xqs, xd, (int)N, (int)K, y, ldy);
+    return hipGetLastError();
 }
 
 hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,

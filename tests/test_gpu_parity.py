@@ -122,7 +122,7 @@ def test_dequantize_bitexact_golden():
 
 
 # ------------------------------------------------------------------------------- mul_mat vs golden
-@pytest.mark.parametrize("algo", [1, 2])
+@pytest.mark.parametrize("algo", [1, 2, 3])
 def test_mul_mat_golden_llama_slice(algo):
     wq, x = load("avx2", "w4096_q4_0"), load("avx2", "x4096_f32")
     y, _ = gpu_mul_mat(wq, 4096, x, algo=algo)
@@ -132,7 +132,7 @@ def test_mul_mat_golden_llama_slice(algo):
     assert rel < 1e-3
 
 
-@pytest.mark.parametrize("algo", [1, 2])
+@pytest.mark.parametrize("algo", [1, 2, 3])
 def test_mul_mat_golden_falcon_k4544(algo):
     wq, x = load("avx2", "w4544_q4_0"), load("avx2", "x4544_f32")
     y, _ = gpu_mul_mat(wq, 4544, x, algo=algo)
@@ -146,9 +146,13 @@ def test_mul_mat_golden_falcon_k4544(algo):
     (64, 1, 1), (64, 33, 3), (128, 100, 8), (4096, 257, 2), (4544, 4672 // 8, 1), (11008, 96, 4),
     (64, 130, 9), (256, 129, 31), (4096, 128, 33), (4544, 200, 65), (11008, 130, 64), (4096, 64, 100),
 ])
-def test_mul_mat_vs_oracle_edges(K, M, N):
+@pytest.mark.parametrize("algo", [0, 2])
+def test_mul_mat_vs_oracle_edges(K, M, N, algo):
+    """auto (GEMV N <= 8, split-K N <= 128, GEMM above) and the LDS-staged GEMM forced."""
+    if algo == 2 and N <= 8:
+        pytest.skip("GEMV shapes")
     wq, x = make_case(K, M, N, seed=K * 7 + M + N)
-    y, yfull = gpu_mul_mat(wq, K, x)
+    y, yfull = gpu_mul_mat(wq, K, x, algo=algo)
     xq = O.quantize_q8_0(x, "avx2")
     y_ref = O.mul_mat(wq, K, x, nthreads=4)
     _, s_abs = block_terms(wq, xq, K)
@@ -159,9 +163,10 @@ def test_mul_mat_vs_oracle_edges(K, M, N):
 def test_gemv_and_gemm_agree(N):
     wq, x = make_case(4096, 192, N, seed=N)
     y1, _ = gpu_mul_mat(wq, 4096, x, algo=1)
-    y2, _ = gpu_mul_mat(wq, 4096, x, algo=2)
     _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), 4096)
-    check_y(y1, y2, s_abs, RTOL, ATOL_BLOCKS)
+    for algo in (2, 3):
+        y2, _ = gpu_mul_mat(wq, 4096, x, algo=algo)
+        check_y(y1, y2, s_abs, RTOL, ATOL_BLOCKS)
 
 
 @pytest.mark.parametrize("N", [1, 3, 8, 20])
@@ -183,7 +188,7 @@ def test_multi_matrix_siblings_match_single_calls(N):
 
 def test_ldy_stride_and_no_out_of_bounds_writes():
     wq, x = make_case(4096, 100, 3, seed=5)
-    for algo in (1, 2):
+    for algo in (1, 2, 3):
         y, yfull = gpu_mul_mat(wq, 4096, x, algo=algo, ldy=128)
         assert np.all(yfull[:, 100:].view(np.uint32) == 0x7F7F7F7F), "wrote outside [0, M) of a row"
         y_ref = O.mul_mat(wq, 4096, x)
@@ -236,6 +241,19 @@ def test_llama7b_prefill_512_full_shape(K, M):
     # size-independent property: linearity in x (x -> 2x doubles q8 scales exactly)
     y2, _ = gpu_mul_mat(wq, K, 2 * x[:64])
     assert np.array_equal(y2.view(np.uint32), (2 * y[:64]).view(np.uint32))
+
+
+@pytest.mark.parametrize("K,M,N", [(4096, 11008, 64), (11008, 4096, 17)])
+def test_llama7b_small_batch_split_k_full_shape(K, M, N):
+    """Split-K MFMA path (9 <= N <= 128) at full LLaMA shapes; linearity x -> 2x bitwise."""
+    wq, x = make_case(K, M, N, seed=5 * K + M + N)
+    y, _ = gpu_mul_mat(wq, K, x, algo=3)
+    xq = O.quantize_q8_0(x, "avx2")
+    y_ref = O.mul_mat(wq, K, x, nthreads=8, mode="avx2", pool=True)
+    rel, _ = check_y(y, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
+    assert rel < 1e-3
+    y2, _ = gpu_mul_mat(wq, K, 2 * x, algo=3)
+    assert np.array_equal(y2.view(np.uint32), (2 * y).view(np.uint32))
 
 
 # ------------------------------------------------------------------------------- tensor ABI (host tensors)

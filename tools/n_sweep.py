@@ -1,0 +1,53 @@
+"""Per-launch time of one q4_0 mul_mat vs token count N (graph replay over 32 distinct weight
+matrices, > Infinity Cache), for the GEMV (N <= 8) and GEMM paths: where the switch sits and that
+small-batch decode scales.  Usage: python tools/n_sweep.py [K M]"""
+import ctypes
+import json
+import os
+import sys
+
+sys.path[:0] = [os.path.join(os.path.dirname(__file__), "..", "llama.cpp-q_4_0_amd", "python")]
+import ggml_hip as gh  # noqa: E402
+
+L = gh.load()
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+M = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+NMAT = 32
+tmp = gh.DeviceBuffer(K * M * 4)
+ws = []
+for i in range(NMAT):
+    b = gh.DeviceBuffer(18 * K // 32 * M)
+    gh.check(L.ggml_hip_fill_gaussian(tmp.ptr, K * M, 300 + i, 0.0, 0.02, None))
+    gh.check(L.ggml_hip_quantize_q4_0(tmp.ptr, K, M, b.ptr, None))
+    ws.append(b)
+tmp.free()
+NMAX = 512
+x = gh.DeviceBuffer(K * NMAX * 4)
+gh.check(L.ggml_hip_fill_gaussian(x.ptr, K * NMAX, 9, 0.0, 1.0, None))
+y = gh.DeviceBuffer(M * NMAX * 4)
+gh.check(L.ggml_hip_reserve_workspace(K, NMAX))
+s = L.ggml_hip_default_stream()
+rows = []
+for N in (1, 2, 3, 4, 6, 8, 9, 16, 32, 64, 128, 256, 512):
+    for algo in ((1, 2, 3) if N <= 8 else (2, 3)):
+        def run():
+            for w in ws:
+                gh.check(L.ggml_hip_mul_mat_q4_0_ex(w.ptr, K, M, x.ptr, N, y.ptr, M, algo, s))
+        run()
+        gh.check(L.ggml_hip_stream_synchronize(s))
+        g = gh.Graph(s)
+        with g:
+            run()
+        g.launch()
+        gh.check(L.ggml_hip_stream_synchronize(s))
+        a, b = gh.Event(), gh.Event()
+        reps = 10
+        a.record(s)
+        for _ in range(reps):
+            g.launch()
+        b.record(s)
+        t = a.elapsed_ms(b) * 1e-3 / (reps * NMAT)
+        nbytes = 18 * K // 32 * M + 4 * K * N + 4 * M * N
+        rows.append({"N": N, "path": {1: "gemv", 2: "gemm", 3: "gemm_sk"}[algo], "us": round(t * 1e6, 2),
+                     "GBps": round(nbytes / t / 1e9, 1), "TOPs": round(2 * M * K * N / t / 1e12, 2)})
+        print(json.dumps(rows[-1]), flush=True)

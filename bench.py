@@ -39,6 +39,16 @@ LAYER = [("wq", 4096, 4096), ("wk", 4096, 4096), ("wv", 4096, 4096), ("wo", 4096
          ("w1", 4096, 11008), ("w3", 4096, 11008), ("w2", 11008, 4096)]
 
 
+# other BASELINE.json configs measured on one GPU (same kernels): (name, layers, spec, sibling groups)
+EXTRA_CONFIGS = [
+    ("LLaMA-13B decode (config 4 shapes, 1 GPU)", 40,
+     [("wq", 5120, 5120), ("wk", 5120, 5120), ("wv", 5120, 5120), ("wo", 5120, 5120),
+      ("w1", 5120, 13824), ("w3", 5120, 13824), ("w2", 13824, 5120)], [[0, 1, 2], [3], [4, 5], [6]]),
+    ("Falcon-7B decode (config 5 shapes, arch/falcon)", 32,
+     [("wqkv", 4544, 4672), ("wo", 4544, 4544), ("w1", 4544, 18176), ("w2", 18176, 4544)], [[0], [1], [2], [3]]),
+]
+
+
 def q4_bytes(K, M):
     return 18 * K // 32 * M
 
@@ -63,14 +73,15 @@ def setup_dist(n_gpus):
 class Stack:
     """Resident weight stack for one rank: per layer per matrix the rank's row slice."""
 
-    def __init__(self, gh, L, rank, world, layers, seed_base=0x5EED0000):
+    def __init__(self, gh, L, rank, world, layers, seed_base=0x5EED0000, spec=None):
+        spec = LAYER if spec is None else spec
         self.mats = []
         self.bufs = []
-        tmp = gh.DeviceBuffer(max(K * M for _, K, M in LAYER) * 4)
+        tmp = gh.DeviceBuffer(max(K * M for _, K, M in spec) * 4)
         total = 0
         for li in range(layers):
             row = []
-            for mi, (name, K, M) in enumerate(LAYER):
+            for mi, (name, K, M) in enumerate(spec):
                 rb = np.zeros(world + 1, np.int64)
                 gh.check(L.ggml_hip_split_rows(M, world, None, rb.ctypes.data_as(ctypes.c_void_p)))
                 m_loc = int(rb[rank + 1] - rb[rank])
@@ -101,6 +112,7 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no HIP graph (launch-per-call)")
     ap.add_argument("--force-split", action="store_true",
                     help="run the multi-GPU code path (row split + RCCL all-gather) even with one rank")
+    ap.add_argument("--no-extra", action="store_true", help="skip the LLaMA-13B / Falcon-7B decode lines")
     ap.add_argument("--no-batch-siblings", action="store_true",
                     help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
     args = ap.parse_args()
@@ -264,6 +276,9 @@ def main():
         result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
         if not args.no_prefill and args.prefill_tokens > 0:
             result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens)
+        if not args.no_extra:
+            result["other_configs"] = [extra_decode(gh, L, stream, *c, steps=args.steps, warmup=args.warmup)
+                                       for c in EXTRA_CONFIGS]
         if not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
@@ -328,6 +343,49 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
             "avg_launch_us": round(tot_t / nlaunch * 1e6, 3), "per_shape": shapes,
             "timing": "HIP events around graph replays of each launch position's 32 back-to-back launches",
             "bytes_per_launch_def": "sum over the launch's matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y)"}
+
+
+def extra_decode(gh, L, stream, name, n_layers, spec, groups, steps=20, warmup=5):
+    """Decode tok/s of another model's q4_0 matmul stack on this GPU: same graph-replayed launch
+    chain as the headline (siblings batched), distinct weights per layer (> Infinity Cache)."""
+    stack = Stack(gh, L, 0, 1, n_layers, seed_base=0x5EEE0000, spec=spec)
+    Ks = sorted({K for _, K, _ in spec})
+    xs = {K: gh.DeviceBuffer(K * 4) for K in Ks}
+    for K in Ks:
+        gh.check(L.ggml_hip_fill_gaussian(xs[K].ptr, K, 0x5EED1000 + K, 0.0, 1.0, None))
+    yb = {i: gh.DeviceBuffer(spec[i][2] * 4) for i in range(len(spec))}
+    keep = []
+
+    def step():
+        for row in stack.mats:
+            for g in groups:
+                n = len(g)
+                wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
+                yp = (ctypes.c_void_p * n)(*[yb[i].ptr for i in g])
+                mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
+                keep.append((wp, yp, mp))
+                gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, row[g[0]][1], xs[row[g[0]][1]].ptr, 1, yp, stream))
+    step()
+    gh.check(L.ggml_hip_stream_synchronize(stream))
+    g = gh.Graph(stream)
+    with g:
+        step()
+    for _ in range(warmup):
+        g.launch()
+    gh.check(L.ggml_hip_stream_synchronize(stream))
+    a, b = gh.Event(), gh.Event()
+    a.record(stream)
+    for _ in range(steps):
+        g.launch()
+    b.record(stream)
+    t = a.elapsed_ms(b) * 1e-3 / steps
+    nbytes = n_layers * sum(q4_bytes(K, M) + 4 * K + 4 * M for _, K, M in spec)
+    del g
+    for buf in stack.bufs:
+        buf.free()
+    return {"config": name, "tok_s": round(1.0 / t, 2), "ms_per_token": round(t * 1e3, 4),
+            "weights_bytes": stack.total_bytes, "launches_per_layer": len(groups),
+            "GBps": round(nbytes / t / 1e9, 1), "hbm_frac": round(nbytes / t / 1e9 / HBM_PEAK_GBPS, 4)}
 
 
 def run_launch(gh, L, kind, a, xs, stream):

@@ -313,6 +313,7 @@ struct GemvMats {
     int n;
     int M;                                // total rows (= row_begin[n])
     int rstride;                          // rows between a wave's consecutive rows = grid * WAVES
+    int map;                              // row -> (workgroup, wave) mapping, see the kernel
 };
 // Every field is read with a constant index: the kernel's kernargs arrive in one batch of scalar
 // loads and the per-row matrix lookup is a chain of s_cselect, not a dependent kernarg load.
@@ -346,9 +347,25 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
                   ld3 = mats.ldy[3] - mats.ldy[2];
     const int npairs = nb >> 1;
     const int nchunk = (npairs + 63) >> 6;
-    const int rstride = mats.rstride;
-    const int row0 = blockIdx.x * WAVES + wave;
-    const int nrows_w = row0 < M ? (M - 1 - row0) / rstride + 1 : 0;
+    // row -> (workgroup b, wave w) mapping (kernarg `map`):
+    //  0 strided:     rows b*WAVES + w + k*grid*WAVES (16 consecutive rows per workgroup pass)
+    //  1 interleaved: rows (k*WAVES + w)*grid + b
+    //  2 blocked:     workgroup b owns the contiguous range [b*M/grid, (b+1)*M/grid), waves stride 16
+    // With grid a multiple of the CU count, 1 and 2 give every CU floor or ceil of M/grid rows per
+    // workgroup (no CU streams twice the bytes of another at the tail); 0 does when M is a
+    // multiple of grid*WAVES.
+    const int map = mats.map;
+    int row0, rstride, rend;
+    if (map == 2) {
+        row0 = (int)(((int64_t)blockIdx.x * M) / (int)gridDim.x) + wave;
+        rend = (int)(((int64_t)(blockIdx.x + 1) * M) / (int)gridDim.x);
+        rstride = WAVES;
+    } else {
+        row0 = map == 1 ? wave * (int)gridDim.x + blockIdx.x : blockIdx.x * WAVES + wave;
+        rend = M;
+        rstride = mats.rstride;
+    }
+    const int nrows_w = row0 < rend ? (rend - 1 - row0) / rstride + 1 : 0;
     const int nitems = nrows_w * nchunk;                            // (row, chunk) items of this wave
     GEMV_STAMP(0);
 
@@ -531,11 +548,18 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     static const int wg_per_cu = env_int("GGML_HIP_GEMV_WG_PER_CU", 2048 / (WAVES * 64));
     const int64_t M = m.row_begin[m.n];
     const int64_t need = (M + WAVES - 1) / WAVES;
-    const int64_t cap = (int64_t)dev.num_cus * (wg_per_cu < 1 ? 1 : wg_per_cu);
-    const unsigned grid = (unsigned)(need < cap ? need : cap);
+    const int64_t cus = dev.num_cus;
+    const int64_t cap = cus * (wg_per_cu < 1 ? 1 : wg_per_cu);
+    // a multiple of the CU count (balanced per CU) once there is more than one WG's rows per CU
+    const int64_t bal = need <= cus ? need : cus * ((need + cus - 1) / cus);
+    const unsigned grid = (unsigned)(bal < cap ? bal : cap);
+    static const int map_env = env_int("GGML_HIP_GEMV_MAP", -1);
     GemvMats ma = m;
     ma.M = (int)M;
     ma.rstride = (int)grid * WAVES;
+    // strided (contiguous 16-row spans, measured best) when its leftover rows form whole rounds of
+    // one workgroup per CU (then every CU gets the same rows), blocked otherwise
+    ma.map = map_env >= 0 ? map_env : ((M % ((int64_t)grid * WAVES)) % (cus * WAVES) == 0 ? 0 : 2);
     (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR>), dim3(grid), dim3(WAVES * 64), lds, s, ma, rowbytes, nb,
                        x, (int)K);

@@ -545,10 +545,14 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     const size_t lds = (size_t)NT * nb * 40;
-    static const int wg_per_cu = env_int("GGML_HIP_GEMV_WG_PER_CU", 2048 / (WAVES * 64));
+    static const int wg_per_cu_env = env_int("GGML_HIP_GEMV_WG_PER_CU", 0);
     const int64_t M = m.row_begin[m.n];
     const int64_t need = (M + WAVES - 1) / WAVES;
     const int64_t cus = dev.num_cus;
+    // one workgroup per CU while that leaves at most two rows per wave (M <= 2*CUs*WAVES: 8192 on
+    // MI355X), two (full occupancy) above; measured per shape with tools/shape_sweep.py
+    const int wg_per_cu = wg_per_cu_env > 0 ? wg_per_cu_env
+                        : (M <= 2 * cus * WAVES ? 1 : 2048 / (WAVES * 64));
     const int64_t cap = cus * (wg_per_cu < 1 ? 1 : wg_per_cu);
     // a multiple of the CU count (balanced per CU) once there is more than one WG's rows per CU
     const int64_t bal = need <= cus ? need : cus * ((need + cus - 1) / cus);

@@ -321,7 +321,11 @@ struct GemvMats {
 // VAR bit 0 (GLB): weight loads are plain global loads with clamped lane addresses
 // VAR bit 1 (XSPLIT): only the first XW waves load and quantize x; the other waves issue their
 //                     weight loads at once (the x loads enter the CU's queue first)
-template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0>
+// PPL > 0 ("row items", decode, K <= 12288): lane l takes pairs l, l+64, ..., l+64*(PPL-1) of the
+//                     row (PPL = ceil(pairs/64)), so one item is a whole row: all of its loads are
+//                     in flight together and it is reduced once (a row of K=4160 no longer costs two
+//                     items for one extra pair).  PPL == 0: 64-pair chunks, one item per chunk.
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, int64_t rowbytes, int nb,
                                                           const float *__restrict__ x, int K) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -346,7 +350,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     const int64_t l0 = mats.ldy[0], ld1 = mats.ldy[1] - mats.ldy[0], ld2 = mats.ldy[2] - mats.ldy[1],
                   ld3 = mats.ldy[3] - mats.ldy[2];
     const int npairs = nb >> 1;
-    const int nchunk = (npairs + 63) >> 6;
+    const int nchunk = PPL > 0 ? 1 : (npairs + 63) >> 6;
+    constexpr int NPR = PPL > 0 ? PPL : 1;                          // pairs per lane per item
+    struct ItemRegs {
+        PairRegs pr[NPR];
+    };
     // row -> (workgroup b, wave w) mapping (kernarg `map`):
     //  0 strided:     rows b*WAVES + w + k*grid*WAVES (16 consecutive rows per workgroup pass)
     //  1 interleaved: rows (k*WAVES + w)*grid + b
@@ -403,21 +411,28 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     };
     auto item_row = [&](int it) __attribute__((always_inline)) { return row0 + (it / nchunk) * rstride; };
     constexpr bool GLB = (VAR & 1) != 0, XSPLIT = (VAR & 2) != 0;
+    static_assert(PPL == 0 || GLB, "row items use the global-load form");
     auto issue = [&](int it) __attribute__((always_inline)) {
         const bool valid = it < nitems;                             // past the end: zero-size descriptor
         const int r = valid ? item_row(it) : row0;
+        ItemRegs v;
         if constexpr (GLB) {                                        // past the end: one shared address
-            const int pp = 64 * (it % nchunk) + lane;
-            const int pc = valid ? (pp < npairs ? pp : npairs - 1) : 0;
-            return load_pair_g(row_ptr(valid ? r : 0) + 36 * pc);
+            const uint8_t *rp = row_ptr(valid ? r : 0);
+#pragma unroll
+            for (int j = 0; j < NPR; j++) {
+                const int pp = 64 * (PPL > 0 ? j : it % nchunk) + lane;
+                const int pc = valid ? (pp < npairs ? pp : npairs - 1) : 0;
+                v.pr[j] = load_pair_g(rp + 36 * pc);
+            }
         } else {
-            return load_pair(row_ptr(valid ? r : 0), valid ? rowbytes : 0, 64 * (it % nchunk) + lane);
+            v.pr[0] = load_pair(row_ptr(valid ? r : 0), valid ? rowbytes : 0, 64 * (it % nchunk) + lane);
         }
+        return v;
     };
     constexpr bool KO_X = DIAG == 8 || DIAG == 10;      // timing knockouts (results invalid)
     constexpr bool KO_LDS = DIAG == 9 || DIAG == 10;
     u32x4 xv[GEMV_PRO];
-    PairRegs buf[DEPTH];
+    ItemRegs buf[DEPTH];
     if constexpr (XSPLIT) {
         // x-waves: wave < XW load + quantize x (XT threads, PRO float4 each per round), then issue
         // their weight loads; the other waves only issue weight loads
@@ -471,9 +486,12 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     float acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) acc[n] = 0.0f;
-    auto process = [&](const PairRegs &v, int it) __attribute__((always_inline)) {
+    auto process = [&](const ItemRegs &vi, int it) __attribute__((always_inline)) {
         const int chunk = it % nchunk;
-        const int p = 64 * chunk + lane;
+#pragma unroll
+        for (int j = 0; j < NPR; j++) {
+        const PairRegs &v = vi.pr[j];
+        const int p = 64 * (PPL > 0 ? j : chunk) + lane;
         if (p < npairs) {
             // even block 2p: d = a.x[15:0], qs = bytes 2..17 ; odd block 2p+1: d = b.x[31:16], qs = b.y..c
             const float dA = h2f(v.a.x & 0xFFFFu);
@@ -494,6 +512,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
                 acc[n] = fmaf((float)sA, dA * dx.x, acc[n]);
                 acc[n] = fmaf((float)sB, dB * dx.y, acc[n]);
             }
+        }
         }
         if (chunk == nchunk - 1) {                                  // row complete: reduce + store
             const int r = item_row(it);
@@ -517,7 +536,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
         for (int d = 0; d < DEPTH; d++) {
             if (it + d >= nitems) break;
             if (DIAG == 7 && it + d == 0) {                         // when the first weights have landed
-                asm volatile("" ::"v"(buf[0].a), "v"(buf[0].b), "v"(buf[0].c));
+                asm volatile("" ::"v"(buf[0].pr[0].a), "v"(buf[0].pr[0].b), "v"(buf[0].pr[0].c));
                 GEMV_STAMP(4);
             }
             process(buf[d], it + d);
@@ -540,7 +559,7 @@ static int env_int(const char *name, int dflt) {
     return e ? atoi(e) : dflt;
 }
 
-template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0>
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0>
 static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
@@ -551,8 +570,16 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     const int64_t cus = dev.num_cus;
     // one workgroup per CU while that leaves at most two rows per wave (M <= 2*CUs*WAVES: 8192 on
     // MI355X), two (full occupancy) above; measured per shape with tools/shape_sweep.py
-    const int wg_per_cu = wg_per_cu_env > 0 ? wg_per_cu_env
-                        : (M <= 2 * cus * WAVES ? 1 : 2048 / (WAVES * 64));
+    static int occ = 0;                    // resident workgroups per CU for this instantiation
+    if (occ == 0) {
+        int nb_occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>,
+                                                         WAVES * 64, lds) != hipSuccess || nb_occ < 1)
+            nb_occ = 1;
+        occ = nb_occ;
+    }
+    int wg_per_cu = wg_per_cu_env > 0 ? wg_per_cu_env : (M <= 2 * cus * WAVES ? 1 : 2048 / (WAVES * 64));
+    if (wg_per_cu > occ) wg_per_cu = occ;  // never more than can be resident (no second round)
     const int64_t cap = cus * (wg_per_cu < 1 ? 1 : wg_per_cu);
     // a multiple of the CU count (balanced per CU) once there is more than one WG's rows per CU
     const int64_t bal = need <= cus ? need : cus * ((need + cus - 1) / cus);
@@ -565,7 +592,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     // one workgroup per CU (then every CU gets the same rows), blocked otherwise
     ma.map = map_env >= 0 ? map_env : ((M % ((int64_t)grid * WAVES)) % (cus * WAVES) == 0 ? 0 : 2);
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR>), dim3(grid), dim3(WAVES * 64), lds, s, ma, rowbytes, nb,
+    hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>), dim3(grid), dim3(WAVES * 64), lds, s, ma, rowbytes, nb,
                        x, (int)K);
     return hipGetLastError();
 }
@@ -586,6 +613,23 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
         if (diag == 8) return launch_gemv_w<NT, 8, 16, 1>(m, K, x, dev, s);
         if (diag == 9) return launch_gemv_w<NT, 9, 16, 1>(m, K, x, dev, s);
         if (diag == 10) return launch_gemv_w<NT, 10, 16, 1>(m, K, x, dev, s);
+    }
+    if constexpr (NT == 1) {                        // decode: one item per row (PPL pairs per lane)
+        static const int rowitems = env_int("GGML_HIP_GEMV_ROWITEMS", 1);
+        const int ppl = (int)((K / 64 + 63) / 64);
+        if (rowitems && var == 3 && diag == 0) {
+            const int rd = depth_env ? depth_env : 1;
+            switch (ppl) {
+                case 1: return rd == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 1>(m, K, x, dev, s)
+                                       : launch_gemv_w<NT, 0, 16, 2, 3, 1>(m, K, x, dev, s);
+                case 2: return rd == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 2>(m, K, x, dev, s)
+                                       : launch_gemv_w<NT, 0, 16, 2, 3, 2>(m, K, x, dev, s);
+                case 3: return rd == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 3>(m, K, x, dev, s)
+                                       : launch_gemv_w<NT, 0, 16, 2, 3, 3>(m, K, x, dev, s);
+                default: break;                     // K > 12288: chunked items below (measured
+                                                    // equal or faster at 4-5 pairs per lane)
+            }
+        }
     }
     if (var == 0) return depth == 1 ? launch_gemv_w<NT, 0, 16, 1, 0>(m, K, x, dev, s)
                                     : launch_gemv_w<NT, 0, 16, 2, 0>(m, K, x, dev, s);

@@ -588,9 +588,11 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     GemvMats ma = m;
     ma.M = (int)M;
     ma.rstride = (int)grid * WAVES;
-    // strided (contiguous 16-row spans, measured best) when its leftover rows form whole rounds of
-    // one workgroup per CU (then every CU gets the same rows), blocked otherwise
-    ma.map = map_env >= 0 ? map_env : ((M % ((int64_t)grid * WAVES)) % (cus * WAVES) == 0 ? 0 : 2);
+    // strided (contiguous 16-row spans) when its leftover rows form whole rounds of one workgroup per
+    // CU (every CU then gets the same rows); otherwise interleaved at two workgroups per CU and
+    // blocked at one (measured per shape, tools/shape_sweep.py)
+    ma.map = map_env >= 0 ? map_env
+           : ((M % ((int64_t)grid * WAVES)) % (cus * WAVES) == 0 ? 0 : ((int64_t)grid > cus ? 1 : 2));
     (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>), dim3(grid), dim3(WAVES * 64), lds, s, ma, rowbytes, nb,
                        x, (int)K);
@@ -618,7 +620,11 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
         static const int rowitems = env_int("GGML_HIP_GEMV_ROWITEMS", 1);
         const int ppl = (int)((K / 64 + 63) / 64);
         if (rowitems && var == 3 && diag == 0) {
-            const int rd = depth_env ? depth_env : 1;
+            // two rows in flight per wave, except the multi-round strided case (M > 2*CUs*16 with
+            // the leftover rows a whole round per CU, e.g. the fused LLaMA-7B wq|wk|wv, M = 12288)
+            const int64_t M = m.row_begin[m.n], r1 = 2 * (int64_t)dev.num_cus * 16;
+            const bool strided_multi = M > r1 && (M % r1) % (r1 / 2) == 0;
+            const int rd = depth_env ? depth_env : (strided_multi ? 1 : 2);
             switch (ppl) {
                 case 1: return rd == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 1>(m, K, x, dev, s)
                                        : launch_gemv_w<NT, 0, 16, 2, 3, 1>(m, K, x, dev, s);

@@ -336,7 +336,7 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
             src = "profiles/r01_gemv_pmc_traffic.json: 2*FETCH_SIZE+WRITE_SIZE (x1024) per GEMV launch, mean"
         except Exception:
             traffic = None
-    return {"bound": "hbm", "kernel": "k_gemv_q4_0<NT=1> (fused q8_0 quantize + q4_0.q8_0 GEMV; VAR 3, ring depth 1 at K=4096, 2 at K=11008)",
+    return {"bound": "hbm", "kernel": "k_gemv_q4_0<NT=1,...> (fused q8_0 quantize + q4_0.q8_0 GEMV, one row item per wave ring slot)",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": src,
             "algorithmic_bytes_per_launch_mean": round(tot_bytes / nlaunch),

@@ -20,7 +20,7 @@ STEPS=${STEPS:-pytest,smoke,bench,prof}
 [[ $STEPS == *bench* ]] && step bench 600 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-}
 if [[ $STEPS == *prof* ]]; then
     export TMPDIR=/tmp
-    step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu ${BENCH_ARGS:-}
+    step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-extra ${BENCH_ARGS:-}
     find gpurun_out/prof -name "*kernel_stats.csv" | head -3
 fi
 exit 0

@@ -893,6 +893,14 @@ int ggml_hip_debug_gemv_stamps(unsigned long long *host, int n) {
     return GGML_HIP_OK;
 }
 
+// not in the public header: tests force each GEMV launch policy (all must give the same y)
+int ggml_hip_debug_set_gemv_policy(int map, int depth, int rowitems, int wg_per_cu) {
+    if (map < -1 || map > 2 || depth < 0 || depth > 2 || rowitems < 0 || rowitems > 1 || wg_per_cu < 0)
+        return fail(GGML_HIP_ERR_INVALID, "bad GEMV policy");
+    ghip::gemv_set_policy(map, depth, rowitems, wg_per_cu);
+    return GGML_HIP_OK;
+}
+
 int ggml_hip_debug_gemm_stamps(unsigned long long *host, int n) {
     HIP_RET(ghip::gemm_read_stamps(host, n));
     return GGML_HIP_OK;

@@ -41,6 +41,10 @@ constexpr int GEMV_MULTI_MAX = 4;
 hipError_t gemv_q4_0_multi(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *x, int64_t N,
                            float *const *y, const int64_t *ldy, const DeviceInfo &dev, hipStream_t s);
 
+// test hook: force the GEMV launch policy (row mapping 0/1/2, ring depth 1/2, row items 0/1,
+// workgroups per CU); -1 / 0 = automatic
+void gemv_set_policy(int map, int depth, int rowitems, int wg_per_cu);
+
 // diagnostic: copy the per-wave phase stamps of the last GGML_HIP_GEMV_DIAG=7 launch
 hipError_t gemv_read_stamps(unsigned long long *host, int n);
 hipError_t gemm_read_stamps(unsigned long long *host, int n);

@@ -547,6 +547,26 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     GEMV_STAMP(6);
 }
 
+static int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+// GEMV launch policy overrides: -1 / 0 = automatic.  Initialised from the environment
+// (GGML_HIP_GEMV_MAP / _DEPTH / _ROWITEMS / _WG_PER_CU) and settable at run time by the
+// non-header debug entry point ggml_hip_debug_set_gemv_policy (tests sweep every path).
+struct GemvPolicy {
+    int map, depth, rowitems, wg_per_cu;
+};
+static GemvPolicy &gemv_policy() {
+    static GemvPolicy p = {env_int("GGML_HIP_GEMV_MAP", -1), env_int("GGML_HIP_GEMV_DEPTH", 0),
+                           env_int("GGML_HIP_GEMV_ROWITEMS", 1), env_int("GGML_HIP_GEMV_WG_PER_CU", 0)};
+    return p;
+}
+void gemv_set_policy(int map, int depth, int rowitems, int wg_per_cu) {
+    gemv_policy() = {map, depth, rowitems, wg_per_cu};
+}
+
 int gemv_max_tokens(int64_t K) {
     const int64_t nb = K / QK;
     int nt = 8;
@@ -554,17 +574,13 @@ int gemv_max_tokens(int64_t K) {
     return nt;
 }
 
-static int env_int(const char *name, int dflt) {
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
 
 template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0>
 static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     const size_t lds = (size_t)NT * nb * 40;
-    static const int wg_per_cu_env = env_int("GGML_HIP_GEMV_WG_PER_CU", 0);
+    const int wg_per_cu_env = gemv_policy().wg_per_cu;
     const int64_t M = m.row_begin[m.n];
     const int64_t need = (M + WAVES - 1) / WAVES;
     const int64_t cus = dev.num_cus;
@@ -584,7 +600,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     // a multiple of the CU count (balanced per CU) once there is more than one WG's rows per CU
     const int64_t bal = need <= cus ? need : cus * ((need + cus - 1) / cus);
     const unsigned grid = (unsigned)(bal < cap ? bal : cap);
-    static const int map_env = env_int("GGML_HIP_GEMV_MAP", -1);
+    const int map_env = gemv_policy().map;
     GemvMats ma = m;
     ma.M = (int)M;
     ma.rstride = (int)grid * WAVES;
@@ -607,7 +623,7 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
     // GGML_HIP_GEMV_DIAG=7 the phase-stamp build, 8/9/10 the timing knockouts (invalid results).
     static const int diag = env_int("GGML_HIP_GEMV_DIAG", 0);
     static const int var = env_int("GGML_HIP_GEMV_VAR", 3);
-    static const int depth_env = env_int("GGML_HIP_GEMV_DEPTH", 0);
+    const int depth_env = gemv_policy().depth;
     const int depth = depth_env ? depth_env : (K / 64 > 64 ? 2 : 1);
     if constexpr (NT == 1) {
         if (diag == 7) return depth == 1 ? launch_gemv_w<NT, 7, 16, 1, 3>(m, K, x, dev, s)
@@ -617,7 +633,7 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
         if (diag == 10) return launch_gemv_w<NT, 10, 16, 1>(m, K, x, dev, s);
     }
     if constexpr (NT == 1) {                        // decode: one item per row (PPL pairs per lane)
-        static const int rowitems = env_int("GGML_HIP_GEMV_ROWITEMS", 1);
+        const int rowitems = gemv_policy().rowitems;
         const int ppl = (int)((K / 64 + 63) / 64);
         if (rowitems && var == 3 && diag == 0) {
             // two rows in flight per wave, except the multi-round strided case (M > 2*CUs*16 with

@@ -378,3 +378,31 @@ def test_split_multi_single_rank_rccl(N, Ms):
             assert np.array_equal(yd.download((N, M), np.float32).view(np.uint32), single.view(np.uint32))
     finally:
         L.ggml_hip_comm_destroy(comm)
+
+
+# ------------------------------------------------------------------------------- GEMV launch policies
+@pytest.mark.parametrize("K,M,N", [(4096, 4544, 1), (4544, 4672, 1), (4096, 12288, 1), (11008, 300, 1),
+                                   (13824, 333, 1), (4096, 9000, 2), (64, 37, 3)])
+def test_gemv_launch_policies_bitwise_identical(K, M, N):
+    """Every GEMV launch policy (row mapping strided / interleaved / blocked, ring depth 1 / 2, row
+    items on / off, 1 / 2 workgroups per CU) does the same per-row fp32 arithmetic in the same
+    order: y must be bitwise identical across all of them, and within the bound of the oracle."""
+    L = ggml_hip.load()
+    L.ggml_hip_debug_set_gemv_policy.argtypes = [ctypes.c_int] * 4
+    wq, x = make_case(K, M, N, seed=K + 3 * M + N)
+    ref = None
+    try:
+        for mp in (0, 1, 2):
+            for depth in (1, 2):
+                for rowitems in (0, 1):
+                    for wg in (1, 2):
+                        ggml_hip.check(L.ggml_hip_debug_set_gemv_policy(mp, depth, rowitems, wg), "policy")
+                        y, _ = gpu_mul_mat(wq, K, x, algo=1)
+                        if ref is None:
+                            ref = y
+                            _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
+                            check_y(y, O.mul_mat(wq, K, x, nthreads=8), s_abs, RTOL, ATOL_BLOCKS)
+                        else:
+                            assert np.array_equal(y.view(np.uint32), ref.view(np.uint32)), (mp, depth, rowitems, wg)
+    finally:
+        ggml_hip.check(L.ggml_hip_debug_set_gemv_policy(-1, 0, 1, 0), "policy reset")

@@ -30,3 +30,10 @@ names = ["start", "issued", "quantized", "barrier", "W landed", "item0 done", "e
 for j, nm in enumerate(names):
     v = (s[:, j] - t0) * 10 / 1000.0   # 100 MHz -> us
     print(f"{nm:12s} min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f} us")
+# by wave role: x-waves (wave index < XW within the workgroup) vs the others
+XW = int(os.environ.get("XW", 4))
+wave_in_wg = np.arange(s.shape[0]) % 16
+for role, sel in (("x-waves", wave_in_wg < XW), ("row-only", wave_in_wg >= XW)):
+    for j in (4, 6):
+        v = (s[sel, j] - t0) * 10 / 1000.0
+        print(f"{role:9s} {names[j]:10s} med {np.median(v):6.2f} p90 {np.percentile(v, 90):6.2f} max {v.max():6.2f} us")

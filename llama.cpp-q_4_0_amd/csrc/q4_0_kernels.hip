@@ -1179,6 +1179,204 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm6_q4_0(const uint8_t *__r
 }
 
 // ---------------------------------------------------------------------------------------------
+// GEMM v7: v6's tile, MFMAs and epilogue, with the activations (75 % of a stage's bytes, already
+// int8) moved global -> LDS by LDS-DMA (`buffer_load_dwordx4 ... lds`, d_x by `buffer_load_dword
+// ... lds`) into a 4-stage ring, so no registers hold them; the weights keep register staging
+// (their nibbles are unpacked on the way into LDS) with THREE stages in flight in named register
+// sets.  Per stage and thread exactly G7_OPS vector-memory operations are issued (past-the-end
+// stages through zero-size descriptors), so one counted `s_waitcnt vmcnt(2*G7_OPS)` before the raw
+// `s_barrier` retires stage s+1 while stages s+2 and s+3 stay in flight across it (an LDS-DMA is a
+// pending LDS write on the VM counter: `__syncthreads()` would drain it).  The LDS-DMA image is
+// lane-linear per wave instruction (1 KiB); the XOR half-swap of the operand reads is produced by
+// choosing each lane's SOURCE address.
+static constexpr int G7_NX = 4;                                  // activation ring depth (stages)
+static constexpr int G7_X = GM_KB * GM_BN * 32;                  // int8 acts   [KB][BN][32]  16 KB
+static constexpr int G7_XD = GM_KB * GM_BN * 4;                  // f32 d_x     [KB][BN]       2 KB
+static constexpr int G7_W = GM_KB * GM_BM * 32;                  // int8 weights [KB][BM][32]  8 KB
+static constexpr int G7_WD = GM_KB * GM_BM * 2;                  // fp16 d_w    [KB][BM]
+static constexpr int G7_LDS = G7_NX * (G7_X + G7_XD) + 2 * (G7_W + G7_WD);   // 89 KB
+static constexpr int G7_OPS = 3 + 2 + 1;                        // per thread per stage: W pair, 2 x glds, d_x glds
+static_assert(G7_X / 1024 == 2 * GM_WAVES, "two 1-KiB activation DMA instructions per wave per stage");
+static_assert(G7_XD / 256 == GM_WAVES, "one 256-B d_x DMA instruction per wave per stage");
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+struct G7W {
+    u32x4 wa, wb;
+    uint32_t wc;
+};
+
+__global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes, int nb,
+                                                               int M, const int8_t *__restrict__ xqs,
+                                                               const float *__restrict__ xd, int N, int K,
+                                                               float *__restrict__ y, int64_t ldy) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *xring = smem;                                          // [NX][X]
+    float *xdring = reinterpret_cast<float *>(smem + G7_NX * G7_X);    // [NX][KB][BN]
+    uint8_t *wbuf = smem + G7_NX * (G7_X + G7_XD);                  // [2][W]
+    uint16_t *wdbuf = reinterpret_cast<uint16_t *>(wbuf + 2 * G7_W);   // [2][KB][BM]
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave & 1, wt = wave >> 1;
+    const int c = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.x * GM_BM;
+    const int n0 = blockIdx.y * GM_BN;
+
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W + (int64_t)m0 * rowbytes, (uint32_t)((int64_t)(M - m0) * rowbytes));
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)(N - n0) * K));
+    const __amdgpu_buffer_rsrc_t drs = make_rsrc(xd + (int64_t)n0 * nb, (uint32_t)((int64_t)(N - n0) * nb * 4));
+    const __amdgpu_buffer_rsrc_t nul = make_rsrc(W, 0);
+    const int sr = tid >> 3, sb = (tid >> 1) & 3, sh = tid & 1;     // weight staging role (as v6)
+
+    // activation DMA: this wave's instructions j = 2*wave, 2*wave+1 of the stage; instruction j fills
+    // LDS bytes [j KiB, (j+1) KiB) = block j/4, tokens 32*(j%4) .. +31; lane i lands at slot i =
+    // (token 32*(j%4) + i/2, physical half i&1) and therefore loads logical half (i&1) ^ ((t>>3)&1)
+    int xsrc[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int j = 2 * wave + q;
+        const int t = 32 * (j & 3) + (lane >> 1);
+        const int hh = (lane & 1) ^ ((t >> 3) & 1);
+        xsrc[q] = t * K + (j >> 2) * QK + 16 * hh;                  // + kb0*32 per stage
+    }
+    // d_x DMA: wave w fills [block w/2][tokens 64*(w&1) .. +63] (f32)
+    const int dsrc = ((64 * (wave & 1) + lane) * nb + (wave >> 1)) * 4;   // + kb0*4 per stage
+
+    auto issue = [&](int st, G7W &g) __attribute__((always_inline)) {
+        const int kb0 = st * GM_KB;
+        const bool valid = kb0 < nb;                                // past the end: no traffic
+        const __amdgpu_buffer_rsrc_t wr_ = valid ? wrs : nul;
+        const int woff = (int)(sr * rowbytes) + (kb0 + (sb & ~1)) * Q4B;
+        g.wa = __builtin_amdgcn_raw_buffer_load_b128(wr_, woff, 0, 0);
+        g.wb = __builtin_amdgcn_raw_buffer_load_b128(wr_, woff + 16, 0, 0);
+        g.wc = __builtin_amdgcn_raw_buffer_load_b32(wr_, woff + 32, 0, 0);
+        const int slot = st & (G7_NX - 1);
+        const __amdgpu_buffer_rsrc_t xr_ = valid ? xrs : nul;
+        const __amdgpu_buffer_rsrc_t dr_ = valid ? drs : nul;
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr_, (lds_void_t *)(xring + slot * G7_X + (2 * wave + q) * 1024), 16,
+                                                     xsrc[q] + kb0 * QK, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(dr_, (lds_void_t *)(xdring + slot * (G7_XD / 4) + wave * 64), 4,
+                                                 dsrc + kb0 * 4, 0, 0, 0);
+    };
+    auto write_w = [&](int st, const G7W &g) __attribute__((always_inline)) {
+        const int kb0 = st * GM_KB;
+        uint8_t *ws = wbuf + (st & 1) * G7_W;
+        uint16_t *wds = wdbuf + (st & 1) * (G7_WD / 2);
+        const bool odd = sb & 1;
+        const uint32_t q0 = odd ? g.wb.y : __builtin_amdgcn_alignbyte(g.wa.y, g.wa.x, 2);
+        const uint32_t q1 = odd ? g.wb.z : __builtin_amdgcn_alignbyte(g.wa.z, g.wa.y, 2);
+        const uint32_t q2 = odd ? g.wb.w : __builtin_amdgcn_alignbyte(g.wa.w, g.wa.z, 2);
+        const uint32_t q3 = odd ? g.wc : __builtin_amdgcn_alignbyte(g.wb.x, g.wa.w, 2);
+        u32x4 t;
+        t.x = nib_to_i8x4(q0, 4 * sh); t.y = nib_to_i8x4(q1, 4 * sh);
+        t.z = nib_to_i8x4(q2, 4 * sh); t.w = nib_to_i8x4(q3, 4 * sh);
+        *reinterpret_cast<u32x4 *>(ws + sb * GM_BM * 32 + gm_half_off(sr, sh)) = t;
+        if (sh == 0) {
+            const uint32_t d16 = odd ? (g.wb.x >> 16) : (g.wa.x & 0xFFFFu);
+            wds[sb * GM_BM + sr] = (uint16_t)((kb0 + sb < nb) ? d16 : 0u);
+        }
+    };
+
+    const int tok = 32 * wt + c;
+    const int wrow = 32 * wr + c;
+    auto ld_ops = [&](int st, int b) __attribute__((always_inline)) {
+        const uint8_t *xs = xring + (st & (G7_NX - 1)) * G7_X;
+        const float *xds = xdring + (st & (G7_NX - 1)) * (G7_XD / 4);
+        const uint8_t *ws = wbuf + (st & 1) * G7_W;
+        const uint16_t *wds = wdbuf + (st & 1) * (G7_WD / 2);
+        G6Ops o;
+        o.a = *reinterpret_cast<const i32x4 *>(xs + b * GM_BN * 32 + gm_half_off(tok, h));
+        o.b = *reinterpret_cast<const i32x4 *>(ws + b * GM_BM * 32 + gm_half_off(wrow, h));
+        o.sx = f2h(xds[b * GM_BN + tok]);                          // exact: d_x is an fp16 value
+        o.sw = wds[b * GM_BM + wrow];
+        return o;
+    };
+    const int mg = 0x4B400000;
+    const i32x16 im = {mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg};
+    const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    auto mfma2 = [&](const G6Ops &o, i32x16 &S, f32x16 &P) __attribute__((always_inline)) {
+        S = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a, o.b, im, 0, 0, 0);
+        const u32x4 as = {h == 0 ? o.sx : 0u, 0u, 0u, 0u};
+        const u32x4 bs = {h == 0 ? o.sw : 0u, 0u, 0u, 0u};
+        P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs), fz,
+                                                   0, 0, 0);
+    };
+    float acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+    auto epi = [&](const i32x16 &S, const f32x16 &P) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc[i] = fmaf(__int_as_float(S[i]) - 12582912.0f, P[i], acc[i]);
+    };
+    i32x16 S0, S1 = im;
+    f32x16 P1 = fz, P0;
+    auto compute = [&](int st) __attribute__((always_inline)) {
+        G6Ops o0 = ld_ops(st, 0);
+        G6Ops o1 = ld_ops(st, 1);
+        mfma2(o0, S0, P0);
+        epi(S1, P1);                          // previous stage's block 3 (S = bias, P = 0 on the first)
+        o0 = ld_ops(st, 2);
+        mfma2(o1, S1, P1);
+        epi(S0, P0);
+        o1 = ld_ops(st, 3);
+        mfma2(o0, S0, P0);
+        epi(S1, P1);
+        mfma2(o1, S1, P1);
+        epi(S0, P0);
+    };
+    auto sync = [&]() __attribute__((always_inline)) {   // retire stage s+1 (and the ds_writes), keep s+2, s+3
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * G7_OPS) : "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+
+    const int nstages = (nb + GM_KB - 1) / GM_KB;
+    G7W g0, g1, g2;
+    issue(0, g0);
+    issue(1, g1);
+    issue(2, g2);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G7_OPS) : "memory");   // stage 0 landed
+    write_w(0, g0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // iteration s: issue s+3 into the register set stage s used, compute s, retire s+1 + write its
+    // weights, barrier.  Register sets rotate g0 -> g1 -> g2 (unrolled by 3).
+    for (int s = 0; s < nstages; s += 3) {
+        issue(s + 3, g0);
+        compute(s);
+        if (s + 1 >= nstages) break;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G7_OPS) : "memory");
+        write_w(s + 1, g1);
+        sync();
+        issue(s + 4, g1);
+        compute(s + 1);
+        if (s + 2 >= nstages) break;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G7_OPS) : "memory");
+        write_w(s + 2, g2);
+        sync();
+        issue(s + 5, g2);
+        compute(s + 2);
+        if (s + 3 >= nstages) break;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G7_OPS) : "memory");
+        write_w(s + 3, g0);
+        sync();
+    }
+    epi(S1, P1);                              // the last block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may outlive the workgroup
+
+    const int row = m0 + wrow;
+    if (row < M) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int t = n0 + 32 * wt + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (t < N) y[(int64_t)t * ldy + row] = acc[i];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Split-K MFMA GEMM for small / medium token counts (9 <= N <= 128 by default).
 //
 // The LDS-staged GEMM above runs (M/64) x ceil(N/128) workgroups that each walk all of K, so for
@@ -1320,7 +1518,20 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
     // GGML_HIP_GEMM_DIAG (diagnostic builds): 1 integer epilogue, 2 no MFMA, 3 no global loads,
     // 4 no LDS staging
     static const int diag = env_int("GGML_HIP_GEMM_DIAG", 0);
-    static const int ver = env_int("GGML_HIP_GEMM_V", 6);
+    static const int ver = env_int("GGML_HIP_GEMM_V", 7);
+    if (ver == 7 && diag == 0) {
+        static bool attr7 = false;
+        if (!attr7) {
+            hipError_t e = hipFuncSetAttribute((const void *)k_gemm7_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               G7_LDS);
+            if (e != hipSuccess) return e;
+            attr7 = true;
+        }
+        (void)hipGetLastError();  // report only this launch's error
+        hipLaunchKernelGGL(k_gemm7_q4_0, grid, dim3(GM_THREADS), G7_LDS, s, (const uint8_t *)W, rowbytes, nb, (int)M,
+                           xqs, xd, (int)N, (int)K, y, ldy);
+        return hipGetLastError();
+    }
     if (ver == 6) {
         // v6 diagnostics (GGML_HIP_GEMM_DIAG): 1 no epilogue VALU, 3 no global loads, 5 phase stamps,
         // 6/7 compute phase only (cvt / default epilogue).  GGML_HIP_GEMM_V=5: the previous kernel.

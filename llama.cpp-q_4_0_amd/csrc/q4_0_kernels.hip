@@ -236,18 +236,19 @@ hipError_t dequantize_q4_0(const void *wq, int64_t K, int64_t M, float *w, hipSt
 // ---------------------------------------------------------------------------------------------
 // GEMV (decode, N <= 8).
 //
-// Lane p of a wave owns block pair p of a 64-pair chunk of one weight row.  A pair is 36 bytes
-// (9 dwords): the 18-byte blocks of a row start 4-byte aligned every second block, so a pair
-// is always dword aligned and the 64 lanes of one load read 2,304 contiguous bytes (a whole
-// K=4096 row).  Loads are buffer_load_dwordx4/x4/x1 through the row's descriptor
-// (out-of-row lanes read 0, no fault).  The even block's qs are re-aligned with
-// v_alignbyte_b32.  x is quantized once per workgroup into LDS (q8_0 ints + fp32 d +
-// 8*sum(q)); the q4_0 nibbles enter v_dot4c_i32_i8 unsigned (0..15) and the -8 offset is
-// applied once per block as -8*sum(q):  sum((n-8)*q) = sum(n*q) - 8*sum(q).
+// Lane p of a wave owns block pair p of a weight row (and p+64, p+128, ... with row items).  A
+// pair is 36 bytes (9 dwords): the 18-byte blocks of a row start 4-byte aligned every second
+// block, so a pair is always dword aligned and the 64 lanes of one load read 2,304 contiguous
+// bytes (a whole K=4096 row).  Production loads are global_load_dwordx4/x4/x1 with clamped lane
+// addresses (VAR bit 0); the descriptor form (out-of-row lanes read 0) is the VAR 0 A/B arm.  The
+// even block's qs are re-aligned with v_alignbyte_b32.  x is quantized once per workgroup into
+// LDS (q8_0 ints + fp32 d + 8*sum(q)); the q4_0 nibbles enter v_dot4c_i32_i8 unsigned (0..15)
+// and the -8 offset is applied once per block as -8*sum(q):  sum((n-8)*q) = sum(n*q) - 8*sum(q).
 //
-// Schedule: the activation loads are issued first, then the wave's first weight chunk, so
-// the q8_0 prologue overlaps the first HBM round trip; after the prologue each wave walks its
-// (row, chunk) items with the next chunk's loads in flight while the current one computes.
+// Schedule: the x-waves load + quantize x while every other wave already streams its first
+// DEPTH items; after the barrier each wave walks its items (whole rows with PPL > 0, 64-pair
+// chunks otherwise) with DEPTH items in flight.  Launch policy (grid, row mapping, depth, row
+// items) in launch_gemv_w / launch_gemv; every policy gives bitwise-identical results.
 
 static constexpr int GEMV_LDS_MAX = 64 * 1024;
 // diagnostic build (GGML_HIP_GEMV_DIAG=7): per-wave s_memrealtime stamps of the phases
@@ -260,6 +261,10 @@ __device__ unsigned long long g_gemv_stamps[8192 * 8];
         }                                                                                        \
     } while (0)
 static constexpr int GEMV_PRO = 4;          // activation float4 loads in flight per thread
+#ifndef GEMV_XPRO_DEF
+#define GEMV_XPRO_DEF 4
+#endif
+static constexpr int GEMV_XPRO = GEMV_XPRO_DEF;   // per x-wave thread in the split prologue
 static constexpr int GEMV_MAXMAT = 4;       // sibling matrices per launch
 
 __device__ __forceinline__ int dot_q4_q8(uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3,
@@ -436,16 +441,17 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     if constexpr (XSPLIT) {
         // x-waves: wave < XW load + quantize x (XT threads, PRO float4 each per round), then issue
         // their weight loads; the other waves only issue weight loads
-        const int XW0 = (total + 64 * GEMV_PRO - 1) / (64 * GEMV_PRO);
+        const int XW0 = (total + 64 * GEMV_XPRO - 1) / (64 * GEMV_XPRO);
         const int XW = XW0 < WAVES ? XW0 : WAVES;
         const int XT = XW * 64;
         if (wave < XW) {
-            for (int base = 0; base < total; base += GEMV_PRO * XT) {
+            u32x4 xw[GEMV_XPRO];
+            for (int base = 0; base < total; base += GEMV_XPRO * XT) {
 #pragma unroll
-                for (int i = 0; i < GEMV_PRO; i++)
-                    xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * XT), 0, 0);
+                for (int i = 0; i < GEMV_XPRO; i++)
+                    xw[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * XT), 0, 0);
 #pragma unroll
-                for (int i = 0; i < GEMV_PRO; i++) quantize_into_lds(xv[i], base + tid + i * XT);
+                for (int i = 0; i < GEMV_XPRO; i++) quantize_into_lds(xw[i], base + tid + i * XT);
             }
             asm volatile("" ::: "memory");                          // weight loads stay behind x
 #pragma unroll
@@ -481,8 +487,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     if (!KO_X) __syncthreads();
     GEMV_STAMP(3);
 
-    // ---- COMPUTE: stream the wave's (row, chunk) items with one item in flight.  Two named
-    // register sets (no register copies: a copy would force a wait on the in-flight loads).
+    // ---- COMPUTE: stream the wave's items with DEPTH items in flight in a ring of named register
+    // sets (no register copies: a copy would force a wait on the in-flight loads).
     float acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) acc[n] = 0.0f;

@@ -94,6 +94,14 @@ bool   ggml_hip_compute_forward(struct ggml_compute_params *params, struct ggml_
 /* ggml_cpu_has_cublas (ggml.c:19465-19470) equivalent: 1 when a HIP device is usable. */
 int    ggml_cpu_has_hipblas(void);
 
+/* Device weight-residency cache.  A CPU-backend Q4_0 src0 (the arch/
+ * frontends never call transform_tensor; the reference re-uploads it every call,
+ * ggml-cuda.cu:2496-2502) is uploaded once per device and reused while a sampled fingerprint of
+ * its bytes is unchanged; LRU under GGML_HIP_WEIGHT_CACHE_MB (default 65536), off with
+ * GGML_HIP_WEIGHT_CACHE=0.  Counters since the last clear; clear frees every cached copy. */
+int    ggml_hip_weight_cache_stats(int64_t *hits, int64_t *misses, int64_t *resident_bytes);
+int    ggml_hip_weight_cache_clear(void);
+
 /* ------------------------------------------------------------------------------------------
  * Tensor-free entry points (device pointers, stream-ordered on `stream` = hipStream_t or NULL
  * for the backend's stream on the current device).  Return enum ggml_hip_status.

@@ -22,6 +22,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ggml_abi.h"
@@ -185,6 +186,99 @@ int reserve_workspace(int id, size_t bytes) {
 bool aligned(const void *p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
 // ------------------------------------------------------------------------------------------
+// Device weight-residency cache for CPU-backend Q4_0 weights.  The arch/
+// frontends never call transform_tensor, so the reference re-uploads src0 on every batched
+// mul_mat (ggml-cuda.cu:2496-2502).  Here a host weight slice is uploaded once per device and
+// reused while a sampled fingerprint of its bytes is unchanged (a slice rewritten in place, or a
+// freed and reallocated buffer at the same address, is uploaded again).  LRU eviction under a byte
+// budget (GGML_HIP_WEIGHT_CACHE_MB, default 65536); GGML_HIP_WEIGHT_CACHE=0 disables it.  Every
+// tensor-ABI call ends with a stream synchronize, so an entry not used by the current call is never
+// referenced by a kernel still in flight when it is evicted.
+
+struct WCacheEntry {
+    void *dev = nullptr;
+    size_t bytes = 0;
+    uint64_t fp = 0;
+    uint64_t last_use = 0;
+};
+struct WCacheKey {
+    const void *host;
+    size_t bytes;
+    int device;
+    bool operator==(const WCacheKey &o) const { return host == o.host && bytes == o.bytes && device == o.device; }
+};
+struct WCacheHash {
+    size_t operator()(const WCacheKey &k) const {
+        return std::hash<const void *>()(k.host) ^ (k.bytes * 0x9E3779B97F4A7C15ull) ^ (size_t)k.device;
+    }
+};
+std::mutex g_wc_mu;
+std::unordered_map<WCacheKey, WCacheEntry, WCacheHash> g_wc;
+size_t g_wc_resident = 0;
+uint64_t g_wc_clock = 0, g_wc_hits = 0, g_wc_misses = 0;
+
+bool wcache_enabled() {
+    static const bool on = !getenv("GGML_HIP_WEIGHT_CACHE") || atoi(getenv("GGML_HIP_WEIGHT_CACHE")) != 0;
+    return on;
+}
+size_t wcache_budget() {
+    static const size_t mb = getenv("GGML_HIP_WEIGHT_CACHE_MB") ? (size_t)atoll(getenv("GGML_HIP_WEIGHT_CACHE_MB")) : 65536;
+    return mb << 20;
+}
+
+// FNV-1a over the first and last 32 bytes and 64 evenly spaced 8-byte samples
+uint64_t wcache_fingerprint(const uint8_t *p, size_t n) {
+    uint64_t h = 1469598103934665603ull ^ n;
+    auto mix = [&](const uint8_t *q, size_t len) {
+        for (size_t i = 0; i < len; i++) h = (h ^ q[i]) * 1099511628211ull;
+    };
+    mix(p, std::min<size_t>(32, n));
+    if (n > 32) mix(p + n - 32, 32);
+    if (n >= 64 * 8)
+        for (int i = 0; i < 64; i++) mix(p + (n / 64) * (size_t)i + (n / 128), 8);
+    return h;
+}
+
+// device copy of host bytes [host, host+bytes) on device id (current device = id), uploaded on
+// stream s on a miss; call_id marks entries in use by the current call (never evicted by it)
+const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, uint64_t call_id) {
+    const uint64_t fp = wcache_fingerprint((const uint8_t *)host, bytes);
+    std::lock_guard<std::mutex> lk(g_wc_mu);
+    const WCacheKey key{host, bytes, id};
+    auto it = g_wc.find(key);
+    if (it != g_wc.end() && it->second.fp == fp) {
+        it->second.last_use = call_id;
+        g_wc_hits++;
+        return it->second.dev;
+    }
+    g_wc_misses++;
+    if (it != g_wc.end()) {                                        // stale: same address, new bytes
+        HIP_FATAL(hipFree(it->second.dev));
+        g_wc_resident -= it->second.bytes;
+        g_wc.erase(it);
+    }
+    while (g_wc_resident + bytes > wcache_budget()) {             // LRU eviction
+        auto victim = g_wc.end();
+        for (auto e = g_wc.begin(); e != g_wc.end(); ++e)
+            if (e->second.last_use != call_id && (victim == g_wc.end() || e->second.last_use < victim->second.last_use))
+                victim = e;
+        if (victim == g_wc.end()) break;                           // everything is in use: over budget
+        HIP_FATAL(hipFree(victim->second.dev));
+        g_wc_resident -= victim->second.bytes;
+        g_wc.erase(victim);
+    }
+    WCacheEntry e;
+    e.bytes = bytes;
+    e.fp = fp;
+    e.last_use = call_id;
+    HIP_FATAL(hipMalloc(&e.dev, bytes));
+    HIP_FATAL(hipMemcpyAsync(e.dev, host, bytes, hipMemcpyHostToDevice, s));
+    g_wc_resident += bytes;
+    g_wc[key] = e;
+    return e.dev;
+}
+
+// ------------------------------------------------------------------------------------------
 // the mul_mat core (device pointers): ggml_compute_forward_mul_mat_q_f32 INIT + COMPUTE
 
 int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, float *y, int64_t ldy, int algo,
@@ -303,6 +397,11 @@ void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor 
     const bool dst_dev = dst->backend == gabi::BACKEND_GPU;
     const size_t wrow = (size_t)(K / QK) * Q4B;
     const int saved = current_device();
+    uint64_t call_id;
+    {
+        std::lock_guard<std::mutex> lk(g_wc_mu);
+        call_id = ++g_wc_clock;
+    }
 
     for (int id = 0; id < g_device_count; id++) {
         if (!split && id != g_main_device) continue;
@@ -326,6 +425,9 @@ void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor 
             if (src0_dev) {
                 const auto *ex = (const ggml_tensor_extra_gpu *)src0->extra;
                 w = (const char *)ex->data_device[id] + (size_t)b * rows * wrow;
+            } else if (wcache_enabled()) {
+                w = wcache_get(id, (const char *)src0->data + (size_t)b * src0->nb[2] + lo * wrow, rows * wrow, s,
+                               call_id);
             } else {
                 void *p = tmp_alloc(rows * wrow);
                 HIP_FATAL(hipMemcpyAsync(p, (const char *)src0->data + (size_t)b * src0->nb[2] + lo * wrow, rows * wrow,
@@ -749,6 +851,28 @@ int ggml_hip_mul_mat_q4_0_split_multi(ggml_hip_comm *c, int n, const void *const
         }
     }
     NCCL_RET(ncclGroupEnd());
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_weight_cache_stats(int64_t *hits, int64_t *misses, int64_t *resident_bytes) {
+    std::lock_guard<std::mutex> lk(g_wc_mu);
+    if (hits) *hits = (int64_t)g_wc_hits;
+    if (misses) *misses = (int64_t)g_wc_misses;
+    if (resident_bytes) *resident_bytes = (int64_t)g_wc_resident;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_weight_cache_clear(void) {
+    ensure_init();
+    std::lock_guard<std::mutex> lk(g_wc_mu);
+    for (int id = 0; id < g_device_count; id++) {
+        HIP_RET(hipSetDevice(id));
+        HIP_RET(hipStreamSynchronize(g_dev[id].stream));
+    }
+    for (auto &e : g_wc) HIP_RET(hipFree(e.second.dev));
+    g_wc.clear();
+    g_wc_resident = 0;
+    g_wc_hits = g_wc_misses = 0;
     return GGML_HIP_OK;
 }
 

@@ -406,3 +406,43 @@ def test_gemv_launch_policies_bitwise_identical(K, M, N):
                             assert np.array_equal(y.view(np.uint32), ref.view(np.uint32)), (mp, depth, rowitems, wg)
     finally:
         ggml_hip.check(L.ggml_hip_debug_set_gemv_policy(-1, 0, 1, 0), "policy reset")
+
+
+# ------------------------------------------------------------------------------- weight-residency cache
+def test_weight_cache_reuses_and_revalidates_host_weights():
+    """a CPU-backend Q4_0 src0 is uploaded once per device and reused (bitwise
+    same y); rewriting the host bytes in place is detected and re-uploaded (y follows the data)."""
+    L = ggml_hip.load()
+    ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+    K, M, N = 4096, 192, 40
+    wq, x = make_case(K, M, N, seed=21)
+    w_np, x_np = np.ascontiguousarray(wq).copy(), np.ascontiguousarray(x)
+
+    def stats():
+        h, m, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        ggml_hip.check(L.ggml_hip_weight_cache_stats(ctypes.byref(h), ctypes.byref(m), ctypes.byref(r)))
+        return h.value, m.value, r.value
+
+    def run():
+        y_np = np.zeros((N, M), np.float32)
+        w = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_Q4_0, (K, M), w_np)
+        xt = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (K, N), x_np)
+        y = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (M, N), y_np)
+        L.ggml_hip_mul_mat(ctypes.byref(w), ctypes.byref(xt), ctypes.byref(y))
+        return y_np
+
+    y1 = run()
+    assert stats()[:2] == (0, 1) and stats()[2] == w_np.nbytes
+    y2 = run()
+    assert stats()[:2] == (1, 1)
+    assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))
+    _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
+    check_y(y1, O.mul_mat(wq, K, x), s_abs, RTOL, ATOL_BLOCKS)
+    wq2, _ = make_case(K, M, 1, seed=22)                 # same address, new bytes
+    w_np[...] = wq2
+    y3 = run()
+    assert stats()[:2] == (1, 2)
+    _, s_abs2 = block_terms(wq2, O.quantize_q8_0(x, "avx2"), K)
+    check_y(y3, O.mul_mat(wq2, K, x), s_abs2, RTOL, ATOL_BLOCKS)
+    ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+    assert stats() == (0, 0, 0)

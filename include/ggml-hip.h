@@ -124,8 +124,10 @@ int ggml_hip_dequantize_q4_0(const void *dev_wq, int64_t K, int64_t M, float *de
  * ggml_hip_reserve_workspace or the first call). */
 int ggml_hip_mul_mat_q4_0(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N,
                           float *dev_y, void *stream);
-/* Same with an explicit algorithm and output stride ldy: 0 auto (1 for N <= 8, 3 for N <= 128, else
- * 2), 1 fused GEMV (N <= 8), 2 LDS-staged int8-MFMA GEMM, 3 split-K int8-MFMA GEMM (small N). */
+/* Same with an explicit algorithm and output stride ldy: 0 auto (4 in exact mode; else 1 for N <= 8,
+ * 3 for N <= 128, else 2), 1 fused GEMV (N <= 8), 2 LDS-staged int8-MFMA GEMM, 3 split-K int8-MFMA
+ * GEMM (small N), 4 exact: every y bit-identical to the reference's x86 AVX2+FMA
+ * ggml_vec_dot_q4_0_q8_0 (ggml.c:2412-2435; same q8_0 bytes, same fp32 fma schedule). */
 int ggml_hip_mul_mat_q4_0_ex(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N,
                              float *dev_y, int64_t ldy, int algo, void *stream);
 /* Sibling mul_mats that share the activation x (ggml graphs issue wq/wk/wv and w1/w3 on the same
@@ -134,6 +136,13 @@ int ggml_hip_mul_mat_q4_0_ex(const void *dev_w, int64_t K, int64_t M, const floa
  * are identical to n separate ggml_hip_mul_mat_q4_0 calls. */
 int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *M, int64_t K, const float *dev_x,
                                 int64_t N, float *const *dev_y, void *stream);
+/* Exact (reproducible) mode, process-wide: every auto-selected mul_mat, including the ggml hook
+ * path (ggml_hip_mul_mat / ggml_hip_compute_forward) and the sibling-matrix calls, runs algorithm 4,
+ * so a ggml graph on this backend reproduces the reference CPU build's mul_mat outputs bit for bit.
+ * Default off (GGML_HIP_EXACT=1 switches it on at first use); the fast kernels stay within the
+ * north-star 1e-3 tolerance.  No ggml-cuda.h counterpart. */
+int ggml_hip_set_exact(int on);
+int ggml_hip_get_exact(void);
 /* Ensure the current device's workspace can serve mul_mat for N tokens of K (call before
  * capturing a HIP graph). */
 int ggml_hip_reserve_workspace(int64_t K, int64_t N);

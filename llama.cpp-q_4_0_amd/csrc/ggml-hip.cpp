@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -281,6 +282,19 @@ const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, ui
 // ------------------------------------------------------------------------------------------
 // the mul_mat core (device pointers): ggml_compute_forward_mul_mat_q_f32 INIT + COMPUTE
 
+// exact mode (algo 4 for every auto-selected mul_mat): GGML_HIP_EXACT=1 or ggml_hip_set_exact
+std::atomic<int> g_exact{-1};
+bool exact_mode() {
+    int v = g_exact.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = getenv("GGML_HIP_EXACT");
+        int want = (e && atoi(e) != 0) ? 1 : 0, expect = -1;
+        g_exact.compare_exchange_strong(expect, want);
+        v = g_exact.load(std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
 int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, float *y, int64_t ldy, int algo,
                 hipStream_t s) {
     if (!w || !x || !y || K <= 0 || M <= 0 || N < 0) return fail(GGML_HIP_ERR_INVALID, "null pointer or bad shape");
@@ -293,15 +307,15 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
         return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large for 32-bit buffer offsets; split rows");
     const int id = current_device();
     const int max_nt = ghip::gemv_max_tokens(K);
-    // auto: fused GEMV for N <= 8, split-K MFMA for N <= 128, LDS-staged MFMA GEMM above
-    // (crossovers measured with tools/n_sweep.py)
-    if (algo == 0) algo = (N <= max_nt) ? 1 : (N <= 128 ? 3 : 2);
+    // auto: exact mode if switched on; else fused GEMV for N <= 8, split-K MFMA for N <= 128,
+    // LDS-staged MFMA GEMM above (crossovers measured with tools/n_sweep.py)
+    if (algo == 0) algo = exact_mode() ? 4 : (N <= max_nt) ? 1 : (N <= 128 ? 3 : 2);
     if (algo == 1) {
         if (N > max_nt) return fail(GGML_HIP_ERR_INVALID, "GEMV path supports N <= gemv_max_tokens(K)");
         HIP_RET(ghip::gemv_q4_0(w, K, M, x, N, y, ldy, g_dev[id].info, s));
         return GGML_HIP_OK;
     }
-    if (algo != 2 && algo != 3) return fail(GGML_HIP_ERR_INVALID, "algo must be 0, 1, 2 or 3");
+    if (algo < 2 || algo > 4) return fail(GGML_HIP_ERR_INVALID, "algo must be 0, 1, 2, 3 or 4");
     const size_t need = workspace_bytes(K, N);
     if (g_dev[id].ws_size < need) {
         int rc = reserve_workspace(id, need);
@@ -310,7 +324,9 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
     int8_t *qs = (int8_t *)g_dev[id].ws;
     float *xd = (float *)((char *)g_dev[id].ws + ((size_t)(N * K + 255) & ~(size_t)255));
     HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s));
-    if (algo == 3)
+    if (algo == 4)
+        HIP_RET(ghip::mm_exact_q4_0(w, K, M, qs, xd, N, y, ldy, s));
+    else if (algo == 3)
         HIP_RET(ghip::gemm_sk_q4_0(w, K, M, qs, xd, N, y, ldy, g_dev[id].info.num_cus, s));
     else
         HIP_RET(ghip::gemm_q4_0(w, K, M, qs, xd, N, y, ldy, s));
@@ -373,6 +389,10 @@ bool ggml_hip_can_mul_mat(const struct ggml_tensor *src0_, const struct ggml_ten
     // ggml-cuda.cu:2595-2610, restricted to the q4_0 path this backend implements
     const tensor *src0 = (const tensor *)src0_, *src1 = (const tensor *)src1_, *dst = (const tensor *)dst_;
     if (!supported_mul_mat(src0, src1, dst)) return false;
+    // no device: decline, so ggml.c plans and runs its own CPU mul_mat (the reference would route
+    // the op here regardless and fail inside ggml_cuda_mul_mat)
+    ensure_init();
+    if (g_device_count == 0) return false;
     return dst->ne[0] >= 32 && dst->ne[1] >= 32 && src1->ne[0] >= 32;
 }
 
@@ -662,8 +682,8 @@ int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *
         total += M[i];
     }
     if (N == 0) return GGML_HIP_OK;
-    if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30)) {
-        for (int i = 0; i < n; i++) {       // GEMM path (x re-quantized per matrix: prefill is MFMA-bound)
+    if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30) || exact_mode()) {
+        for (int i = 0; i < n; i++) {       // GEMM / exact path (x re-quantized per matrix: prefill is MFMA-bound)
             int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 0, s);
             if (rc != GGML_HIP_OK) return rc;
         }
@@ -678,6 +698,13 @@ int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *
     HIP_RET(ghip::gemv_q4_0_multi(n, dev_w, M, K, dev_x, N, dev_y, ldy, g_dev[current_device()].info, s));
     return GGML_HIP_OK;
 }
+
+int ggml_hip_set_exact(int on) {
+    g_exact.store(on ? 1 : 0, std::memory_order_relaxed);
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_get_exact(void) { return exact_mode() ? 1 : 0; }
 
 int ggml_hip_reserve_workspace(int64_t K, int64_t N) {
     ensure_init();

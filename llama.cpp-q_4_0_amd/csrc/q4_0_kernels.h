@@ -58,6 +58,11 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
 hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
                         float *y, int64_t ldy, int num_cus, hipStream_t s);
 
+// Exact mode: y bit-identical to the reference's AVX2+FMA ggml_vec_dot_q4_0_q8_0 (ggml.c:2412-2435),
+// per-lane sequential fma chains in block order; any N.
+hipError_t mm_exact_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
+                         float *y, int64_t ldy, hipStream_t s);
+
 // Multi-GPU helper: y[n*ldy + row0[r] + i] = slab[r][n][i] for i < rows[r] (gather compaction).
 hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const int64_t *row_begin_dev,
                          int64_t N, float *y, int64_t ldy, hipStream_t s);

@@ -1577,6 +1577,130 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
 }
 
 // ---------------------------------------------------------------------------------------------
+// Exact mode (algo 4): every y bit-identical to the reference's x86 AVX2+FMA
+// ggml_vec_dot_q4_0_q8_0 (ggml.c:2412-2435), which is a fixed fp32 schedule:
+//   d      = fp32(d_w) * fp32(d_x)                         (exact: 11 x 11 significant bits)
+//   lane j = sum of the 4 products of block elements 4j..4j+3 (bytes_from_nibbles_32 order:
+//            elements 0..15 = low nibbles of qs[0..15], 16..31 = high nibbles), an exact int
+//   acc_j  = fma(d, float(lane j), acc_j), block after block, for j = 0..7
+//   y      = ((acc0+acc4) + (acc2+acc6)) + ((acc1+acc5) + (acc3+acc7))   (hsum_float_8, ggml.c:591)
+// Eight threads per output row each run one lane's chain in block order, so the only freedom
+// left is the memory schedule: weights and activations are staged through LDS a chunk of EX_C
+// blocks at a time (global reads coalesced across the row), the next chunk's global loads in
+// flight while the current one is consumed.  The three hsum adds are xor-shuffles 4, 2, 1 within
+// the row's 8 lanes (fp32 addition is commutative, so lane k's acc_k + acc_{k^4} is the
+// reference's r_k on both lanes).  The int8 q8_0 operand is the SoA quantizer output (bit-exact
+// bytes; xd = the fp16-rounded scale as fp32), so d_w * xd is the reference's d.
+constexpr int EX_RB = 16;                    // output rows per workgroup (8 lanes each)
+constexpr int EX_THREADS = EX_RB * 8;        // 128
+constexpr int EX_C = 32;                     // blocks per chunk (even: chunk starts stay dword aligned)
+constexpr int EX_WROW = EX_C * Q4B + 4;      // LDS bytes per staged weight row (odd dword stride)
+constexpr int EX_WDW = EX_C * Q4B / 4;       // 144 dwords of one row's chunk
+constexpr int EX_WPT = (EX_RB * EX_WDW + EX_THREADS - 1) / EX_THREADS;   // 18 staged dwords per thread
+
+template <int NC>
+__global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes,
+                                                               int nb, int M, const int8_t *__restrict__ xqs,
+                                                               const float *__restrict__ xd, int N, int K,
+                                                               float *__restrict__ y, int64_t ldy) {
+    static_assert(NC * EX_C * 8 % EX_THREADS == 0 && NC * EX_C <= EX_THREADS * 2, "x staging shape");
+    constexpr int XPT = NC * EX_C * 8 / EX_THREADS;          // staged x dwords per thread
+    constexpr int DPT = (NC * EX_C + EX_THREADS - 1) / EX_THREADS;
+    __shared__ uint32_t wl[EX_RB * EX_WROW / 4];
+    __shared__ uint32_t xl[NC * EX_C * 8];                    // [col][block][8 dwords]
+    __shared__ float dl[NC * EX_C];                           // [col][block]
+    const int t = threadIdx.x, lane = t & 7, r = t >> 3;
+    const int m0 = blockIdx.x * EX_RB, n0 = blockIdx.y * NC;
+    const int rows = min(EX_RB, M - m0), cols = min(NC, N - n0);
+    const uint8_t *wbase = W + (int64_t)m0 * rowbytes;
+    uint32_t wreg[EX_WPT], xreg[XPT];
+    float dreg[DPT];
+    // global -> registers for the chunk starting at block b0 (cb blocks, cb even)
+    auto fetch = [&](int b0, int cb) __attribute__((always_inline)) {
+        const int wdw = cb * Q4B / 4;
+#pragma unroll
+        for (int k = 0; k < EX_WPT; k++) {
+            const int i = t + k * EX_THREADS, rr = i / EX_WDW, c = i - rr * EX_WDW;
+            if (rr < rows && c < wdw)
+                wreg[k] = *reinterpret_cast<const uint32_t *>(wbase + rr * rowbytes + (int64_t)b0 * Q4B + 4 * c);
+        }
+#pragma unroll
+        for (int k = 0; k < XPT; k++) {
+            const int i = t + k * EX_THREADS, c = i / (EX_C * 8), j = i - c * (EX_C * 8);
+            if (c < cols && j < cb * 8)
+                xreg[k] = *reinterpret_cast<const uint32_t *>(xqs + (int64_t)(n0 + c) * K + (int64_t)b0 * 32 + 4 * j);
+        }
+#pragma unroll
+        for (int k = 0; k < DPT; k++) {
+            const int i = t + k * EX_THREADS, c = i / EX_C, j = i - c * EX_C;
+            if (i < NC * EX_C && c < cols && j < cb) dreg[k] = xd[(int64_t)(n0 + c) * nb + b0 + j];
+        }
+    };
+    auto stash = [&]() __attribute__((always_inline)) {     // registers -> LDS (same index maps)
+#pragma unroll
+        for (int k = 0; k < EX_WPT; k++) {
+            const int i = t + k * EX_THREADS, rr = i / EX_WDW, c = i - rr * EX_WDW;
+            if (rr < EX_RB) wl[rr * (EX_WROW / 4) + c] = wreg[k];
+        }
+#pragma unroll
+        for (int k = 0; k < XPT; k++) xl[t + k * EX_THREADS] = xreg[k];
+#pragma unroll
+        for (int k = 0; k < DPT; k++)
+            if (t + k * EX_THREADS < NC * EX_C) dl[t + k * EX_THREADS] = dreg[k];
+    };
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[c] = 0.0f;
+    const uint16_t *wrow = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint8_t *>(wl) + r * EX_WROW);
+    const int qoff = 1 + 2 * (lane & 3), shift = lane & 4;   // qs[4(j&3)..+3], low (j<4) / high nibbles
+    fetch(0, min(EX_C, nb));
+    for (int b0 = 0; b0 < nb; b0 += EX_C) {
+        const int cb = min(EX_C, nb - b0);
+        __syncthreads();                                      // previous chunk fully consumed
+        stash();
+        __syncthreads();
+        if (b0 + EX_C < nb) fetch(b0 + EX_C, min(EX_C, nb - b0 - EX_C));   // next chunk in flight
+        for (int b = 0; b < cb; b++) {
+            const uint16_t *wb = wrow + b * (Q4B / 2);
+            const float dw = h2f(wb[0]);
+            const uint32_t q = (uint32_t)wb[qoff] | ((uint32_t)wb[qoff + 1] << 16);
+            const int wv = (int)nib_to_i8x4(q, shift);
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const int s = __builtin_amdgcn_sdot4(wv, (int)xl[(c * EX_C + b) * 8 + lane], 0, false);
+                acc[c] = __builtin_fmaf(dw * dl[c * EX_C + b], (float)s, acc[c]);
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        float v = acc[c];
+        v = v + __shfl_xor(v, 4, 8);       // r_k = acc_k + acc_{k+4}
+        v = v + __shfl_xor(v, 2, 8);       // lane 0: r0 + r2, lane 1: r1 + r3
+        v = v + __shfl_xor(v, 1, 8);       // lane 0: (r0 + r2) + (r1 + r3)
+        if (lane == 0 && r < rows && c < cols) y[(int64_t)(n0 + c) * ldy + m0 + r] = v;
+    }
+}
+
+hipError_t mm_exact_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
+                         float *y, int64_t ldy, hipStream_t s) {
+    const int nb = (int)(K / QK);
+    const int64_t rowbytes = (int64_t)nb * Q4B;
+    const int nc = N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : 8;
+    dim3 grid((unsigned)((M + EX_RB - 1) / EX_RB), (unsigned)((N + nc - 1) / nc));
+    (void)hipGetLastError();  // report only this launch's error
+    auto args = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(EX_THREADS), 0, s, (const uint8_t *)W, rowbytes, nb, (int)M, xqs, xd,
+                           (int)N, (int)K, y, ldy);
+    };
+    if (nc == 1) args(k_mm_exact_q4_0<1>);
+    else if (nc == 2) args(k_mm_exact_q4_0<2>);
+    else if (nc == 4) args(k_mm_exact_q4_0<4>);
+    else args(k_mm_exact_q4_0<8>);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // multi-GPU gather compaction: slabs [nranks][N][max_rows] -> y[n][row_begin[r] + i]
 
 __global__ __launch_bounds__(256) void k_scatter_slabs(const float *__restrict__ slabs, int nranks,

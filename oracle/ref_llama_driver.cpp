@@ -1,0 +1,74 @@
+// ref_llama_driver.cpp — TEST INFRASTRUCTURE ONLY (the caller side, like ref_hip_driver.c): the
+// reference's own llama.cpp (its GGJT v3 loader, llama.cpp:383-503, and its eval graph) compiled
+// from /root/reference, loads a model file and evaluates a prompt.  Built twice by oracle/Makefile:
+// CPU-only (golden logits) and with -DGGML_USE_CUBLAS linked against libggml_hip_cuda.so, where
+// ggml.c's hooks send every Q4_0 mul_mat of a >= 32-token batch to the MI355X backend (weights stay
+// CPU tensors, n_gpu_layers = 0: the arch/-frontend situation; they hit the weight-residency cache).
+#include "llama.h"
+
+#include <execinfo.h>
+#include <csignal>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <unistd.h>
+
+static bool g_trace = false;
+#define STAGE(msg) do { if (g_trace) { fprintf(stderr, "refllama: %s\n", msg); fflush(stderr); } } while (0)
+
+static void refllama_segv(int sig) {   // REFLLAMA_BACKTRACE=1: native stack of a crash (no gdb here)
+    void *f[64];
+    const int n = backtrace(f, 64);
+    backtrace_symbols_fd(f, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+extern "C" int refllama_logits(const char *path, const int *tokens, int n_tokens, int n_threads, int logits_all,
+                               float *out, int out_cap, int n_evals) {
+    g_trace = getenv("REFLLAMA_BACKTRACE") != nullptr;
+    if (g_trace) {   // own stack for the handler: a stack overflow must still print
+        static char alt[1 << 16];
+        stack_t ss{};
+        ss.ss_sp = alt;
+        ss.ss_size = sizeof(alt);
+        sigaltstack(&ss, nullptr);
+        struct sigaction sa {};
+        sa.sa_handler = refllama_segv;
+        sa.sa_flags = SA_ONSTACK;
+        sigaction(SIGSEGV, &sa, nullptr);
+    }
+    llama_init_backend(false);
+    STAGE("backend initialised");
+    llama_context_params p = llama_context_default_params();
+    p.n_ctx = 256;
+    p.n_batch = 512;
+    p.n_gpu_layers = 0;
+    p.seed = 1;
+    p.use_mmap = getenv("REFLLAMA_NO_MMAP") == nullptr;
+    p.logits_all = logits_all != 0;
+    llama_model *m = llama_load_model_from_file(path, p);
+    if (!m) return -1;
+    STAGE("model loaded");
+    llama_context *c = llama_new_context_with_model(m, p);
+    if (!c) {
+        llama_free_model(m);
+        return -2;
+    }
+    STAGE("context created");
+    int rc = 0;
+    for (int e = 0; e < (n_evals > 0 ? n_evals : 1) && rc == 0; e++)   // repeated evals: same logits
+        rc = llama_eval(c, (const llama_token *)tokens, n_tokens, 0, n_threads) ? -3 : 0;
+    STAGE("evaluated");
+    const int nv = llama_n_vocab(c);
+    if (rc == 0) {
+        const int rows = logits_all ? n_tokens : 1;
+        const int cnt = rows * nv < out_cap ? rows * nv : out_cap;
+        memcpy(out, llama_get_logits(c), sizeof(float) * (size_t)cnt);
+        rc = nv;
+    }
+    llama_free(c);
+    STAGE("context freed");
+    llama_free_model(m);
+    return rc;
+}

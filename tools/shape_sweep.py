@@ -1,6 +1,6 @@
 """Decode (N=1) GEMV per shape: graph replay over 32 distinct weight matrices (> Infinity Cache),
 per-launch us and GB/s, for the LLaMA-7B/13B and Falcon-7B shapes (BASELINE configs 2, 4, 5).
-Usage: python tools/shape_sweep.py [K:M ...]"""
+Usage: [ALGO=4] [NTOK=1] python tools/shape_sweep.py [K:M ...]   (ALGO default 1 = fused GEMV)"""
 import json
 import os
 import sys
@@ -13,6 +13,8 @@ shapes = [tuple(map(int, a.split(":"))) for a in sys.argv[1:]] or [
     (4096, 4096), (4096, 11008), (11008, 4096), (5120, 5120), (5120, 13824), (13824, 5120),
     (4544, 4672), (4544, 4544), (4544, 18176), (18176, 4544)]
 s = L.ggml_hip_default_stream()
+ALGO = int(os.environ.get("ALGO", "1"))
+NTOK = int(os.environ.get("NTOK", "1"))
 NMAT = 32
 for K, M in shapes:
     tmp = gh.DeviceBuffer(K * M * 4)
@@ -23,13 +25,13 @@ for K, M in shapes:
         gh.check(L.ggml_hip_quantize_q4_0(tmp.ptr, K, M, b.ptr, None))
         ws.append(b)
     tmp.free()
-    x = gh.DeviceBuffer(K * 4)
-    gh.check(L.ggml_hip_fill_gaussian(x.ptr, K, 9, 0.0, 1.0, None))
-    y = gh.DeviceBuffer(M * 4)
+    x = gh.DeviceBuffer(NTOK * K * 4)
+    gh.check(L.ggml_hip_fill_gaussian(x.ptr, NTOK * K, 9, 0.0, 1.0, None))
+    y = gh.DeviceBuffer(NTOK * M * 4)
 
     def run():
         for w in ws:
-            gh.check(L.ggml_hip_mul_mat_q4_0_ex(w.ptr, K, M, x.ptr, 1, y.ptr, M, 1, s))
+            gh.check(L.ggml_hip_mul_mat_q4_0_ex(w.ptr, K, M, x.ptr, NTOK, y.ptr, M, ALGO, s))
     run()
     gh.check(L.ggml_hip_stream_synchronize(s))
     g = gh.Graph(s)
@@ -45,7 +47,7 @@ for K, M in shapes:
     t = a.elapsed_ms(b) * 1e-3 / (10 * NMAT)
     nbytes = 18 * K // 32 * M + 4 * K + 4 * M
     npairs = K // 64
-    print(json.dumps({"K": K, "M": M, "pairs": npairs, "chunk_fill": round(npairs / (64 * -(-npairs // 64)), 3),
+    print(json.dumps({"algo": ALGO, "N": NTOK, "K": K, "M": M, "pairs": npairs, "chunk_fill": round(npairs / (64 * -(-npairs // 64)), 3),
                       "us": round(t * 1e6, 2), "GBps": round(nbytes / t / 1e9, 1)}), flush=True)
     del g
     for w in ws:

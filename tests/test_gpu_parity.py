@@ -258,6 +258,25 @@ def test_llama7b_small_batch_split_k_full_shape(K, M, N):
 
 
 # ------------------------------------------------------------------------------- tensor ABI (host tensors)
+def test_can_mul_mat_rule():
+    """Q4_0 x F32 -> F32 with ne0, ne1, ne10 >= 32 (ggml-cuda.cu:2595-2610); other types: no."""
+    L = ggml_hip.load()
+    K, M = 4096, 64
+    for N, expect in ((32, True), (31, False), (512, True)):
+        w = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_Q4_0, (K, M))
+        x = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (K, N))
+        y = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (M, N))
+        assert bool(L.ggml_hip_can_mul_mat(ctypes.byref(w), ctypes.byref(x), ctypes.byref(y))) == expect
+    wf = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (K, M))
+    assert not L.ggml_hip_can_mul_mat(ctypes.byref(wf), ctypes.byref(x), ctypes.byref(y))
+    w96 = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_Q4_0, (96, M))     # K % 64 != 0 -> CPU path
+    x96 = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (96, 64))
+    y96 = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (M, 64))
+    assert not L.ggml_hip_can_mul_mat(ctypes.byref(w96), ctypes.byref(x96), ctypes.byref(y96))
+    assert L.ggml_hip_mul_mat_get_wsize(ctypes.byref(w), ctypes.byref(x), ctypes.byref(y)) == 0
+
+
+
 def test_tensor_abi_compute_forward_host_tensors():
     """ggml.c:15645-15652 hook: node taken, only ith == 0 / COMPUTE computes; batch dim ne2 = 2."""
     L = ggml_hip.load()

@@ -33,3 +33,24 @@ def test_reference_llama_cpu_reproduces_golden_logits(tmp_path):
     got = ref_logits(CPU_LIB, mp)
     gold = np.load(os.path.join(GOLD, "llama_tiny_logits.npy"))
     assert np.array_equal(got.view(np.uint32), gold.view(np.uint32))
+
+
+HIP_LIB = os.path.join(ROOT, "oracle", "_ref", "libllama_ref_hip.so")
+
+
+@pytest.mark.skipif(not os.path.exists(HIP_LIB), reason="oracle/_ref/libllama_ref_hip.so not built")
+def test_reference_llama_gpu_build_without_device_declines_to_cpu(tmp_path):
+    """The -DGGML_USE_CUBLAS build linked against libggml_hip_cuda.so, on a host with no HIP device:
+    the loader and context run through every hook (host_malloc, set_scratch_size, set_tensor_split,
+    ...), can_mul_mat declines every node, and ggml's CPU ops reproduce the golden logits bitwise."""
+    from hip_env import ggml_hip
+    if ggml_hip.load().ggml_hip_device_count() > 0:
+        pytest.skip("a HIP device is present (tests/test_gpu_llama_ggjt.py covers it)")
+    import sys
+    sys.path.insert(0, GOLD)
+    from gen_llama_golden import ref_logits
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp)
+    got = ref_logits(HIP_LIB, mp, n_evals=2)
+    gold = np.load(os.path.join(GOLD, "llama_tiny_logits.npy"))
+    assert np.array_equal(got.view(np.uint32), gold.view(np.uint32))

@@ -1584,94 +1584,185 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
 //            elements 0..15 = low nibbles of qs[0..15], 16..31 = high nibbles), an exact int
 //   acc_j  = fma(d, float(lane j), acc_j), block after block, for j = 0..7
 //   y      = ((acc0+acc4) + (acc2+acc6)) + ((acc1+acc5) + (acc3+acc7))   (hsum_float_8, ggml.c:591)
-// Eight threads per output row each run one lane's chain in block order, so the only freedom
-// left is the memory schedule: weights and activations are staged through LDS a chunk of EX_C
-// blocks at a time (global reads coalesced across the row), the next chunk's global loads in
-// flight while the current one is consumed.  The three hsum adds are xor-shuffles 4, 2, 1 within
-// the row's 8 lanes (fp32 addition is commutative, so lane k's acc_k + acc_{k^4} is the
-// reference's r_k on both lanes).  The int8 q8_0 operand is the SoA quantizer output (bit-exact
-// bytes; xd = the fp16-rounded scale as fp32), so d_w * xd is the reference's d.
-constexpr int EX_RB = 16;                    // output rows per workgroup (8 lanes each)
-constexpr int EX_THREADS = EX_RB * 8;        // 128
-constexpr int EX_C = 32;                     // blocks per chunk (even: chunk starts stay dword aligned)
-constexpr int EX_WROW = EX_C * Q4B + 4;      // LDS bytes per staged weight row (odd dword stride)
-constexpr int EX_WDW = EX_C * Q4B / 4;       // 144 dwords of one row's chunk
-constexpr int EX_WPT = (EX_RB * EX_WDW + EX_THREADS - 1) / EX_THREADS;   // 18 staged dwords per thread
+// Eight threads per output row each run one lane's chain in block order, so all the freedom left
+// is the memory schedule.  Chunks of EX_C = 64 blocks move global -> LDS by LDS-DMA only (no
+// register staging, so nothing in flight is tied to a loop-carried register): a 3-slot ring, two
+// chunks in flight, one counted `s_waitcnt vmcnt` + raw `s_barrier` per chunk (the slot refilled
+// after the barrier is the one every wave finished before it).  Per slot:
+//   weights: the 16 rows' 1152-byte row pieces as 16-byte units interleaved across rows (unit
+//            (row r, piece k) at u = 16k + r, 9 x 1 KiB `buffer_load_dwordx4 ... lds` per wave):
+//            the consumer's word D of row r sits at byte 256(D/4) + 16r + 4(D%4), bank
+//            4r + D%4, so the 4 rows x 4 distinct words of a 32-lane group never conflict;
+//   x:       int8 q8_0 bytes [col][block][32] (1 KiB per column-half, one DMA each);
+//   d_x:     f32 [col][64] (one 256-byte dword DMA per column).
+// Per step (block b of a chunk) lane j of row r: the qs word of elements 4j..4j+3 (an aligned
+// word for odd blocks, v_alignbyte of two words for even ones), nib = 0..15 per byte, and lane
+// j's exact integer sum_(4j..4j+3) (nib - 8) x = v_dot4_i32_i8(nib, x, v_dot4_i32_i8(x, -8)).
+// The LDS operands of 8 steps are read one batch ahead.  The three hsum adds are xor-shuffles 4,
+// 2, 1 within the row's 8 lanes (fp32 addition is commutative: lane k's acc_k + acc_{k^4} is the
+// reference's r_k on both lanes).  x and d_x are the SoA quantizer's output (bit-exact bytes;
+// d_x = the fp16-rounded scale as fp32), so d_w * d_x is the reference's d.
+constexpr int EX_RB = 16;                            // output rows per workgroup (8 lanes each)
+constexpr int EX_THREADS = EX_RB * 8;                // 128 = 2 waves
+constexpr int EX_C = 64;                             // blocks per chunk
+constexpr int EX_WB = EX_RB * EX_C * Q4B;            // weight bytes per slot (18 KiB)
+constexpr int EX_WI = EX_WB / 1024 / 2;              // 1-KiB weight DMAs per wave per chunk (9)
+constexpr int EX_S = 3;                              // ring slots
+static_assert(EX_WB % 2048 == 0, "whole 1-KiB weight DMAs per wave");
+
+template <int NC>
+struct ExLayout {
+    static constexpr int XB = NC * EX_C * 32;                    // x bytes per slot
+    static constexpr int DXW = (NC + 1) / 2;                     // d_x DMAs per wave per chunk
+    static constexpr int DXB = DXW * 2 * 64 * 4;                 // d_x bytes per slot
+    static constexpr int SLOT = EX_WB + XB + DXB;
+    static constexpr int OPS = EX_WI + NC + DXW;                 // vector-memory ops per wave per chunk
+    static_assert(OPS <= 63, "vmcnt immediate");
+};
 
 template <int NC>
 __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes,
                                                                int nb, int M, const int8_t *__restrict__ xqs,
                                                                const float *__restrict__ xd, int N, int K,
                                                                float *__restrict__ y, int64_t ldy) {
-    static_assert(NC * EX_C * 8 % EX_THREADS == 0 && NC * EX_C <= EX_THREADS * 2, "x staging shape");
-    constexpr int XPT = NC * EX_C * 8 / EX_THREADS;          // staged x dwords per thread
-    constexpr int DPT = (NC * EX_C + EX_THREADS - 1) / EX_THREADS;
-    __shared__ uint32_t wl[EX_RB * EX_WROW / 4];
-    __shared__ uint32_t xl[NC * EX_C * 8];                    // [col][block][8 dwords]
-    __shared__ float dl[NC * EX_C];                           // [col][block]
-    const int t = threadIdx.x, lane = t & 7, r = t >> 3;
+    using Lay = ExLayout<NC>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int t = threadIdx.x, l64 = t & 63, lane = t & 7, r = t >> 3;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int q = lane & 3, shift = lane & 4;               // qs word q; low (j < 4) / high nibbles
     const int m0 = blockIdx.x * EX_RB, n0 = blockIdx.y * NC;
     const int rows = min(EX_RB, M - m0), cols = min(NC, N - n0);
-    const uint8_t *wbase = W + (int64_t)m0 * rowbytes;
-    uint32_t wreg[EX_WPT], xreg[XPT];
-    float dreg[DPT];
-    // global -> registers for the chunk starting at block b0 (cb blocks, cb even)
-    auto fetch = [&](int b0, int cb) __attribute__((always_inline)) {
-        const int wdw = cb * Q4B / 4;
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W + (int64_t)m0 * rowbytes, (uint32_t)((int64_t)rows * rowbytes));
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)cols * K));
+    const __amdgpu_buffer_rsrc_t drs = make_rsrc(xd + (int64_t)n0 * nb, (uint32_t)((int64_t)cols * nb * 4));
+    const __amdgpu_buffer_rsrc_t nul = make_rsrc(W, 0);
+    const int nchunks = (nb + EX_C - 1) / EX_C;
+    // weight DMA i of this wave (slot instruction 9*wave + i) covers units 64(9 wave + i) + l64:
+    // row l64 & 15, piece 4(9 wave + i) + (l64 >> 4)
+    const int wsrc = (l64 & 15) * (int)rowbytes + 16 * (4 * EX_WI * wave + (l64 >> 4));
+
+    auto issue = [&](int ch) __attribute__((always_inline)) {
+        const bool valid = ch < nchunks;                    // past the end: counted, no traffic
+        const int b0 = valid ? ch * EX_C : 0;
+        uint8_t *slot = smem + (ch % EX_S) * Lay::SLOT;
+        const __amdgpu_buffer_rsrc_t w_ = valid ? wrs : nul;
 #pragma unroll
-        for (int k = 0; k < EX_WPT; k++) {
-            const int i = t + k * EX_THREADS, rr = i / EX_WDW, c = i - rr * EX_WDW;
-            if (rr < rows && c < wdw)
-                wreg[k] = *reinterpret_cast<const uint32_t *>(wbase + rr * rowbytes + (int64_t)b0 * Q4B + 4 * c);
-        }
+        for (int i = 0; i < EX_WI; i++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(w_, (lds_void_t *)(slot + 1024 * (EX_WI * wave + i)), 16,
+                                                     wsrc + b0 * Q4B + 64 * i, 0, 0, 0);
+        const __amdgpu_buffer_rsrc_t x_ = valid ? xrs : nul;
 #pragma unroll
-        for (int k = 0; k < XPT; k++) {
-            const int i = t + k * EX_THREADS, c = i / (EX_C * 8), j = i - c * (EX_C * 8);
-            if (c < cols && j < cb * 8)
-                xreg[k] = *reinterpret_cast<const uint32_t *>(xqs + (int64_t)(n0 + c) * K + (int64_t)b0 * 32 + 4 * j);
-        }
+        for (int c = 0; c < NC; c++)                         // wave w loads half w of each column
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(x_, (lds_void_t *)(slot + EX_WB + c * EX_C * 32 + 1024 * wave), 16,
+                                                     c * K + b0 * 32 + 1024 * wave + 16 * l64, 0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < DPT; k++) {
-            const int i = t + k * EX_THREADS, c = i / EX_C, j = i - c * EX_C;
-            if (i < NC * EX_C && c < cols && j < cb) dreg[k] = xd[(int64_t)(n0 + c) * nb + b0 + j];
+        for (int cc = 0; cc < Lay::DXW; cc++) {
+            const int c = 2 * cc + wave;
+            const __amdgpu_buffer_rsrc_t d_ = (valid && c < NC) ? drs : nul;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(d_, (lds_void_t *)(slot + EX_WB + Lay::XB + 256 * c), 4,
+                                                     (c * nb + b0 + l64) * 4, 0, 0, 0);
         }
     };
-    auto stash = [&]() __attribute__((always_inline)) {     // registers -> LDS (same index maps)
+
+    // per-lane byte offsets (within a slot) of word D = 9 p4 + q + delta of row r, p4 = pair % 4;
+    // pair p = 4g + p4 adds 2304 g (= 36 g words) as an immediate
+    auto woff = [&](int D) __attribute__((always_inline)) { return 256 * (D >> 2) + 16 * r + 4 * (D & 3); };
+    int aE1[4], aE2[4], aO[4];
 #pragma unroll
-        for (int k = 0; k < EX_WPT; k++) {
-            const int i = t + k * EX_THREADS, rr = i / EX_WDW, c = i - rr * EX_WDW;
-            if (rr < EX_RB) wl[rr * (EX_WROW / 4) + c] = wreg[k];
-        }
-#pragma unroll
-        for (int k = 0; k < XPT; k++) xl[t + k * EX_THREADS] = xreg[k];
-#pragma unroll
-        for (int k = 0; k < DPT; k++)
-            if (t + k * EX_THREADS < NC * EX_C) dl[t + k * EX_THREADS] = dreg[k];
-    };
+    for (int p4 = 0; p4 < 4; p4++) {
+        aE1[p4] = woff(9 * p4 + q);
+        aE2[p4] = woff(9 * p4 + q + 1);
+        aO[p4] = woff(9 * p4 + 5 + q);
+    }
+    const int rbase = 16 * r;                               // + 256 (D>>2) + 4 (D&3) for lane-free D
+
     float acc[NC];
 #pragma unroll
     for (int c = 0; c < NC; c++) acc[c] = 0.0f;
-    const uint16_t *wrow = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint8_t *>(wl) + r * EX_WROW);
-    const int qoff = 1 + 2 * (lane & 3), shift = lane & 4;   // qs[4(j&3)..+3], low (j<4) / high nibbles
-    fetch(0, min(EX_C, nb));
-    for (int b0 = 0; b0 < nb; b0 += EX_C) {
-        const int cb = min(EX_C, nb - b0);
-        __syncthreads();                                      // previous chunk fully consumed
-        stash();
-        __syncthreads();
-        if (b0 + EX_C < nb) fetch(b0 + EX_C, min(EX_C, nb - b0 - EX_C));   // next chunk in flight
-        for (int b = 0; b < cb; b++) {
-            const uint16_t *wb = wrow + b * (Q4B / 2);
-            const float dw = h2f(wb[0]);
-            const uint32_t q = (uint32_t)wb[qoff] | ((uint32_t)wb[qoff + 1] << 16);
-            const int wv = (int)nib_to_i8x4(q, shift);
+
+    // one step's operands
+    struct Op {
+        uint32_t wlo, whi, dwbits, x[NC];
+        float dx[NC];
+    };
+    auto load_x = [&](Op &o, const uint8_t *slot, int b) __attribute__((always_inline)) {
 #pragma unroll
-            for (int c = 0; c < NC; c++) {
-                const int s = __builtin_amdgcn_sdot4(wv, (int)xl[(c * EX_C + b) * 8 + lane], 0, false);
-                acc[c] = __builtin_fmaf(dw * dl[c * EX_C + b], (float)s, acc[c]);
+        for (int c = 0; c < NC; c++) {
+            o.x[c] = reinterpret_cast<const uint32_t *>(slot + EX_WB + c * EX_C * 32)[b * 8 + lane];
+            o.dx[c] = reinterpret_cast<const float *>(slot + EX_WB + Lay::XB + 256 * c)[b];
+        }
+    };
+    auto load_step = [&](Op &o, const uint8_t *slot, int b) __attribute__((always_inline)) {
+        const int p = b >> 1, p4 = p & 3, g = p >> 2;
+        const uint8_t *wsl = slot + 2304 * g;
+        if (b & 1) {
+            o.wlo = *reinterpret_cast<const uint32_t *>(wsl + aO[p4]);
+            o.dwbits = *reinterpret_cast<const uint32_t *>(wsl + rbase + 256 * ((9 * p4 + 4) >> 2) + 4 * ((9 * p4 + 4) & 3));
+        } else {
+            o.wlo = *reinterpret_cast<const uint32_t *>(wsl + aE1[p4]);
+            o.whi = *reinterpret_cast<const uint32_t *>(wsl + aE2[p4]);
+            o.dwbits = *reinterpret_cast<const uint32_t *>(wsl + rbase + 256 * ((9 * p4) >> 2) + 4 * ((9 * p4) & 3));
+        }
+        load_x(o, slot, b);
+    };
+    auto use_step = [&](const Op &o, int b) __attribute__((always_inline)) {
+        const uint32_t w = (b & 1) ? o.wlo : __builtin_amdgcn_alignbyte(o.whi, o.wlo, 2);
+        const float dw = (b & 1) ? h2f(o.dwbits >> 16) : h2f(o.dwbits);
+        const uint32_t nib = (w >> shift) & 0x0F0F0F0Fu;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int bias = __builtin_amdgcn_sdot4((int)o.x[c], (int)0xF8F8F8F8, 0, false);   // -8 sum x
+            const int sgn = __builtin_amdgcn_sdot4((int)nib, (int)o.x[c], bias, false);
+            acc[c] = __builtin_fmaf(dw * o.dx[c], (float)sgn, acc[c]);
+        }
+    };
+    constexpr int BB = NC <= 2 ? 4 : 2;                      // steps per pipelined batch (lgkmcnt <= 15)
+
+    issue(0);
+    issue(1);
+    for (int ch = 0; ch < nchunks; ch++) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Lay::OPS) : "memory");   // my DMAs of chunk ch landed
+        __builtin_amdgcn_s_barrier();                       // everyone's landed; chunk ch-1 consumed
+        issue(ch + 2);                                      // into chunk ch-1's slot
+        const uint8_t *slot = smem + (ch % EX_S) * Lay::SLOT;
+        const int cb = min(EX_C, nb - ch * EX_C);
+        if (cb == EX_C) {
+            Op ops[2][BB];
+#pragma unroll
+            for (int b = 0; b < BB; b++) load_step(ops[0][b], slot, b);
+#pragma unroll
+            for (int i = 0; i < EX_C / BB; i++) {
+                // sched_barrier: keep the next batch's LDS reads ahead of this batch's math (the
+                // scheduler otherwise pulls each read down to its use and waits on it)
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + 1 < EX_C / BB) {
+#pragma unroll
+                    for (int b = 0; b < BB; b++) load_step(ops[(i + 1) & 1][b], slot, (i + 1) * BB + b);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int b = 0; b < BB; b++) use_step(ops[i & 1][b], i * BB + b);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            for (int pp = 0; pp < cb / 2; pp++) {           // tail chunk (cb even), generic addressing
+                Op o0, o1;
+                const int p4 = pp & 3, g = pp >> 2;
+                const uint8_t *wsl = slot + 2304 * g;
+                o0.wlo = *reinterpret_cast<const uint32_t *>(wsl + woff(9 * p4 + q));
+                o0.whi = *reinterpret_cast<const uint32_t *>(wsl + woff(9 * p4 + q + 1));
+                o0.dwbits = *reinterpret_cast<const uint32_t *>(wsl + woff(9 * p4));
+                o1.wlo = *reinterpret_cast<const uint32_t *>(wsl + woff(9 * p4 + 5 + q));
+                o1.dwbits = *reinterpret_cast<const uint32_t *>(wsl + rbase + 256 * ((9 * p4 + 4) >> 2) +
+                                                                4 * ((9 * p4 + 4) & 3));
+                load_x(o0, slot, 2 * pp);
+                load_x(o1, slot, 2 * pp + 1);
+                use_step(o0, 0);
+                use_step(o1, 1);
             }
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // no LDS-DMA may outlive the workgroup
 #pragma unroll
     for (int c = 0; c < NC; c++) {
         float v = acc[c];
@@ -1682,22 +1773,35 @@ __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const uint8_t *__r
     }
 }
 
-hipError_t mm_exact_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
-                         float *y, int64_t ldy, hipStream_t s) {
+template <int NC>
+static hipError_t launch_exact(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
+                               float *y, int64_t ldy, hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
-    const int nc = N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : 8;
-    dim3 grid((unsigned)((M + EX_RB - 1) / EX_RB), (unsigned)((N + nc - 1) / nc));
+    const int lds = EX_S * ExLayout<NC>::SLOT;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_mm_exact_q4_0<NC>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    dim3 grid((unsigned)((M + EX_RB - 1) / EX_RB), (unsigned)((N + NC - 1) / NC));
     (void)hipGetLastError();  // report only this launch's error
-    auto args = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, dim3(EX_THREADS), 0, s, (const uint8_t *)W, rowbytes, nb, (int)M, xqs, xd,
-                           (int)N, (int)K, y, ldy);
-    };
-    if (nc == 1) args(k_mm_exact_q4_0<1>);
-    else if (nc == 2) args(k_mm_exact_q4_0<2>);
-    else if (nc == 4) args(k_mm_exact_q4_0<4>);
-    else args(k_mm_exact_q4_0<8>);
+    hipLaunchKernelGGL(k_mm_exact_q4_0<NC>, grid, dim3(EX_THREADS), lds, s, (const uint8_t *)W, rowbytes, nb, (int)M,
+                       xqs, xd, (int)N, (int)K, y, ldy);
     return hipGetLastError();
+}
+
+hipError_t mm_exact_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
+                         float *y, int64_t ldy, hipStream_t s) {
+    static const int nc_env = env_int("GGML_HIP_EXACT_NC", 0);   // tuning: columns per workgroup
+    // measured (tools/exact_nc.sh, 4096 x 4096): 8 columns best at N = 8, 2 at N = 40 and 512
+    const int nc = nc_env ? nc_env : N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : 2;
+    if (nc == 1) return launch_exact<1>(W, K, M, xqs, xd, N, y, ldy, s);
+    if (nc == 2) return launch_exact<2>(W, K, M, xqs, xd, N, y, ldy, s);
+    if (nc == 4) return launch_exact<4>(W, K, M, xqs, xd, N, y, ldy, s);
+    return launch_exact<8>(W, K, M, xqs, xd, N, y, ldy, s);
 }
 
 // ---------------------------------------------------------------------------------------------

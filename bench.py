@@ -113,6 +113,7 @@ def main():
     ap.add_argument("--force-split", action="store_true",
                     help="run the multi-GPU code path (row split + RCCL all-gather) even with one rank")
     ap.add_argument("--no-extra", action="store_true", help="skip the LLaMA-13B / Falcon-7B decode lines")
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-mode (bit-identical) decode line")
     ap.add_argument("--no-batch-siblings", action="store_true",
                     help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
     args = ap.parse_args()
@@ -276,6 +277,8 @@ def main():
         result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
         if not args.no_prefill and args.prefill_tokens > 0:
             result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens)
+        if not args.no_exact:
+            result["exact_mode"] = exact_decode(gh, L, decode_step, stream, args)
         if not args.no_extra:
             result["other_configs"] = [extra_decode(gh, L, stream, *c, steps=args.steps, warmup=args.warmup)
                                        for c in EXTRA_CONFIGS]
@@ -343,6 +346,33 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
             "avg_launch_us": round(tot_t / nlaunch * 1e6, 3), "per_shape": shapes,
             "timing": "HIP events around graph replays of each launch position's 32 back-to-back launches",
             "bytes_per_launch_def": "sum over the launch's matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y)"}
+
+
+def exact_decode(gh, L, decode_step, stream, args):
+    """The headline decode graph re-captured in exact mode (ggml_hip_set_exact): every mul_mat runs
+    algorithm 4, bit-identical to the reference's AVX2 ggml_vec_dot_q4_0_q8_0 (tests/test_gpu_exact.py)."""
+    prev = L.ggml_hip_get_exact()
+    gh.check(L.ggml_hip_set_exact(1))
+    try:
+        decode_step()
+        gh.check(L.ggml_hip_stream_synchronize(stream))
+        g = gh.Graph(stream)
+        with g:
+            decode_step()
+        for _ in range(args.warmup):
+            g.launch()
+        gh.check(L.ggml_hip_stream_synchronize(stream))
+        a, b = gh.Event(), gh.Event()
+        a.record(stream)
+        for _ in range(args.steps):
+            g.launch()
+        b.record(stream)
+        t = a.elapsed_ms(b) * 1e-3 / args.steps * 32 / args.layers
+        del g
+    finally:
+        L.ggml_hip_set_exact(prev)
+    return {"tok_s": round(1.0 / t, 2), "ms_per_token": round(t * 1e3, 4),
+            "numerics": "every y bit-identical to the reference's AVX2 ggml_vec_dot_q4_0_q8_0 (algo 4)"}
 
 
 def extra_decode(gh, L, stream, name, n_layers, spec, groups, steps=20, warmup=5):

@@ -214,6 +214,9 @@ struct WCacheHash {
     }
 };
 std::mutex g_wc_mu;
+// host copies made by ggml_hip_transform_tensor for tensors that stay on the CPU
+std::mutex g_host_copy_mu;
+std::unordered_map<const void *, void *> g_host_copies;
 std::unordered_map<WCacheKey, WCacheEntry, WCacheHash> g_wc;
 size_t g_wc_resident = 0;
 uint64_t g_wc_clock = 0, g_wc_hits = 0, g_wc_misses = 0;
@@ -533,6 +536,27 @@ void ggml_hip_transform_tensor(void *data, struct ggml_tensor *tensor_) {
     // ggml-cuda.cu:2766-2809
     ensure_init();
     tensor *t = (tensor *)tensor_;
+    if (t->type != gabi::TYPE_Q4_0 || g_device_count == 0) {
+        // Not on this backend's path (e.g. the F32 norm weights llama.cpp offloads with a layer,
+        // llama.cpp:1063-1070): ggml.c computes the ops that read them on the CPU and asserts CPU
+        // operands there (ggml.c:15650), so the tensor stays a CPU tensor, on a host copy this
+        // backend owns (the loader may free `data` after the call, llama.cpp:680-683).
+        const size_t bytes = gabi::nbytes(t);
+        void *h = malloc(bytes ? bytes : 1);
+        if (!h) {
+            fprintf(stderr, "ggml_hip_transform_tensor: host copy of %zu bytes failed\n", bytes);
+            abort();
+        }
+        memcpy(h, data, bytes);
+        {
+            std::lock_guard<std::mutex> lk(g_host_copy_mu);
+            g_host_copies[t] = h;
+        }
+        t->data = h;
+        t->backend = gabi::BACKEND_CPU;
+        t->extra = nullptr;
+        return;
+    }
     const int64_t nrows = gabi::nrows(t);
     const size_t nb1 = t->nb[1];
     auto *extra = new ggml_tensor_extra_gpu;
@@ -565,6 +589,16 @@ void ggml_hip_transform_tensor(void *data, struct ggml_tensor *tensor_) {
 void ggml_hip_free_data(struct ggml_tensor *tensor_) {
     // ggml-cuda.cu:2811-2828
     tensor *t = (tensor *)tensor_;
+    {
+        std::lock_guard<std::mutex> lk(g_host_copy_mu);
+        auto it = g_host_copies.find(t);
+        if (it != g_host_copies.end()) {      // a tensor transform_tensor kept on the CPU
+            if (t->data == it->second) t->data = nullptr;
+            free(it->second);
+            g_host_copies.erase(it);
+            return;
+        }
+    }
     if (!on_device(t) || !t->extra) return;
     ensure_init();
     auto *extra = (ggml_tensor_extra_gpu *)t->extra;

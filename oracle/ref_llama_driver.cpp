@@ -3,7 +3,8 @@
 // from /root/reference, loads a model file and evaluates a prompt.  Built twice by oracle/Makefile:
 // CPU-only (golden logits) and with -DGGML_USE_CUBLAS linked against libggml_hip_cuda.so, where
 // ggml.c's hooks send every Q4_0 mul_mat of a >= 32-token batch to the MI355X backend (weights stay
-// CPU tensors, n_gpu_layers = 0: the arch/-frontend situation; they hit the weight-residency cache).
+// CPU tensors at n_gpu_layers = 0, the arch/-frontend situation, and hit the weight-residency cache;
+// n_gpu_layers > 0 sends the offloaded layers' weights through the loader's transform_tensor).
 #include "llama.h"
 
 #include <execinfo.h>
@@ -24,8 +25,12 @@ static void refllama_segv(int sig) {   // REFLLAMA_BACKTRACE=1: native stack of 
     raise(sig);
 }
 
+// Evaluates the prompt (n_evals times from n_past = 0: repeated evals give the same logits), then
+// n_decode single-token steps (tokens decode_tokens[i] at n_past = n_tokens + i), whose logits go
+// to decode_out[i * n_vocab].  Returns n_vocab, or < 0 on error.
 extern "C" int refllama_logits(const char *path, const int *tokens, int n_tokens, int n_threads, int logits_all,
-                               float *out, int out_cap, int n_evals) {
+                               float *out, int out_cap, int n_evals, int n_gpu_layers, const int *decode_tokens,
+                               int n_decode, float *decode_out) {
     g_trace = getenv("REFLLAMA_BACKTRACE") != nullptr;
     if (g_trace) {   // own stack for the handler: a stack overflow must still print
         static char alt[1 << 16];
@@ -43,7 +48,7 @@ extern "C" int refllama_logits(const char *path, const int *tokens, int n_tokens
     llama_context_params p = llama_context_default_params();
     p.n_ctx = 256;
     p.n_batch = 512;
-    p.n_gpu_layers = 0;
+    p.n_gpu_layers = n_gpu_layers;   // > 0: the loader uploads those layers (llama.cpp:678-685)
     p.seed = 1;
     p.use_mmap = getenv("REFLLAMA_NO_MMAP") == nullptr;
     p.logits_all = logits_all != 0;
@@ -65,7 +70,11 @@ extern "C" int refllama_logits(const char *path, const int *tokens, int n_tokens
         const int rows = logits_all ? n_tokens : 1;
         const int cnt = rows * nv < out_cap ? rows * nv : out_cap;
         memcpy(out, llama_get_logits(c), sizeof(float) * (size_t)cnt);
-        rc = nv;
+        for (int i = 0; i < n_decode && rc == 0; i++) {
+            rc = llama_eval(c, (const llama_token *)&decode_tokens[i], 1, n_tokens + i, n_threads) ? -4 : 0;
+            if (rc == 0) memcpy(decode_out + (size_t)i * nv, llama_get_logits(c), sizeof(float) * (size_t)nv);
+        }
+        if (rc == 0) rc = nv;
     }
     llama_free(c);
     STAGE("context freed");

@@ -76,3 +76,4 @@ def write(path, hp=HP, seed=0x5EED9000):
 # 40 tokens (N >= 32: the reference's can_mul_mat sends the batch to the backend); BOS first
 # (llama_eval_internal requires it)
 PROMPT = [1] + [int(t) for t in (np.arange(1, 40) * 37 + 11) % HP["n_vocab"]]
+DECODE = [7, 123, 301]                      # single-token steps after the prompt (n_past = 40, 41, 42)

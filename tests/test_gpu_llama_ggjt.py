@@ -24,7 +24,7 @@ pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not os.path.exists(HIP_LIB), reason="oracle/_ref/libllama_ref_hip.so not built")]
 
 
-def run_llama(tmp_path, exact):
+def run_llama(tmp_path, exact, ngl):
     sys.path.insert(0, GOLD)
     from gen_llama_golden import ref_logits
     L = ggml_hip.load()
@@ -34,26 +34,39 @@ def run_llama(tmp_path, exact):
     mp = str(tmp_path / "m.ggjt")
     assert G.write(mp) == json.load(open(os.path.join(GOLD, "llama_tiny_manifest.json")))["model_sha256"]
     try:
-        got = ref_logits(HIP_LIB, mp, n_evals=2)
+        got, dec = ref_logits(HIP_LIB, mp, n_evals=2, n_gpu_layers=ngl, with_decode=True)
         h, m, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         ggml_hip.check(L.ggml_hip_weight_cache_stats(ctypes.byref(h), ctypes.byref(m), ctypes.byref(r)))
     finally:
         ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
         L.ggml_hip_set_exact(prev)
-    n_q4 = 7 * G.HP["n_layer"] + 1
-    assert (m.value, h.value) == (n_q4, n_q4), "every Q4_0 mul_mat ran on the backend (uploaded once, reused)"
-    return got, np.load(os.path.join(GOLD, "llama_tiny_logits.npy"))
+    # Q4_0 mul_mats whose weights stayed CPU tensors (llama.cpp:1053-1070: the last ngl layers, and
+    # the output matrix from ngl > n_layer, are offloaded through transform_tensor); those go through
+    # the residency cache on the two prompt evals (N = 40 >= 32); decode steps (N = 1) run them on the
+    # CPU (can_mul_mat), offloaded ones on the backend
+    nl = G.HP["n_layer"]
+    cpu_q4 = 7 * max(0, nl - ngl) + (1 if ngl <= nl else 0)
+    assert (m.value, h.value) == (cpu_q4, cpu_q4)
+    return (got, dec), (np.load(os.path.join(GOLD, "llama_tiny_logits.npy")),
+                        np.load(os.path.join(GOLD, "llama_tiny_decode_logits.npy")))
 
 
-def test_reference_llama_on_backend_exact_mode_bitwise(tmp_path):
-    got, gold = run_llama(tmp_path, exact=True)
+# n_gpu_layers: 0 (weights in the cache), 1 (one layer uploaded), 2 (all layers), 3 (+ output,
+# GPU_SPLIT), 99 (+ the F32 norms and the KV cache handed to the backend, which keeps them on the CPU)
+@pytest.mark.parametrize("ngl", [0, 1, 2, 3, 99])
+def test_reference_llama_on_backend_exact_mode_bitwise(tmp_path, ngl):
+    (got, dec), (gold, dgold) = run_llama(tmp_path, exact=True, ngl=ngl)
     assert np.array_equal(got.view(np.uint32), gold.view(np.uint32))
+    assert np.array_equal(dec.view(np.uint32), dgold.view(np.uint32))
 
 
-def test_reference_llama_on_backend_fast_kernels(tmp_path):
-    got, gold = run_llama(tmp_path, exact=False)
-    assert np.isfinite(got).all()
-    row = np.abs(got - gold).max(1) / np.abs(gold).max()
+@pytest.mark.parametrize("ngl", [0, 99])
+def test_reference_llama_on_backend_fast_kernels(tmp_path, ngl):
+    (got, dec), (gold, dgold) = run_llama(tmp_path, exact=False, ngl=ngl)
+    assert np.isfinite(got).all() and np.isfinite(dec).all()
+    scale = np.abs(gold).max()
+    row = np.abs(got - gold).max(1) / scale
     assert (row < 1e-5).mean() >= 0.75, row
     assert row.max() < 2e-2, row
     assert (got.argmax(1) == gold.argmax(1)).mean() >= 0.95
+    assert np.abs(dec - dgold).max() / scale < 2e-2

@@ -30,9 +30,11 @@ def test_reference_llama_cpu_reproduces_golden_logits(tmp_path):
     from gen_llama_golden import ref_logits
     mp = str(tmp_path / "m.ggjt")
     G.write(mp)
-    got = ref_logits(CPU_LIB, mp)
+    got, dec = ref_logits(CPU_LIB, mp, with_decode=True)
     gold = np.load(os.path.join(GOLD, "llama_tiny_logits.npy"))
     assert np.array_equal(got.view(np.uint32), gold.view(np.uint32))
+    dgold = np.load(os.path.join(GOLD, "llama_tiny_decode_logits.npy"))
+    assert np.array_equal(dec.view(np.uint32), dgold.view(np.uint32))
 
 
 HIP_LIB = os.path.join(ROOT, "oracle", "_ref", "libllama_ref_hip.so")
@@ -51,6 +53,8 @@ def test_reference_llama_gpu_build_without_device_declines_to_cpu(tmp_path):
     from gen_llama_golden import ref_logits
     mp = str(tmp_path / "m.ggjt")
     G.write(mp)
-    got = ref_logits(HIP_LIB, mp, n_evals=2)
+    got, dec = ref_logits(HIP_LIB, mp, n_evals=2, with_decode=True)
     gold = np.load(os.path.join(GOLD, "llama_tiny_logits.npy"))
     assert np.array_equal(got.view(np.uint32), gold.view(np.uint32))
+    dgold = np.load(os.path.join(GOLD, "llama_tiny_decode_logits.npy"))
+    assert np.array_equal(dec.view(np.uint32), dgold.view(np.uint32))

@@ -7,7 +7,7 @@ export PYTHONUNBUFFERED=1
 for r in $(seq 1 ${ROUNDS:-2}); do
   for spec in $SPECS; do
     name=${spec%%=*}; envs=${spec#*=}
-    env $(echo "$envs" | tr ',' ' ') timeout -k 10 240 python bench.py --steps 20 --warmup 3 --no-cpu --no-prefill \
+    env $(echo "$envs" | tr ',' ' ') timeout -k 10 240 python bench.py --steps 20 --warmup 3 --no-cpu --no-prefill --no-exact --no-extra \
         > gpurun_out/ab/$name.$r.log 2>&1
     rc=$?
     python - "$name" gpurun_out/ab/$name.$r.log <<'PY'

@@ -15,7 +15,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 export PYTHONUNBUFFERED=1
 STEPS=${STEPS:-pytest,smoke,bench,prof}
-[[ $STEPS == *pytest* ]] && step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *pytest* ]] && step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 [[ $STEPS == *smoke* ]] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]] && step bench 600 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-}
 if [[ $STEPS == *prof* ]]; then

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "ggml_abi.h"
+#include "ggml_ops.h"
 #include "q4_0_kernels.h"
 
 using gabi::tensor;
@@ -363,6 +364,381 @@ bool supported_mul_mat(const tensor *src0, const tensor *src1, const tensor *dst
            src0->ne[3] == src1->ne[3] && is_contiguous(src0) && is_contiguous(src1) && is_contiguous(dst);
 }
 
+[[noreturn]] void op_abort(const tensor *t, const char *why) {
+    // the reference asserts the same way (GGML_ASSERT in ggml-cuda.cu's op wrappers): a node that
+    // reaches a device op must be computable there, ggml.c cannot fall back once an operand is on
+    // the device (ggml.c:15650)
+    fprintf(stderr, "ggml_hip_compute_forward: op %d (%s): %s\n", t->op, t->name, why);
+    abort();
+}
+
+// ------------------------------------------------------------------------------------------
+// device storage of graph tensors (assign_buffers) and of uploaded tensors
+
+std::mutex g_own_mu;
+std::unordered_map<void *, int> g_owned;                 // hipMalloc'ed by this backend for a tensor
+std::unordered_map<const tensor *, ggml_tensor_extra_gpu *> g_graph_extra;   // reused across evals
+
+void own_device_buffer(void *p) {
+    std::lock_guard<std::mutex> lk(g_own_mu);
+    g_owned[p] = 1;
+}
+bool release_device_buffer(void *p) {      // true when p was allocated by this backend (free it)
+    std::lock_guard<std::mutex> lk(g_own_mu);
+    return g_owned.erase(p) != 0;
+}
+void forget_graph_extra(const tensor *t, ggml_tensor_extra_gpu *extra) {
+    std::lock_guard<std::mutex> lk(g_own_mu);
+    auto it = g_graph_extra.find(t);
+    if (it != g_graph_extra.end() && it->second == extra) g_graph_extra.erase(it);
+    delete extra;
+}
+
+// ggml-cuda.cu:2830-2892.  Graph tensors of an eval live in a context that is reset every eval, at
+// the same addresses: their extras are kept per tensor address and reused (the reference leaks one
+// per offloaded node per eval).
+void assign_buffers_impl(tensor *t, bool scratch, bool force_inplace) {
+    if (scratch && g_scratch_size == 0) return;
+    ensure_init();
+    if (g_device_count == 0) return;
+    // recursively assign buffers until a compute tensor is found
+    if (t->src0 && t->src0->backend == gabi::BACKEND_CPU) {
+        const int op0 = t->src0->op;
+        if (op0 == gabi::OP_RESHAPE || op0 == gabi::OP_TRANSPOSE || op0 == gabi::OP_VIEW)
+            assign_buffers_impl(t->src0, scratch, force_inplace);
+    }
+    if (t->op == gabi::OP_CPY && t->src1->backend == gabi::BACKEND_CPU) assign_buffers_impl(t->src1, scratch, force_inplace);
+
+    t->backend = gabi::BACKEND_GPU;
+    ggml_tensor_extra_gpu *extra;
+    {
+        std::lock_guard<std::mutex> lk(g_own_mu);
+        auto it = g_graph_extra.find(t);
+        if (it == g_graph_extra.end()) it = g_graph_extra.emplace(t, new ggml_tensor_extra_gpu).first;
+        extra = it->second;
+    }
+    memset(extra, 0, sizeof(*extra));
+    const bool inplace = (t->src0 && t->src0->data == t->data) || t->op == gabi::OP_VIEW || force_inplace;
+    const size_t size = gabi::nbytes(t);
+    const int id = g_main_device;
+    HIP_FATAL(hipSetDevice(id));
+    if (inplace && t->src0 && on_device(t->src0)) {
+        size_t offset = 0;
+        if (t->op == gabi::OP_VIEW) memcpy(&offset, t->opt[0]->data, sizeof(size_t));   // ggml_view_impl
+        extra->data_device[id] = (char *)((ggml_tensor_extra_gpu *)t->src0->extra)->data_device[id] + offset;
+    } else if (t->op == gabi::OP_CPY) {
+        extra->data_device[id] = ((ggml_tensor_extra_gpu *)t->src1->extra)->data_device[id];
+    } else if (scratch) {
+        if (size > g_scratch_size) {
+            fprintf(stderr, "ggml_hip_assign_buffers: tensor of %zu bytes exceeds the %zu-byte scratch\n", size,
+                    g_scratch_size);
+            abort();
+        }
+        if (g_scratch_offset + size > g_scratch_size) g_scratch_offset = 0;
+        if (!g_scratch) HIP_FATAL(hipMalloc(&g_scratch, g_scratch_size));
+        extra->data_device[id] = (char *)g_scratch + g_scratch_offset;
+        g_scratch_offset += (size + 255) & ~(size_t)255;    // 256-byte aligned slots (kernels load 16 B)
+    } else {
+        void *p = nullptr;
+        HIP_FATAL(hipMalloc(&p, size ? size : 1));
+        HIP_FATAL(hipMemset(p, 0, size));
+        own_device_buffer(p);
+        extra->data_device[id] = p;
+    }
+    t->extra = extra;
+}
+
+// ------------------------------------------------------------------------------------------
+// host-built lookup tables of the CPU ops (bit-exact restatements, ggml_ops.hip)
+
+uint16_t f32_to_f16_bits(float f) {          // GGML_FP32_TO_FP16 (F16C _cvtss_sh(x, 0): RNE)
+    const _Float16 h = (_Float16)f;
+    uint16_t b;
+    memcpy(&b, &h, 2);
+    return b;
+}
+float f16_bits_to_f32(uint16_t b) {
+    _Float16 h;
+    memcpy(&h, &b, 2);
+    return (float)h;
+}
+
+struct OpTables {
+    uint16_t *silu = nullptr;                // table_silu_f16 (ggml.c:4252)
+    uint16_t *exp = nullptr;                 // table_exp_f16  (ggml.c:4253)
+};
+std::mutex g_tab_mu;
+OpTables g_tabs[GGML_HIP_MAX_DEVICES];
+
+// ggml_init builds them as fp16(silu(f)) and fp16(expf(f)) for every fp16 bit pattern f with the
+// host libm (ggml.c:4246-4254); the same formula with the same libm gives the same 2 x 64 K entries
+const OpTables &op_tables(int id, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    OpTables &t = g_tabs[id];
+    if (!t.silu) {
+        std::vector<uint16_t> silu(65536), ex(65536);
+#pragma clang loop vectorize(disable)
+        for (int i = 0; i < 65536; i++) {
+            const float f = f16_bits_to_f32((uint16_t)i);
+            silu[i] = f32_to_f16_bits(f / (1.0f + expf(-f)));
+            ex[i] = f32_to_f16_bits(expf(f));
+        }
+        HIP_FATAL(hipMalloc(&t.silu, 2 * 65536 * sizeof(uint16_t)));
+        t.exp = t.silu + 65536;
+        HIP_FATAL(hipMemcpyAsync(t.silu, silu.data(), 65536 * 2, hipMemcpyHostToDevice, s));
+        HIP_FATAL(hipMemcpyAsync(t.exp, ex.data(), 65536 * 2, hipMemcpyHostToDevice, s));
+        HIP_FATAL(hipStreamSynchronize(s));
+    }
+    return t;
+}
+
+// rope (mode 0) cos/sin per position p and pair j of a row of ne0 values: theta starts at (float)p
+// and is multiplied by theta_scale = powf(10000.0, -2.0f/n_dims) once per pair, cos/sin by the host
+// libm (ggml.c:12772, 12811-12816).  One table per (ne0, n_dims), grown to the positions seen.
+struct RopeTable {
+    int64_t ne0 = 0;
+    int n_dims = 0;
+    int64_t npos = 0;
+    float *dev = nullptr;                    // float2 [npos][ne0/2]
+};
+std::vector<RopeTable> g_rope[GGML_HIP_MAX_DEVICES];
+
+const float *rope_table(int id, int64_t ne0, int n_dims, int64_t need_pos, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    RopeTable *rt = nullptr;
+    for (auto &r : g_rope[id])
+        if (r.ne0 == ne0 && r.n_dims == n_dims) rt = &r;
+    if (!rt) {
+        g_rope[id].push_back(RopeTable{});
+        rt = &g_rope[id].back();
+        rt->ne0 = ne0;
+        rt->n_dims = n_dims;
+    }
+    if (rt->npos < need_pos) {
+        int64_t npos = std::max<int64_t>(need_pos, 2 * rt->npos);
+        npos = std::max<int64_t>(npos, 512);
+        const int64_t np = ne0 / 2;
+        const float theta_scale = powf(10000.0, -2.0f / n_dims);
+        std::vector<float> h((size_t)(npos * np * 2));
+        for (int64_t p = 0; p < npos; p++) {
+            float theta = (float)p;
+            for (int64_t j = 0; j < np; j++) {
+                h[(size_t)(p * np + j) * 2] = cosf(theta);
+                h[(size_t)(p * np + j) * 2 + 1] = sinf(theta);
+                theta *= theta_scale;
+            }
+        }
+        if (rt->dev) {
+            HIP_FATAL(hipStreamSynchronize(s));   // earlier ropes may still read the old table
+            HIP_FATAL(hipFree(rt->dev));
+        }
+        HIP_FATAL(hipMalloc(&rt->dev, h.size() * sizeof(float)));
+        HIP_FATAL(hipMemcpyAsync(rt->dev, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, s));
+        HIP_FATAL(hipStreamSynchronize(s));
+        rt->npos = npos;
+    }
+    return rt->dev;
+}
+
+// ------------------------------------------------------------------------------------------
+// the non-Q4_0 device ops (ggml-cuda.cu:2569-2760 + ggml_cuda_op 2286-2567, restated): operands on
+// the device are used in place, host operands are staged through pool temporaries, a host dst is
+// downloaded; a node whose operands are all device resident is only enqueued (no synchronize)
+
+struct OpCall {
+    int id;
+    hipStream_t s;
+    std::vector<std::pair<void *, size_t>> tmp;
+    bool sync = false;
+    void *temp(size_t bytes) {
+        size_t a = 0;
+        void *p = pool_malloc(id, bytes ? bytes : 16, &a);
+        tmp.push_back({p, a});
+        return p;
+    }
+    // device address of t's data (host tensors uploaded; they must be contiguous)
+    char *in(const tensor *t) {
+        if (t->backend == gabi::BACKEND_GPU) return (char *)((ggml_tensor_extra_gpu *)t->extra)->data_device[id];
+        if (t->backend == gabi::BACKEND_GPU_SPLIT) op_abort(t, "row-split operand outside a Q4_0 mul_mat");
+        if (!is_contiguous(t)) op_abort(t, "non-contiguous host operand of a device op");
+        const size_t bytes = gabi::nbytes(t);
+        void *p = temp(bytes);
+        HIP_FATAL(hipMemcpyAsync(p, t->data, bytes, hipMemcpyHostToDevice, s));
+        sync = true;
+        return (char *)p;
+    }
+    char *out(const tensor *t) {
+        if (t->backend == gabi::BACKEND_GPU) return (char *)((ggml_tensor_extra_gpu *)t->extra)->data_device[id];
+        if (!is_contiguous(t)) op_abort(t, "non-contiguous host destination of a device op");
+        sync = true;
+        return (char *)temp(gabi::nbytes(t));
+    }
+    void finish(const tensor *dst, const char *d) {
+        if (dst->backend != gabi::BACKEND_GPU)
+            HIP_FATAL(hipMemcpyAsync(dst->data, d, gabi::nbytes(dst), hipMemcpyDeviceToHost, s));
+        if (sync) HIP_FATAL(hipStreamSynchronize(s));
+        for (auto &x : tmp) pool_free(id, x.first, x.second);
+    }
+};
+
+bool same_shape(const tensor *a, const tensor *b) {
+    return a->ne[0] == b->ne[0] && a->ne[1] == b->ne[1] && a->ne[2] == b->ne[2] && a->ne[3] == b->ne[3];
+}
+
+std::atomic<int64_t> g_op_count[gabi::OP_COUNT];      // device nodes run, per ggml op (debug stats)
+
+void run_device_op(tensor *t) {
+    const int op = t->op;
+    if (op >= 0 && op < gabi::OP_COUNT) g_op_count[op].fetch_add(1, std::memory_order_relaxed);
+    if (op == gabi::OP_RESHAPE || op == gabi::OP_VIEW || op == gabi::OP_PERMUTE || op == gabi::OP_TRANSPOSE) return;
+    const tensor *a = t->src0, *b = t->src1;
+    OpCall c{g_main_device, nullptr, {}};
+    HIP_FATAL(hipSetDevice(c.id));
+    c.s = g_dev[c.id].stream;
+    auto f32 = [&](const tensor *x) {
+        if (x->type != gabi::TYPE_F32) op_abort(t, "operand type must be F32");
+    };
+    switch (op) {
+        case gabi::OP_ADD: {                                     // ggml.c:8260
+            f32(a), f32(b), f32(t);
+            if (!same_shape(a, b) || !same_shape(a, t) || !is_contiguous(a) || !is_contiguous(b) || !is_contiguous(t))
+                op_abort(t, "add needs contiguous operands of one shape");
+            const char *pa = c.in(a), *pb = c.in(b);
+            char *d = c.out(t);
+            HIP_FATAL(ghip::op_add_f32((const float *)pa, (const float *)pb, (float *)d,
+                                       t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3], c.s));
+            c.finish(t, d);
+            return;
+        }
+        case gabi::OP_MUL: {                                     // ggml.c:9149 (rows of b repeat)
+            f32(a), f32(b), f32(t);
+            if (!same_shape(a, t) || b->ne[0] != a->ne[0] || a->ne[1] % b->ne[1] || a->ne[2] % b->ne[2] ||
+                a->ne[3] % b->ne[3] || !is_contiguous(a) || !is_contiguous(b) || !is_contiguous(t))
+                op_abort(t, "mul needs contiguous operands, b rows repeating over a");
+            const char *pa = c.in(a), *pb = c.in(b);
+            char *d = c.out(t);
+            HIP_FATAL(ghip::op_mul_f32((const float *)pa, (const float *)pb, (float *)d, a->ne[0], a->ne[1], a->ne[2],
+                                       a->ne[3], b->ne[1], b->ne[2], b->ne[3], c.s));
+            c.finish(t, d);
+            return;
+        }
+        case gabi::OP_SILU: {                                    // ggml.c:10188 (GGML_SILU_FP16)
+            f32(a), f32(t);
+            if (!same_shape(a, t) || !is_contiguous(a) || !is_contiguous(t)) op_abort(t, "silu needs contiguous operands");
+            const OpTables &tb = op_tables(c.id, c.s);
+            const char *pa = c.in(a);
+            char *d = c.out(t);
+            HIP_FATAL(ghip::op_silu_f32((const float *)pa, (float *)d, t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3],
+                                        tb.silu, c.s));
+            c.finish(t, d);
+            return;
+        }
+        case gabi::OP_RMS_NORM: {                                // ggml.c:10389
+            f32(a), f32(t);
+            if (!same_shape(a, t) || !is_contiguous(a) || !is_contiguous(t)) op_abort(t, "rms_norm needs contiguous rows");
+            const char *pa = c.in(a);
+            char *d = c.out(t);
+            HIP_FATAL(ghip::op_rms_norm_f32((const float *)pa, (float *)d, a->ne[0], gabi::nrows(a), a->ne[0], t->ne[0],
+                                            c.s));
+            c.finish(t, d);
+            return;
+        }
+        case gabi::OP_SCALE: {                                   // ggml.c:11633, scale factor read on the host
+            f32(a), f32(t);
+            if (!same_shape(a, t) || !is_contiguous(a) || !is_contiguous(t) || b->backend != gabi::BACKEND_CPU)
+                op_abort(t, "scale needs contiguous operands and a host scalar");
+            const float v = *(const float *)b->data;
+            const char *pa = c.in(a);
+            char *d = c.out(t);
+            HIP_FATAL(ghip::op_scale_f32((const float *)pa, (float *)d, v, t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3], c.s));
+            c.finish(t, d);
+            return;
+        }
+        case gabi::OP_DIAG_MASK_INF: {                           // ggml.c:12195
+            f32(a), f32(t);
+            if (!same_shape(a, t) || !is_contiguous(a) || !is_contiguous(t) || b->backend != gabi::BACKEND_CPU)
+                op_abort(t, "diag_mask_inf needs contiguous operands and host parameters");
+            const int n_past = ((const int32_t *)b->data)[0];
+            const char *pa = c.in(a);
+            char *d = c.out(t);
+            HIP_FATAL(ghip::op_diag_mask_inf_f32((const float *)pa, (float *)d, a->ne[0], gabi::nrows(a), a->ne[1], n_past,
+                                                 c.s));
+            c.finish(t, d);
+            return;
+        }
+        case gabi::OP_SOFT_MAX: {                                // ggml.c:12284
+            f32(a), f32(t);
+            if (!same_shape(a, t) || !is_contiguous(a) || !is_contiguous(t)) op_abort(t, "soft_max needs contiguous rows");
+            const OpTables &tb = op_tables(c.id, c.s);
+            const char *pa = c.in(a);
+            char *d = c.out(t);
+            HIP_FATAL(ghip::op_soft_max_f32((const float *)pa, (float *)d, a->ne[0], gabi::nrows(a), tb.exp, c.s));
+            c.finish(t, d);
+            return;
+        }
+        case gabi::OP_ROPE: {                                    // ggml.c:12714, mode 0 (LLaMA)
+            f32(a), f32(t);
+            if (b->backend != gabi::BACKEND_CPU) op_abort(t, "rope parameters must be a host tensor");
+            const int n_past = ((const int32_t *)b->data)[0];
+            const int n_dims = ((const int32_t *)b->data)[1];
+            const int mode = ((const int32_t *)b->data)[2];
+            if (mode != 0) op_abort(t, "only rope mode 0 is implemented on the device");
+            if (!same_shape(a, t) || a->nb[0] != 4 || t->nb[0] != 4 || a->ne[0] % 2 || n_dims % 2 || n_past < 0)
+                op_abort(t, "rope needs f32 rows of even length");
+            const int64_t np = a->ne[0] / 2;
+            const float *cs = rope_table(c.id, a->ne[0], n_dims, (int64_t)n_past + a->ne[2], c.s);
+            const char *pa = c.in(a);
+            char *d = c.out(t);
+            // a host source was uploaded contiguous: its strides are the contiguous ones
+            int64_t nbx[4], nbd[4];
+            for (int i = 0; i < 4; i++) {
+                nbx[i] = a->backend == gabi::BACKEND_GPU ? (int64_t)a->nb[i] : 0;
+                nbd[i] = t->backend == gabi::BACKEND_GPU ? (int64_t)t->nb[i] : 0;
+            }
+            if (a->backend != gabi::BACKEND_GPU) nbx[1] = a->ne[0] * 4, nbx[2] = nbx[1] * a->ne[1], nbx[3] = nbx[2] * a->ne[2];
+            if (t->backend != gabi::BACKEND_GPU) nbd[1] = t->ne[0] * 4, nbd[2] = nbd[1] * t->ne[1], nbd[3] = nbd[2] * t->ne[2];
+            HIP_FATAL(ghip::op_rope_f32(pa, d, a->ne, nbx, nbd, cs + (size_t)n_past * np * 2, (int)np, c.s));
+            c.finish(t, d);
+            return;
+        }
+        case gabi::OP_CPY: {                                     // ggml-cuda.cu:2690-2727: src0 -> src1 (a view)
+            if (a->type != gabi::TYPE_F32 || (b->type != gabi::TYPE_F32 && b->type != gabi::TYPE_F16))
+                op_abort(t, "cpy supports F32 -> F32 / F16");
+            if (a->backend != gabi::BACKEND_GPU || b->backend != gabi::BACKEND_GPU)
+                op_abort(t, "cpy needs both operands on the device (ggml-cuda.cu:2695-2696)");
+            if (a->ne[3] != 1 || b->ne[3] != 1) op_abort(t, "cpy supports 3-d tensors");
+            const int64_t n = a->ne[0] * a->ne[1] * a->ne[2];
+            if (n != b->ne[0] * b->ne[1] * b->ne[2]) op_abort(t, "cpy element counts differ");
+            const char *pa = c.in(a);
+            char *pb = (char *)((ggml_tensor_extra_gpu *)b->extra)->data_device[c.id];
+            HIP_FATAL(ghip::op_cpy_f32(pa, pb, b->type == gabi::TYPE_F16, n, a->ne[0], a->ne[1], a->nb[0], a->nb[1],
+                                       a->nb[2], b->ne[0], b->ne[1], b->nb[0], b->nb[1], b->nb[2], c.s));
+            c.finish(b, pb);
+            return;
+        }
+        case gabi::OP_MUL_MAT: {                                 // F16 x F32: ggml.c:11026 (attention on the KV cache)
+            if (b->type != gabi::TYPE_F32 || t->type != gabi::TYPE_F32 || a->nb[0] != 2 || b->nb[0] != 4)
+                op_abort(t, "f16 mul_mat needs F16 rows (nb00 = 2) x F32 rows (nb10 = 4) -> F32");
+            if (a->backend != gabi::BACKEND_GPU) op_abort(t, "f16 mul_mat needs src0 on the device");
+            if (a->ne[0] != b->ne[0] || a->ne[2] != b->ne[2] || a->ne[3] != 1 || b->ne[3] != 1 || t->ne[0] != a->ne[1] ||
+                t->ne[1] != b->ne[1] || t->ne[2] != a->ne[2] || !is_contiguous(t))
+                op_abort(t, "f16 mul_mat shape");
+            if (a->ne[0] > INT32_MAX) op_abort(t, "f16 mul_mat K too large");
+            const char *pa = c.in(a);
+            const char *pb = c.in(b);
+            int64_t nb11 = b->nb[1], nb12 = b->nb[2];
+            if (b->backend != gabi::BACKEND_GPU) nb11 = b->ne[0] * 4, nb12 = nb11 * b->ne[1];
+            char *d = c.out(t);
+            HIP_FATAL(ghip::op_mul_mat_f16_f32(pa, pb, (float *)d, (int)a->ne[0], a->ne[1], b->ne[1], a->ne[2], a->nb[1],
+                                               a->nb[2], nb11, nb12, c.s));
+            c.finish(t, d);
+            return;
+        }
+        default:
+            op_abort(t, "not a device op");
+    }
+}
+
 }  // namespace
 
 // ==========================================================================================
@@ -441,6 +817,7 @@ void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor 
             tmp.push_back({p, a});
             return p;
         };
+        bool need_sync = !dst_dev || split || !src0_dev;   // host dst, gathers, host weights (cache)
         for (int64_t b = 0; b < nbatch; b++) {
             // weights: resident slice, or upload the row slice (the reference re-uploads every
             // call too, ggml-cuda.cu:2496-2502)
@@ -507,7 +884,9 @@ void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor 
                 }
             }
         }
-        HIP_FATAL(hipStreamSynchronize(s));   // temporaries are reusable after this (ggml-cuda.cu:2546-2566)
+        // temporaries are reusable after this (ggml-cuda.cu:2546-2566); a call whose operands were all
+        // device resident stays stream-ordered (full offload: the next op runs on the same stream)
+        if (need_sync || !tmp.empty()) HIP_FATAL(hipStreamSynchronize(s));
         for (auto &t : tmp) pool_free(id, t.first, t.second);
     }
     HIP_FATAL(hipSetDevice(saved));
@@ -536,10 +915,9 @@ void ggml_hip_transform_tensor(void *data, struct ggml_tensor *tensor_) {
     // ggml-cuda.cu:2766-2809
     ensure_init();
     tensor *t = (tensor *)tensor_;
-    if (t->type != gabi::TYPE_Q4_0 || g_device_count == 0) {
-        // Not on this backend's path (e.g. the F32 norm weights llama.cpp offloads with a layer,
-        // llama.cpp:1063-1070): ggml.c computes the ops that read them on the CPU and asserts CPU
-        // operands there (ggml.c:15650), so the tensor stays a CPU tensor, on a host copy this
+    if ((t->type != gabi::TYPE_Q4_0 && t->type != gabi::TYPE_F32 && t->type != gabi::TYPE_F16) || g_device_count == 0) {
+        // A type no device op reads: ggml.c computes the ops that read it on the CPU and asserts
+        // CPU operands there (ggml.c:15650), so the tensor stays a CPU tensor, on a host copy this
         // backend owns (the loader may free `data` after the call, llama.cpp:680-683).
         const size_t bytes = gabi::nbytes(t);
         void *h = malloc(bytes ? bytes : 1);
@@ -557,6 +935,8 @@ void ggml_hip_transform_tensor(void *data, struct ggml_tensor *tensor_) {
         t->extra = nullptr;
         return;
     }
+    if (t->type != gabi::TYPE_Q4_0 && t->backend == gabi::BACKEND_GPU_SPLIT)
+        t->backend = gabi::BACKEND_GPU;   // only the Q4_0 mul_mat reads row-split operands
     const int64_t nrows = gabi::nrows(t);
     const size_t nb1 = t->nb[1];
     auto *extra = new ggml_tensor_extra_gpu;
@@ -581,6 +961,7 @@ void ggml_hip_transform_tensor(void *data, struct ggml_tensor *tensor_) {
         HIP_FATAL(hipMalloc(&buf, size));
         HIP_FATAL(hipMemcpy(buf, (const char *)data + lo * nb1, size, hipMemcpyHostToDevice));
         extra->data_device[id] = buf;
+        own_device_buffer(buf);
     }
     HIP_FATAL(hipSetDevice(saved));
     t->extra = extra;
@@ -604,22 +985,23 @@ void ggml_hip_free_data(struct ggml_tensor *tensor_) {
     auto *extra = (ggml_tensor_extra_gpu *)t->extra;
     const int saved = current_device();
     for (int id = 0; id < g_device_count; id++) {
-        if (!extra->data_device[id]) continue;
+        if (!extra->data_device[id] || !release_device_buffer(extra->data_device[id])) continue;
         HIP_FATAL(hipSetDevice(id));
         HIP_FATAL(hipFree(extra->data_device[id]));
     }
     HIP_FATAL(hipSetDevice(saved));
-    delete extra;
+    forget_graph_extra(t, extra);
     t->extra = nullptr;
 }
 
-// Graph-tensor offload (ggml-cuda.cu:2830-2904).  This backend implements only MUL_MAT, so a
-// tensor handed over for offload stays a CPU tensor: every op around the mul_mat keeps running on
-// the CPU with valid host data, and the mul_mat streams its activations over PCIe.  (Full
-// offload needs the remaining ops on the GPU — SURVEY.md §8f row 4, out of scope here.)
-void ggml_hip_assign_buffers(struct ggml_tensor *) {}
-void ggml_hip_assign_buffers_no_scratch(struct ggml_tensor *) {}
-void ggml_hip_assign_buffers_force_inplace(struct ggml_tensor *) {}
+// Graph-tensor offload (ggml-cuda.cu:2830-2904): the tensor becomes a device tensor; its storage
+// is its source's (in-place ops and views, at the view's byte offset), its copy target's (CPY), a
+// slot of the VRAM scratch ring (scratch: wraps to the start when full, as the reference does),
+// or its own zeroed buffer (no_scratch: the KV cache).  Every op of such a graph runs on the
+// device (ggml_hip_compute_forward), so activations stay resident across the layer.
+void ggml_hip_assign_buffers(struct ggml_tensor *t) { assign_buffers_impl((tensor *)t, true, false); }
+void ggml_hip_assign_buffers_no_scratch(struct ggml_tensor *t) { assign_buffers_impl((tensor *)t, false, false); }
+void ggml_hip_assign_buffers_force_inplace(struct ggml_tensor *t) { assign_buffers_impl((tensor *)t, false, true); }
 
 void ggml_hip_set_main_device(int main_device) {
     // ggml-cuda.cu:2906-2918
@@ -644,22 +1026,56 @@ void ggml_hip_free_scratch(void) {
 }
 
 bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_tensor *tensor_) {
-    // ggml-cuda.cu:2933-3021, MUL_MAT case: taken when any operand is device resident or
-    // can_mul_mat holds; only ith == 0 in COMPUTE executes (the others spin in ggml.c:17285-17287)
+    // ggml-cuda.cu:2933-3021: a node is taken when any operand is device resident (MUL_MAT also when
+    // can_mul_mat holds for host operands); only ith == 0 in COMPUTE executes (the other threads
+    // spin in ggml.c:17285-17287).  Q4_0 mul_mat -> the q4_0 kernels; F16 mul_mat (attention on the
+    // KV cache) and the other ops of a LLaMA layer -> ggml_ops.hip; views are free.
     const gabi::compute_params *params = (const gabi::compute_params *)params_;
     tensor *t = (tensor *)tensor_;
-    if (t->op != gabi::OP_MUL_MAT) return false;
-    if (!supported_mul_mat(t->src0, t->src1, t)) return false;
-    ensure_init();
-    if (g_device_count == 0) return false;
     const bool any_on_device = t->backend == gabi::BACKEND_GPU || on_device(t->src0) ||
                                (t->src1 && t->src1->backend == gabi::BACKEND_GPU);
-    if (!any_on_device && !ggml_hip_can_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1,
-                                                (ggml_tensor *)t))
-        return false;
+    bool f16_mul_mat = false;
+    switch (t->op) {
+        case gabi::OP_MUL_MAT:
+            if (t->src0 && t->src0->type == gabi::TYPE_F16) {
+                if (!any_on_device) return false;
+                f16_mul_mat = true;
+                break;
+            }
+            if (!supported_mul_mat(t->src0, t->src1, t)) return false;
+            ensure_init();
+            if (g_device_count == 0) return false;
+            if (!any_on_device && !ggml_hip_can_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1,
+                                                        (ggml_tensor *)t))
+                return false;
+            break;
+        case gabi::OP_ADD:
+        case gabi::OP_MUL:
+        case gabi::OP_SILU:
+        case gabi::OP_RMS_NORM:
+        case gabi::OP_SCALE:
+        case gabi::OP_CPY:
+        case gabi::OP_DIAG_MASK_INF:
+        case gabi::OP_SOFT_MAX:
+        case gabi::OP_ROPE:
+        case gabi::OP_RESHAPE:
+        case gabi::OP_VIEW:
+        case gabi::OP_PERMUTE:
+        case gabi::OP_TRANSPOSE:
+            if (!any_on_device) return false;
+            break;
+        default:
+            return false;
+    }
     if (params->ith != 0) return true;
     if (params->type == gabi::TASK_INIT || params->type == gabi::TASK_FINALIZE) return true;
-    ggml_hip_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1, (ggml_tensor *)t);
+    ensure_init();
+    if (t->op == gabi::OP_MUL_MAT && !f16_mul_mat) {
+        g_op_count[gabi::OP_MUL_MAT].fetch_add(1, std::memory_order_relaxed);
+        ggml_hip_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1, (ggml_tensor *)t);
+    }
+    else
+        run_device_op(t);
     return true;
 }
 
@@ -1083,6 +1499,15 @@ int ggml_hip_debug_set_gemv_policy(int map, int depth, int rowitems, int wg_per_
     if (map < -1 || map > 2 || depth < 0 || depth > 2 || rowitems < 0 || rowitems > 1 || wg_per_cu < 0)
         return fail(GGML_HIP_ERR_INVALID, "bad GEMV policy");
     ghip::gemv_set_policy(map, depth, rowitems, wg_per_cu);
+    return GGML_HIP_OK;
+}
+
+// not in the public header: nodes taken by ggml_hip_compute_forward per ggml op (counts[op], op < n);
+// reset when reset != 0 (tests check which ops of a full-offload graph ran on the device)
+int ggml_hip_debug_op_stats(int64_t *counts, int n, int reset) {
+    for (int i = 0; i < n && i < gabi::OP_COUNT; i++) counts[i] = g_op_count[i].load();
+    if (reset)
+        for (auto &c : g_op_count) c.store(0);
     return GGML_HIP_OK;
 }
 

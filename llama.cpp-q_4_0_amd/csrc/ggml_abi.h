@@ -15,10 +15,12 @@ constexpr int MAX_DIMS = 4;   // GGML_MAX_DIMS  ggml.h:196
 constexpr int MAX_OPT = 4;    // GGML_MAX_OPT   ggml.h:200
 constexpr int MAX_NAME = 48;  // GGML_MAX_NAME  ggml.h:201
 
-enum type : int { TYPE_F32 = 0, TYPE_F16 = 1, TYPE_Q4_0 = 2, TYPE_Q8_0 = 8, TYPE_COUNT = 19 };
+enum type : int { TYPE_F32 = 0, TYPE_F16 = 1, TYPE_Q4_0 = 2, TYPE_Q8_0 = 8, TYPE_I32 = 18, TYPE_COUNT = 19 };
 enum backend : int { BACKEND_CPU = 0, BACKEND_GPU = 10, BACKEND_GPU_SPLIT = 20 };   // ggml.h:257-261
-enum op : int { OP_NONE = 0, OP_MUL_MAT = 32, OP_RESHAPE = 38, OP_VIEW = 39, OP_PERMUTE = 40,
-                OP_TRANSPOSE = 41, OP_COUNT = 68 };
+// enum ggml_op (ggml.h:274-350, with the fork's GGML_OP_EXT_* at 28-31; tests/golden/ggml_op_enum.json)
+enum op : int { OP_NONE = 0, OP_ADD = 2, OP_MUL = 6, OP_SILU = 23, OP_RMS_NORM = 26, OP_MUL_MAT = 32, OP_SCALE = 34,
+                OP_CPY = 36, OP_RESHAPE = 38, OP_VIEW = 39, OP_PERMUTE = 40, OP_TRANSPOSE = 41,
+                OP_DIAG_MASK_INF = 45, OP_SOFT_MAX = 47, OP_ROPE = 49, OP_COUNT = 68 };
 enum task_type : int { TASK_INIT = 0, TASK_COMPUTE = 1, TASK_FINALIZE = 2 };
 
 struct tensor {
@@ -67,7 +69,9 @@ static_assert(offsetof(compute_params, wsize) == 16, "wsize");
 static_assert(offsetof(compute_params, wdata) == 24, "wdata");
 
 // GGML_TYPE_SIZE / GGML_BLCK_SIZE for the types this backend touches (ggml.c:3586-3620)
-inline size_t type_size(int t) { return t == TYPE_F32 ? 4 : t == TYPE_F16 ? 2 : t == TYPE_Q4_0 ? 18 : t == TYPE_Q8_0 ? 34 : 0; }
+inline size_t type_size(int t) {
+    return t == TYPE_F32 || t == TYPE_I32 ? 4 : t == TYPE_F16 ? 2 : t == TYPE_Q4_0 ? 18 : t == TYPE_Q8_0 ? 34 : 0;
+}
 inline int blck_size(int t) { return (t == TYPE_Q4_0 || t == TYPE_Q8_0) ? 32 : 1; }
 inline size_t nbytes(const tensor *t) {
     return (size_t)(t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]) * type_size(t->type) / blck_size(t->type);

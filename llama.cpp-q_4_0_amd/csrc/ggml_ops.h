@@ -1,0 +1,32 @@
+// ggml_ops.h — launchers of the non-matmul ggml ops (ggml_ops.hip).
+// All pointers are device pointers; strides are in bytes unless named ld*.  Internal to
+// libggml_hip.so: the boundary is ggml_hip_compute_forward (include/ggml-hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ghip {
+
+hipError_t op_add_f32(const float *a, const float *b, float *d, int64_t n, hipStream_t s);
+// d[r][c] = a[r][c] * b[row of b that row r repeats][c]; a, b, d contiguous
+hipError_t op_mul_f32(const float *a, const float *b, float *d, int64_t ne00, int64_t ne01, int64_t ne02, int64_t ne03,
+                      int64_t ne11, int64_t ne12, int64_t ne13, hipStream_t s);
+// table: 65536 fp16 bits, ggml's table_silu_f16 / table_exp_f16 (built on the host, same formula)
+hipError_t op_silu_f32(const float *x, float *d, int64_t n, const uint16_t *table, hipStream_t s);
+hipError_t op_scale_f32(const float *x, float *d, float v, int64_t n, hipStream_t s);
+hipError_t op_diag_mask_inf_f32(const float *x, float *d, int64_t ncols, int64_t nrows, int64_t rows_per_channel,
+                                int n_past, hipStream_t s);
+hipError_t op_rms_norm_f32(const float *x, float *d, int64_t ncols, int64_t nrows, int64_t ldx, int64_t ldd,
+                           hipStream_t s);
+hipError_t op_soft_max_f32(const float *x, float *d, int64_t ncols, int64_t nrows, const uint16_t *table, hipStream_t s);
+// mode-0 rope; cs = float2 (cos, sin) [ne[2] tokens][npairs = ne[0]/2], row 0 = position n_past
+hipError_t op_rope_f32(const void *x, void *d, const int64_t ne[4], const int64_t nbx[4], const int64_t nbd[4],
+                       const void *cs, int npairs, hipStream_t s);
+hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne00, int64_t ne01, int64_t nb00,
+                      int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11, int64_t nb10, int64_t nb11, int64_t nb12,
+                      hipStream_t s);
+// dst [ne02][ne11][ne01] f32 contiguous = src0 f16 rows (K, strides nb01/nb02) . fp16(src1 f32 rows)
+hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11, int64_t ne02,
+                              int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s);
+
+}  // namespace ghip

@@ -1,0 +1,300 @@
+// ggml_ops.hip — gfx950 kernels for the non-matmul ggml ops of a fully offloaded LLaMA layer
+// (SURVEY.md §8f row 4), each a restatement of the reference's CPU op so that a graph run on the
+// device reproduces ggml.c's results bit for bit:
+//
+//   add_f32          ggml_compute_forward_add_f32      ggml.c:8260   dst = a + b
+//   mul_f32          ggml_compute_forward_mul_f32      ggml.c:9149   dst = a * b (b rows broadcast)
+//   silu_f32         ggml_vec_silu_f32 (GGML_SILU_FP16) ggml.c:3531  y = table_silu_f16[fp16(x)]
+//   rms_norm_f32     ggml_compute_forward_rms_norm_f32 ggml.c:10389  double sum of x*x, eps 1e-6
+//   rope_f32         ggml_compute_forward_rope_f32     ggml.c:12714  mode 0; cos/sin from a host table
+//   diag_mask_inf    ggml_compute_forward_diag_mask_f32 ggml.c:12195
+//   soft_max_f32     ggml_compute_forward_soft_max_f32 ggml.c:12284  fp16 exp table, double sum
+//   scale_f32        ggml_compute_forward_scale_f32    ggml.c:11633
+//   cpy_f32_{f32,f16} ggml_compute_forward_dup (strided), GGML_FP32_TO_FP16 = RNE
+//   mul_mat_f16_f32  ggml_compute_forward_mul_mat_f16_f32 ggml.c:11026 + ggml_vec_dot_f16 ggml.c:2303
+//                    (src1 rounded to fp16, the AVX F16 lane schedule and reduction order)
+//
+// The transcendental parts (silu, exp, cos/sin) are NOT evaluated on the device: ggml.c itself
+// evaluates silu and exp through 64 K-entry fp16 tables built with the host libm (ggml.c:4246-4254),
+// and rope's cos/sin are host libm values too; the backend builds the same tables on the host
+// (ggml-hip.cpp) and the kernels look them up.  All other arithmetic is IEEE single/double in the
+// CPU's order (built with -ffp-contract=off; the sums the CPU forms in double are formed in double).
+// These are small, latency-bound launches (a decode layer moves a few KB through them); one wave
+// per row where the CPU reduces over a row, one lane per element otherwise.
+#include "ggml_ops.h"
+
+#include <cmath>
+
+namespace ghip {
+
+namespace {
+
+__device__ __forceinline__ float h2f_bits(uint16_t b) {
+    _Float16 h;
+    __builtin_memcpy(&h, &b, 2);
+    return (float)h;
+}
+__device__ __forceinline__ uint16_t f2h_bits(float f) {
+    asm volatile("" : "+v"(f));           // keep hipcc from folding into v_fma_mix (sign of zero)
+    const _Float16 h = (_Float16)f;       // v_cvt_f16_f32: round to nearest even (F16C _cvtss_sh(x, 0))
+    uint16_t b;
+    __builtin_memcpy(&b, &h, 2);
+    return b;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+constexpr int TPB = 256;
+
+inline unsigned blocks(int64_t n, int per = TPB) { return (unsigned)((n + per - 1) / per); }
+
+// ----------------------------------------------------------------------------------- elementwise
+__global__ __launch_bounds__(TPB) void k_add_f32(const float *a, const float *b, float *d, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i < n) d[i] = a[i] + b[i];
+}
+
+// src0/dst contiguous [ne03][ne02][ne01][ne00]; src1 contiguous [ne13][ne12][ne11][ne00], repeated
+__global__ __launch_bounds__(TPB) void k_mul_f32(const float *a, const float *b, float *d, int64_t ne00, int64_t ne01,
+                                                 int64_t ne02, int64_t nrows, int64_t ne11, int64_t ne12, int64_t ne13) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= nrows * ne00) return;
+    const int64_t r = i / ne00, c = i - r * ne00;
+    const int64_t i03 = r / (ne02 * ne01), i02 = (r / ne01) % ne02, i01 = r % ne01;
+    const int64_t rb = ((i03 % ne13) * ne12 + (i02 % ne12)) * ne11 + (i01 % ne11);
+    d[i] = a[i] * b[rb * ne00 + c];
+}
+
+__global__ __launch_bounds__(TPB) void k_silu_f32(const float *x, float *d, int64_t n, const uint16_t *table) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i < n) d[i] = h2f_bits(table[f2h_bits(x[i])]);
+}
+
+__global__ __launch_bounds__(TPB) void k_scale_f32(const float *x, float *d, float v, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i < n) d[i] = x[i] * v;
+}
+
+// rows [nrows][ncols] with row r in channel r / rows_per_channel at row j = r % rows_per_channel:
+// element i of row j becomes -inf when i > n_past + j (and i >= n_past, which that implies)
+__global__ __launch_bounds__(TPB) void k_diag_mask_inf_f32(const float *x, float *d, int64_t ncols, int64_t n,
+                                                           int64_t rows_per_channel, int n_past) {
+    const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (k >= n) return;
+    const int64_t r = k / ncols, i = k - r * ncols, j = r % rows_per_channel;
+    d[k] = i > n_past + j ? -INFINITY : x[k];
+}
+
+// ----------------------------------------------------------------------------------- row reductions
+// one wave per row: sum = (double)(x*x) over the row, mean = (float)(sum / n), scale = 1/sqrt(mean + eps)
+__global__ __launch_bounds__(TPB) void k_rms_norm_f32(const float *x, float *d, int64_t ncols, int64_t nrows,
+                                                      int64_t ldx, int64_t ldd) {
+    const int64_t r = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nrows) return;
+    const float *xr = x + r * ldx;
+    double s = 0.0;
+    for (int64_t i = lane; i < ncols; i += 64) {
+        const float v = xr[i];
+        s += (double)(v * v);
+    }
+    s = wave_sum_d(s);
+    const float mean = (float)(s / (double)ncols);
+    // (float)sqrt((double)v) is the correctly rounded sqrtf(v) (double has >= 2*24+2 bits)
+    const float scale = 1.0f / (float)__builtin_sqrt((double)(mean + 1e-6f));
+    float *dr = d + r * ldd;
+    for (int64_t i = lane; i < ncols; i += 64) dr[i] = xr[i] * scale;
+}
+
+// one wave per row: max, then val = exp_table[fp16(x - max)] (0 for -inf), double sum, y = val * (float)(1/sum)
+__global__ __launch_bounds__(TPB) void k_soft_max_f32(const float *x, float *d, int64_t ncols, int64_t nrows,
+                                                      const uint16_t *table) {
+    const int64_t r = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nrows) return;
+    const float *xr = x + r * ncols;
+    float *dr = d + r * ncols;
+    float mx = -INFINITY;
+    for (int64_t i = lane; i < ncols; i += 64) mx = fmaxf(mx, xr[i]);
+    mx = wave_max_f(mx);
+    double s = 0.0;
+    for (int64_t i = lane; i < ncols; i += 64) {
+        const float v = xr[i];
+        float e = 0.0f;
+        if (v != -INFINITY) {
+            e = h2f_bits(table[f2h_bits(v - mx)]);
+            s += (double)e;
+        }
+        dr[i] = e;
+    }
+    s = wave_sum_d(s);
+    const float inv = (float)(1.0 / s);
+    for (int64_t i = lane; i < ncols; i += 64) dr[i] = dr[i] * inv;
+}
+
+// ----------------------------------------------------------------------------------- rope (mode 0)
+// x/d: [ne3][ne2][ne1][ne0] with byte strides; token i2 uses position p = n_past + i2, pair j of a row
+// uses cs[(p - p0) * npairs + j] = (cos, sin) of theta_j (host libm, theta_j = p * theta_scale^j by
+// repeated float multiplication as ggml.c:12814 does)
+__global__ __launch_bounds__(TPB) void k_rope_f32(const char *x, char *d, int64_t ne0, int64_t ne1, int64_t ne2,
+                                                  int64_t nb01, int64_t nb02, int64_t nb03, int64_t nb1, int64_t nb2,
+                                                  int64_t nb3, int64_t n, const float2 *cs, int npairs) {
+    const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (k >= n) return;
+    const int64_t np = ne0 / 2;
+    const int64_t j = k % np;
+    const int64_t r = k / np;
+    const int64_t i1 = r % ne1, i2 = (r / ne1) % ne2, i3 = r / (ne1 * ne2);
+    const float2 t = cs[i2 * npairs + j];
+    const float *s = (const float *)(x + i3 * nb03 + i2 * nb02 + i1 * nb01) + 2 * j;
+    float *o = (float *)(d + i3 * nb3 + i2 * nb2 + i1 * nb1) + 2 * j;
+    const float x0 = s[0], x1 = s[1];
+    o[0] = x0 * t.x - x1 * t.y;
+    o[1] = x0 * t.y + x1 * t.x;
+}
+
+// ----------------------------------------------------------------------------------- cpy (strided)
+template <bool F16>
+__global__ __launch_bounds__(TPB) void k_cpy_f32(const char *x, char *d, int64_t n, int64_t ne00, int64_t ne01,
+                                                 int64_t nb00, int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11,
+                                                 int64_t nb10, int64_t nb11, int64_t nb12) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const int64_t i02 = i / (ne00 * ne01), i01 = (i / ne00) % ne01, i00 = i % ne00;
+    const int64_t i12 = i / (ne10 * ne11), i11 = (i / ne10) % ne11, i10 = i % ne10;
+    const float v = *(const float *)(x + i00 * nb00 + i01 * nb01 + i02 * nb02);
+    char *o = d + i10 * nb10 + i11 * nb11 + i12 * nb12;
+    if (F16)
+        *(uint16_t *)o = f2h_bits(v);
+    else
+        *(float *)o = v;
+}
+
+// ----------------------------------------------------------------------------------- f16 x f32 mul_mat
+// dst[i2][i1][i0] = ggml_vec_dot_f16(K, src0[i2][i0][:], fp16(src1[i2][i1][:])), src0 rows f16
+// (nb00 = 2), src1 rows f32 (nb10 = 4), arbitrary row/channel strides (the permuted K and the
+// transposed V views of the KV cache).  32 lanes per output = the 4 x 8 fp32 accumulator lanes of
+// the AVX F16 loop (element e < np goes to lane e % 32, fma in order of e); then GGML_F32x8_REDUCE
+// (accumulators (0+2)+(1+3), 128-bit halves, two hadds) and the tail e >= np added in double.
+__global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32(const char *s0, const char *s1, float *d, int K,
+                                                         int64_t ne01, int64_t ne11, int64_t ne02, int64_t nb01,
+                                                         int64_t nb02, int64_t nb11, int64_t nb12) {
+    const int64_t o = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 5;   // output index
+    const int l = threadIdx.x & 31;
+    const int64_t nout = ne01 * ne11 * ne02;
+    const bool valid = o < nout;
+    const int64_t oc = valid ? o : 0;
+    const int64_t i0 = oc % ne01, i1 = (oc / ne01) % ne11, i2 = oc / (ne01 * ne11);
+    const uint16_t *xr = (const uint16_t *)(s0 + i2 * nb02 + i0 * nb01);
+    const float *yr = (const float *)(s1 + i2 * nb12 + i1 * nb11);
+    const int np = K & ~31;
+    float acc = 0.0f;
+    for (int e = l; e < np; e += 32) acc = fmaf(h2f_bits(xr[e]), h2f_bits(f2h_bits(yr[e])), acc);
+    // lane = 8*j + m: a_m = s0 + s2, b_m = s1 + s3, c_m = a_m + b_m
+    const float p16 = __shfl_xor(acc, 16, 32);
+    const float a = acc + p16;                                        // lanes 0-7: s0+s2, 8-15: s1+s3
+    const float p8 = __shfl_xor(a, 8, 32);
+    const float c = a + p8;                                           // lanes 0-7: (s0+s2)+(s1+s3)
+    const float c4 = __shfl_xor(c, 4, 32);
+    const float t0 = c + c4;                                          // lanes 0-3: c_k + c_{k+4}
+    const float t01 = t0 + __shfl_xor(t0, 1, 32);                     // lane 0: t0_0 + t0_1, lane 2: t0_2 + t0_3
+    const float t23 = __shfl(t01, 2, 32);
+    const float res = t01 + t23;                                      // lane 0
+    if (l == 0 && valid) {
+        double sum = (double)res;
+        for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(yr[e])));
+        d[o] = (float)sum;
+    }
+}
+
+}  // namespace
+
+hipError_t op_add_f32(const float *a, const float *b, float *d, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_add_f32, dim3(blocks(n)), dim3(TPB), 0, s, a, b, d, n);
+    return hipGetLastError();
+}
+
+hipError_t op_mul_f32(const float *a, const float *b, float *d, int64_t ne00, int64_t ne01, int64_t ne02, int64_t ne03,
+                      int64_t ne11, int64_t ne12, int64_t ne13, hipStream_t s) {
+    const int64_t nrows = ne01 * ne02 * ne03;
+    if (nrows * ne00 <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mul_f32, dim3(blocks(nrows * ne00)), dim3(TPB), 0, s, a, b, d, ne00, ne01, ne02, nrows, ne11,
+                       ne12, ne13);
+    return hipGetLastError();
+}
+
+hipError_t op_silu_f32(const float *x, float *d, int64_t n, const uint16_t *table, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_silu_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, n, table);
+    return hipGetLastError();
+}
+
+hipError_t op_scale_f32(const float *x, float *d, float v, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scale_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, v, n);
+    return hipGetLastError();
+}
+
+hipError_t op_diag_mask_inf_f32(const float *x, float *d, int64_t ncols, int64_t nrows, int64_t rows_per_channel,
+                                int n_past, hipStream_t s) {
+    const int64_t n = ncols * nrows;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_diag_mask_inf_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, ncols, n, rows_per_channel, n_past);
+    return hipGetLastError();
+}
+
+hipError_t op_rms_norm_f32(const float *x, float *d, int64_t ncols, int64_t nrows, int64_t ldx, int64_t ldd,
+                           hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rms_norm_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, ldx, ldd);
+    return hipGetLastError();
+}
+
+hipError_t op_soft_max_f32(const float *x, float *d, int64_t ncols, int64_t nrows, const uint16_t *table, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_soft_max_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, table);
+    return hipGetLastError();
+}
+
+hipError_t op_rope_f32(const void *x, void *d, const int64_t ne[4], const int64_t nbx[4], const int64_t nbd[4],
+                       const void *cs, int npairs, hipStream_t s) {
+    const int64_t n = ne[0] / 2 * ne[1] * ne[2] * ne[3];
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rope_f32, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1], ne[2],
+                       nbx[1], nbx[2], nbx[3], nbd[1], nbd[2], nbd[3], n, (const float2 *)cs, npairs);
+    return hipGetLastError();
+}
+
+hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne00, int64_t ne01, int64_t nb00,
+                      int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11, int64_t nb10, int64_t nb11, int64_t nb12,
+                      hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (to_f16)
+        hipLaunchKernelGGL(k_cpy_f32<true>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, n, ne00, ne01,
+                           nb00, nb01, nb02, ne10, ne11, nb10, nb11, nb12);
+    else
+        hipLaunchKernelGGL(k_cpy_f32<false>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, n, ne00, ne01,
+                           nb00, nb01, nb02, ne10, ne11, nb10, nb11, nb12);
+    return hipGetLastError();
+}
+
+hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11, int64_t ne02,
+                              int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s) {
+    const int64_t nout = ne01 * ne11 * ne02;
+    if (nout <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mul_mat_f16_f32, dim3(blocks(nout * 32)), dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d,
+                       K, ne01, ne11, ne02, nb01, nb02, nb11, nb12);
+    return hipGetLastError();
+}
+
+}  // namespace ghip

@@ -1,9 +1,13 @@
 """The reference's unmodified llama.cpp (built with -DGGML_USE_CUBLAS, linked against
 libggml_hip_cuda.so) loads the tiny GGJT v3 LLaMA file with its own loader and evaluates a
-40-token prompt: ggml.c's can_mul_mat sends every Q4_0 mul_mat of the batch (2 layers x 7 + the
-output projection = 15 weight matrices, N = 40) to the MI355X backend, the CPU-backend weights go
-through the device residency cache, everything else stays on ggml's CPU ops.  The logits must
-match the reference's CPU-only golden logits within the propagated north-star tolerance."""
+40-token prompt and three decode steps.  At n_gpu_layers 0 ggml.c's can_mul_mat sends every Q4_0
+mul_mat of the batch (2 layers x 7 + the output projection, N = 40) to the MI355X backend through
+the weight-residency cache and everything else stays on ggml's CPU ops; with more offloaded layers
+the loader uploads their weights and norms and the graph's nodes run on the device (SURVEY §8f
+row 4: rms_norm, mul, add, silu, rope, scale, diag_mask_inf, soft_max, cpy into the KV cache, the
+f16 attention mul_mats), up to the whole layer stack with a device KV cache.  In exact mode the
+logits are bit-identical to the reference's CPU-only golden logits at every offload level; the
+fast kernels stay within the propagated north-star tolerance."""
 import ctypes
 import json
 import os
@@ -24,7 +28,17 @@ pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not os.path.exists(HIP_LIB), reason="oracle/_ref/libllama_ref_hip.so not built")]
 
 
-def run_llama(tmp_path, exact, ngl):
+OPS = json.load(open(os.path.join(GOLD, "ggml_op_enum.json")))
+
+
+def op_stats(L, reset=True):
+    L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    c = np.zeros(OPS["GGML_OP_COUNT"], np.int64)
+    ggml_hip.check(L.ggml_hip_debug_op_stats(c.ctypes.data, c.size, 1 if reset else 0), "op stats")
+    return c
+
+
+def run_llama(tmp_path, exact, ngl, stats=None):
     sys.path.insert(0, GOLD)
     from gen_llama_golden import ref_logits
     L = ggml_hip.load()
@@ -33,10 +47,13 @@ def run_llama(tmp_path, exact, ngl):
     ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
     mp = str(tmp_path / "m.ggjt")
     assert G.write(mp) == json.load(open(os.path.join(GOLD, "llama_tiny_manifest.json")))["model_sha256"]
+    op_stats(L)
     try:
         got, dec = ref_logits(HIP_LIB, mp, n_evals=2, n_gpu_layers=ngl, with_decode=True)
         h, m, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         ggml_hip.check(L.ggml_hip_weight_cache_stats(ctypes.byref(h), ctypes.byref(m), ctypes.byref(r)))
+        if stats is not None:
+            stats.append(op_stats(L))
     finally:
         ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
         L.ggml_hip_set_exact(prev)
@@ -51,13 +68,24 @@ def run_llama(tmp_path, exact, ngl):
                         np.load(os.path.join(GOLD, "llama_tiny_decode_logits.npy")))
 
 
-# n_gpu_layers: 0 (weights in the cache), 1 (one layer uploaded), 2 (all layers), 3 (+ output,
-# GPU_SPLIT), 99 (+ the F32 norms and the KV cache handed to the backend, which keeps them on the CPU)
-@pytest.mark.parametrize("ngl", [0, 1, 2, 3, 99])
+# n_gpu_layers (llama.cpp:1029-1076, 1117-1147, 1294-1313; n_layer = 2): 0 (weights in the cache),
+# 1 (one layer's weights and norms on the device, its activations in the VRAM scratch), 2 (all
+# layers), 3 (+ the final norm and the row-split output matrix), 4 (+ the V cache and the attention
+# ops that read it), 5 = 99 (+ the K cache: the whole graph but get_rows and the last mul on the device)
+@pytest.mark.parametrize("ngl", [0, 1, 2, 3, 4, 99])
 def test_reference_llama_on_backend_exact_mode_bitwise(tmp_path, ngl):
-    (got, dec), (gold, dgold) = run_llama(tmp_path, exact=True, ngl=ngl)
+    stats = []
+    (got, dec), (gold, dgold) = run_llama(tmp_path, exact=True, ngl=ngl, stats=stats)
     assert np.array_equal(got.view(np.uint32), gold.view(np.uint32))
     assert np.array_equal(dec.view(np.uint32), dgold.view(np.uint32))
+    ran = stats[0]
+    nl = G.HP["n_layer"]
+    if ngl >= 1:     # an offloaded layer's norms, residual adds and FFN ops ran on the device
+        for op in ("GGML_OP_RMS_NORM", "GGML_OP_MUL", "GGML_OP_ADD", "GGML_OP_SILU"):
+            assert ran[OPS[op]] > 0, op
+    if ngl > nl + 2:  # full offload: the attention ops on the device KV cache too
+        for op in ("GGML_OP_ROPE", "GGML_OP_SCALE", "GGML_OP_DIAG_MASK_INF", "GGML_OP_SOFT_MAX", "GGML_OP_CPY"):
+            assert ran[OPS[op]] > 0, op
 
 
 @pytest.mark.parametrize("ngl", [0, 99])

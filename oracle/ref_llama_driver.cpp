@@ -8,6 +8,8 @@
 #include "llama.h"
 
 #include <execinfo.h>
+#include <chrono>
+#include <vector>
 #include <csignal>
 #include <cstdio>
 #include <cstdlib>
@@ -78,6 +80,54 @@ extern "C" int refllama_logits(const char *path, const int *tokens, int n_tokens
     }
     llama_free(c);
     STAGE("context freed");
+    llama_free_model(m);
+    return rc;
+}
+
+// End-to-end timing (tools/e2e_llama.py): load, evaluate an n_prompt-token prompt (reps times from
+// n_past = 0), then n_decode single-token evals; wall times via steady_clock around llama_eval.
+// out[0] = load s, out[1] = prompt ms (mean over reps), out[2] = decode ms per token; the logits of
+// the last decode step go to last_logits[0..n_vocab).  Returns n_vocab or < 0.
+extern "C" int refllama_bench(const char *path, int n_prompt, int n_decode, int n_threads, int n_gpu_layers, int n_ctx,
+                              int reps, double *out, float *last_logits) {
+    using clk = std::chrono::steady_clock;
+    llama_init_backend(false);
+    llama_context_params p = llama_context_default_params();
+    p.n_ctx = n_ctx;
+    p.n_batch = 512;
+    p.n_gpu_layers = n_gpu_layers;
+    p.seed = 1;
+    const auto t0 = clk::now();
+    llama_model *m = llama_load_model_from_file(path, p);
+    if (!m) return -1;
+    llama_context *c = llama_new_context_with_model(m, p);
+    if (!c) {
+        llama_free_model(m);
+        return -2;
+    }
+    out[0] = std::chrono::duration<double>(clk::now() - t0).count();
+    const int nv = llama_n_vocab(c);
+    std::vector<llama_token> toks(n_prompt);
+    for (int i = 0; i < n_prompt; i++) toks[i] = i == 0 ? 1 : (llama_token)((i * 7919 + 13) % nv);
+    int rc = 0;
+    double prompt_ms = 0;
+    for (int r = 0; r < reps && rc == 0; r++) {
+        const auto a = clk::now();
+        rc = llama_eval(c, toks.data(), n_prompt, 0, n_threads) ? -3 : 0;
+        prompt_ms += std::chrono::duration<double, std::milli>(clk::now() - a).count();
+    }
+    out[1] = prompt_ms / (reps > 0 ? reps : 1);
+    const auto a = clk::now();
+    for (int i = 0; i < n_decode && rc == 0; i++) {
+        const llama_token t = (llama_token)((i * 104729 + 7) % nv);
+        rc = llama_eval(c, &t, 1, n_prompt + i, n_threads) ? -4 : 0;
+    }
+    out[2] = n_decode > 0 ? std::chrono::duration<double, std::milli>(clk::now() - a).count() / n_decode : 0.0;
+    if (rc == 0) {
+        memcpy(last_logits, llama_get_logits(c), sizeof(float) * (size_t)nv);
+        rc = nv;
+    }
+    llama_free(c);
     llama_free_model(m);
     return rc;
 }

@@ -1,0 +1,145 @@
+"""End-to-end LLaMA-7B-shaped decode through the reference's own llama.cpp on the backend.
+
+Writes a GGJT v3 q4_0 model of LLaMA-7B shape (n_vocab 32000, n_embd 4096, n_head 32, n_layer 32,
+n_ff 11008; random valid q4_0 blocks, F32 norms ~ 1; no checkpoint exists offline) and evaluates it
+with oracle/_ref's builds of the reference llama.cpp + ggml.c (the caller side, unmodified):
+  cpu     libllama_ref_cpu.so  (ggml.c's AVX2 path, N_CPU threads)
+  offload libllama_ref_hip.so  n_gpu_layers = 99: weights, norms, KV cache and every node but the
+          token embedding lookup on the MI355X, fast and exact mode.
+Reports load time, prompt ms, decode ms/token and tok/s; checks that exact mode's last logits are
+bitwise equal to the CPU's (and the fast kernels' within tolerance).
+This measures the reference's host executor around the backend (graph build + ggml_graph_compute
+per token), not a kernel: the kernel numbers are bench.py's.
+
+  python tools/e2e_llama.py [--decode 64] [--threads-cpu 16] [--out profiles/r01_e2e_llama7b.json]
+"""
+import argparse
+import ctypes
+import json
+import os
+import struct
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "llama.cpp-q_4_0_amd", "python")]
+CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "libllama_ref_cpu.so")
+HIP_LIB = os.path.join(ROOT, "oracle", "_ref", "libllama_ref_hip.so")
+HP7B = dict(n_vocab=32000, n_embd=4096, n_mult=256, n_head=32, n_layer=32, n_rot=128, ftype=2)
+
+
+def n_ff(hp):
+    return ((2 * (4 * hp["n_embd"]) // 3 + hp["n_mult"] - 1) // hp["n_mult"]) * hp["n_mult"]   # llama.cpp:935
+
+
+def write_model(path, hp, seed=7):
+    """GGJT v3 (llama.cpp:383-503): header, vocab, then per tensor a record and 32-byte aligned data."""
+    rng = np.random.default_rng(seed)
+    E, V, F = hp["n_embd"], hp["n_vocab"], n_ff(hp)
+
+    def q4(ne):
+        nblk = ne[0] * ne[1] // 32
+        b = np.frombuffer(rng.bytes(nblk * 18), np.uint8).reshape(nblk, 18).copy()
+        d = rng.uniform(0.0015, 0.0035, nblk).astype(np.float16).view(np.uint8).reshape(nblk, 2)
+        b[:, :2] = d
+        return 2, ne, b
+
+    def f32(ne):
+        return 0, ne, (1.0 + 0.05 * rng.standard_normal(int(np.prod(ne)))).astype(np.float32)
+
+    specs = [("tok_embeddings.weight", lambda: q4((E, V))), ("norm.weight", lambda: f32((E,))),
+             ("output.weight", lambda: q4((E, V)))]
+    for i in range(hp["n_layer"]):
+        p = f"layers.{i}."
+        specs.append((p + "attention_norm.weight", lambda: f32((E,))))
+        for w in ("wq", "wk", "wv", "wo"):
+            specs.append((p + f"attention.{w}.weight", lambda: q4((E, E))))
+        specs.append((p + "ffn_norm.weight", lambda: f32((E,))))
+        specs.append((p + "feed_forward.w1.weight", lambda: q4((E, F))))
+        specs.append((p + "feed_forward.w2.weight", lambda: q4((F, E))))
+        specs.append((p + "feed_forward.w3.weight", lambda: q4((E, F))))
+    with open(path, "wb") as f:
+        f.write(struct.pack("<II", 0x67676A74, 3))
+        f.write(struct.pack("<7I", hp["n_vocab"], hp["n_embd"], hp["n_mult"], hp["n_head"], hp["n_layer"],
+                            hp["n_rot"], hp["ftype"]))
+        for i in range(hp["n_vocab"]):
+            tok = f"<t{i}>".encode()
+            f.write(struct.pack("<I", len(tok)) + tok + struct.pack("<f", -float(i)))
+        for name, gen in specs:
+            typ, ne, data = gen()
+            nb = name.encode()
+            f.write(struct.pack("<III", len(ne), len(nb), typ) + struct.pack(f"<{len(ne)}I", *ne) + nb)
+            f.write(b"\0" * (-f.tell() & 31))
+            f.write(data.tobytes())
+    return os.path.getsize(path)
+
+
+def bench(lib_path, model, n_prompt, n_decode, threads, ngl, reps, nv):
+    lib = ctypes.CDLL(lib_path)
+    lib.refllama_bench.restype = ctypes.c_int
+    lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    out = np.zeros(3, np.float64)
+    logits = np.zeros(nv, np.float32)
+    rc = lib.refllama_bench(model.encode(), n_prompt, n_decode, threads, ngl, 512, reps, out.ctypes.data,
+                            logits.ctypes.data)
+    if rc != nv:
+        raise RuntimeError(f"refllama_bench({lib_path}) failed: {rc}")
+    return {"load_s": round(out[0], 2), "prompt_tokens": n_prompt, "prompt_ms": round(out[1], 2),
+            "decode_tokens": n_decode, "decode_ms_per_token": round(out[2], 3),
+            "decode_tok_s": round(1e3 / out[2], 2) if out[2] > 0 else None, "threads": threads,
+            "n_gpu_layers": ngl}, logits
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--decode", type=int, default=64)
+    ap.add_argument("--decode-cpu", type=int, default=8)
+    ap.add_argument("--prompt", type=int, default=8)
+    ap.add_argument("--threads-cpu", type=int, default=16)
+    ap.add_argument("--threads-gpu", type=int, default=1)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    import ggml_hip as gh
+    L = gh.load()
+    d = tempfile.mkdtemp(prefix="e2e7b_", dir=os.environ.get("E2E_DIR", "/tmp"))
+    model = os.path.join(d, "llama7b-q4_0-synthetic.ggjt")
+    t0 = time.time()
+    size = write_model(model, HP7B)
+    print(f"model {size / 1e9:.2f} GB written in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    nv = HP7B["n_vocab"]
+    res = {"model": "LLaMA-7B shape, GGJT v3 q4_0, random valid blocks (synthetic)", "model_bytes": size,
+           "caller": "reference llama.cpp + ggml.c (oracle/_ref builds, unmodified sources)", "n_ctx": 512}
+    try:
+        if not args.no_cpu:
+            res["cpu"], lg_cpu = bench(CPU_LIB, model, args.prompt, args.decode_cpu, args.threads_cpu, 0, 1, nv)
+            print("cpu", res["cpu"], file=sys.stderr, flush=True)
+        for mode in ("fast", "exact"):
+            gh.check(L.ggml_hip_set_exact(1 if mode == "exact" else 0))
+            r, lg = bench(HIP_LIB, model, args.prompt, args.decode, args.threads_gpu, 99, 3, nv)
+            r["finite"] = bool(np.isfinite(lg).all())
+            if not args.no_cpu:       # same token sequence as the CPU run: compare the last logits
+                _, lg8 = bench(HIP_LIB, model, args.prompt, args.decode_cpu, args.threads_gpu, 99, 1, nv)
+                scale = float(np.abs(lg_cpu).max())
+                r["last_logits_vs_cpu"] = ("bitwise" if np.array_equal(lg8.view(np.uint32), lg_cpu.view(np.uint32))
+                                           else f"max |d|/max|y| {float(np.abs(lg8 - lg_cpu).max()) / scale:.2e}")
+            res[f"offload_{mode}"] = r
+            print(mode, r, file=sys.stderr, flush=True)
+        gh.check(L.ggml_hip_set_exact(0))
+    finally:
+        os.remove(model)
+        os.rmdir(d)
+    if "cpu" in res:
+        res["cpu_cpu_name"] = open("/proc/cpuinfo").read().split("model name")[1].split(":")[1].split("\n")[0].strip()
+    line = json.dumps(res)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -468,8 +468,9 @@ def cpu_baseline(budget_s):
     LLaMA-7B layers (> LLC), tok/s = 1 / (32 x layer time).
 
     kind "reference": the reference's own ggml.c (oracle/_ref, compiled from /root/reference by
-    oracle/Makefile, AVX2/FMA/F16C branches) driven through ggml_mul_mat + ggml_graph_compute per
-    matmul (oracle/ref_bench.c).  kind "port" (only when oracle/_ref was not built): the oracle's
+    oracle/Makefile, AVX2/FMA/F16C branches): the mul_mat nodes of the rotating layer copies in one
+    ggml graph per pass, one ggml_graph_compute each (oracle/ref_bench.c), as llama.cpp computes one
+    graph per token.  kind "port" (only when oracle/_ref was not built): the oracle's
     AVX2 restatement with the same row split and per-call thread spawn."""
     nthreads = int(os.environ.get("CPU_BASELINE_THREADS", min(16, os.cpu_count() or 1)))
     n_copies = 6                                   # ~680 MB of weights: beyond any host LLC
@@ -481,18 +482,20 @@ def cpu_baseline(budget_s):
         R.ref_layers_create.argtypes = [ctypes.c_int, ctypes.c_int]
         R.ref_layer_run.restype = ctypes.c_double
         R.ref_layer_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        R.ref_stack_run.restype = ctypes.c_double
+        R.ref_stack_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         R.ref_layers_destroy.argtypes = [ctypes.c_void_p, ctypes.c_int]
         h = R.ref_layers_create(n_copies, 1)
-        R.ref_layer_run(h, 0, nthreads)            # warm
+        R.ref_stack_run(h, n_copies, nthreads)     # warm
         total, n_layers_run = 0.0, 0
         while total < budget_s:
-            total += R.ref_layer_run(h, n_layers_run % n_copies, nthreads)
-            n_layers_run += 1
+            total += R.ref_stack_run(h, n_copies, nthreads)
+            n_layers_run += n_copies
         R.ref_layers_destroy(h, n_copies)
         t = total / n_layers_run
         kind = "reference"
-        what = ("reference ggml.c (oracle/_ref, -march=x86-64-v3) ggml_mul_mat + ggml_graph_compute per "
-                f"matmul, n_threads={nthreads}")
+        what = ("reference ggml.c (oracle/_ref, -march=x86-64-v3): the layers' ggml_mul_mat nodes in one graph, "
+                f"one ggml_graph_compute per pass (as llama.cpp per token), n_threads={nthreads}")
     else:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O

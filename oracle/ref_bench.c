@@ -2,9 +2,12 @@
  * ref_bench.c — TEST INFRASTRUCTURE ONLY: times the REFERENCE ggml CPU path (ggml.c compiled
  * from /root/reference into oracle/_ref by oracle/Makefile) for bench.py's cpu_baseline.
  *
- * One "layer" = the 7 q4_0 mul_mats of a LLaMA-7B decoder layer, each a ggml_mul_mat node
- * computed by ggml_graph_compute with n_threads worker threads (threads spawned per graph
+ * One "layer" = the 7 q4_0 mul_mats of a LLaMA-7B decoder layer, ggml_mul_mat nodes.  ref_stack_run
+ * puts the mul_mats of all n_layers layer copies into ONE graph and runs one ggml_graph_compute with
+ * n_threads worker threads, as llama.cpp runs one graph per token (threads spawned once per graph
  * compute, ggml.c:17540-17571; INIT q8_0 on one thread, COMPUTE row split, ggml.c:11226-11411).
+ * ref_layer_run (one graph per mul_mat) is kept for comparison: its per-call thread spawn adds
+ * ~0.5 ms per mul_mat.
  * The weights are filled with a repeating pattern of valid q4_0 blocks: the timing does not
  * depend on the values.
  */
@@ -59,6 +62,20 @@ double ref_layer_run(void *h, int l, int n_threads) {
         gf.n_threads = n_threads;
         ggml_graph_compute(L[l].ctx, &gf);
     }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* all n_layers layers (7 x n_layers mul_mat nodes) in one graph, one ggml_graph_compute; seconds */
+double ref_stack_run(void *h, int n_layers, int n_threads) {
+    struct ref_layer *L = (struct ref_layer *)h;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    struct ggml_cgraph gf = ggml_build_forward(L[0].out[0]);
+    for (int l = 0; l < n_layers; l++)
+        for (int i = 0; i < 7; i++) ggml_build_forward_expand(&gf, L[l].out[i]);
+    gf.n_threads = n_threads;
+    ggml_graph_compute(L[0].ctx, &gf);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

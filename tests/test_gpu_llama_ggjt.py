@@ -98,3 +98,39 @@ def test_reference_llama_on_backend_fast_kernels(tmp_path, ngl):
     assert row.max() < 2e-2, row
     assert (got.argmax(1) == gold.argmax(1)).mean() >= 0.95
     assert np.abs(dec - dgold).max() / scale < 2e-2
+
+
+CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "libllama_ref_cpu.so")
+
+
+@pytest.mark.skipif(not os.path.exists(CPU_LIB), reason="oracle/_ref/libllama_ref_cpu.so not built")
+def test_long_decode_full_offload_exact_bitwise(tmp_path):
+    """600 single-token steps at full offload (KV cache, rope positions and soft_max rows up to 608,
+    the rope table regrown past its first 512 positions): the last logits equal the reference's
+    CPU-only build bit for bit (both run live on this host through refllama_bench)."""
+    L = ggml_hip.load()
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp)
+    nv = G.HP["n_vocab"]
+
+    def run(lib_path, ngl):
+        lib = ctypes.CDLL(lib_path)
+        lib.refllama_bench.restype = ctypes.c_int
+        lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+        out = np.zeros(3, np.float64)
+        lg = np.zeros(nv, np.float32)
+        assert lib.refllama_bench(mp.encode(), 8, 600, 1, ngl, 1024, 1, out.ctypes.data, lg.ctypes.data) == nv
+        return lg
+
+    prev = L.ggml_hip_get_exact()
+    ggml_hip.check(L.ggml_hip_set_exact(1), "set_exact")
+    op_stats(L)
+    try:
+        got = run(HIP_LIB, 99)
+        ran = op_stats(L)
+    finally:
+        L.ggml_hip_set_exact(prev)
+    ref = run(CPU_LIB, 0)
+    assert np.isfinite(ref).all()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert ran[OPS["GGML_OP_SOFT_MAX"]] >= 600 * G.HP["n_layer"]

@@ -21,9 +21,8 @@ extern "C" {
 
 void   ggml_init_cublas(void);                                           /* ggml-cuda.h:15 */
 void   ggml_cuda_set_tensor_split(const float *tensor_split);            /* ggml-cuda.h:16 */
-/* ggml-cuda.h:18: element-wise mul is outside this backend's scope (ggml_cuda_compute_forward
- * never routes GGML_OP_MUL here); calling it is a fatal error with a message. */
-void   ggml_cuda_mul(const struct ggml_tensor *src0, const struct ggml_tensor *src1, struct ggml_tensor *dst);
+void   ggml_cuda_mul(const struct ggml_tensor *src0, const struct ggml_tensor *src1,
+                     struct ggml_tensor *dst);                           /* ggml-cuda.h:18 */
 bool   ggml_cuda_can_mul_mat(const struct ggml_tensor *src0, const struct ggml_tensor *src1,
                              struct ggml_tensor *dst);                   /* ggml-cuda.h:19 */
 size_t ggml_cuda_mul_mat_get_wsize(const struct ggml_tensor *src0, const struct ggml_tensor *src1,

@@ -70,6 +70,9 @@ size_t ggml_hip_mul_mat_get_wsize(const struct ggml_tensor *src0, const struct g
  * is a host tensor. */
 void   ggml_hip_mul_mat(const struct ggml_tensor *src0, const struct ggml_tensor *src1,
                         struct ggml_tensor *dst);
+/* ggml_cuda_mul (ggml-cuda.h:18, ggml-cuda.cu:2580-2583): dst = src0 * src1 (F32, src1 rows
+ * repeated over src0), on the device, operands host or device resident. */
+void   ggml_hip_mul(const struct ggml_tensor *src0, const struct ggml_tensor *src1, struct ggml_tensor *dst);
 /* ggml_cuda_host_malloc / host_free (ggml-cuda.h:24-25): pinned host memory, NULL on failure. */
 void  *ggml_hip_host_malloc(size_t size);
 void   ggml_hip_host_free(void *ptr);

@@ -9,9 +9,8 @@ extern "C" {
 
 void ggml_init_cublas(void) { ggml_init_hip(); }
 void ggml_cuda_set_tensor_split(const float *tensor_split) { ggml_hip_set_tensor_split(tensor_split); }
-void ggml_cuda_mul(const struct ggml_tensor *, const struct ggml_tensor *, struct ggml_tensor *) {
-    fprintf(stderr, "ggml-hip: ggml_cuda_mul (element-wise GGML_OP_MUL) is not provided by this backend\n");
-    abort();
+void ggml_cuda_mul(const struct ggml_tensor *src0, const struct ggml_tensor *src1, struct ggml_tensor *dst) {
+    ggml_hip_mul(src0, src1, dst);
 }
 bool ggml_cuda_can_mul_mat(const struct ggml_tensor *src0, const struct ggml_tensor *src1, struct ggml_tensor *dst) {
     return ggml_hip_can_mul_mat(src0, src1, dst);

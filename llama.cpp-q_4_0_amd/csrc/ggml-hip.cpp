@@ -892,6 +892,16 @@ void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor 
     HIP_FATAL(hipSetDevice(saved));
 }
 
+void ggml_hip_mul(const struct ggml_tensor *src0, const struct ggml_tensor *src1, struct ggml_tensor *dst) {
+    // ggml_cuda_mul (ggml-cuda.cu:2580-2583): the MUL node on the device, whatever dst->op says
+    ensure_init();
+    tensor node = *(const tensor *)dst;
+    node.op = gabi::OP_MUL;
+    node.src0 = (tensor *)src0;
+    node.src1 = (tensor *)src1;
+    run_device_op(&node);
+}
+
 void *ggml_hip_host_malloc(size_t size) {
     // ggml-cuda.cu:1884-1899
     ensure_init();

@@ -114,3 +114,18 @@ def test_cuda_abi_shim_exports_reference_names():
     assert not [s for s in declared if s not in exported]
     deps = subprocess.check_output(["readelf", "-d", shim], text=True)
     assert "libggml_hip.so" in deps and "oracle" not in deps
+
+
+def test_op_enum_mirror_matches_reference_header():
+    """csrc/ggml_abi.h's GGML_OP_* / GGML_TYPE_* values equal the reference ggml.h's (the fork shifts
+    MUL_MAT and later ops by four EXT ops); the fixture was generated from the reference header by
+    tests/golden/gen_ggml_enum.c."""
+    import json
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ref = json.load(open(os.path.join(root, "tests", "golden", "ggml_op_enum.json")))
+    src = open(os.path.join(root, "llama.cpp-q_4_0_amd", "csrc", "ggml_abi.h")).read()
+    mine = {m.group(1): int(m.group(2)) for m in re.finditer(r"\b(OP_\w+|TYPE_\w+) = (\d+)", src)}
+    for name, v in ref.items():
+        key = name.replace("GGML_", "")
+        assert mine[key] == v, (name, mine.get(key), v)

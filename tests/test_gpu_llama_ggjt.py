@@ -103,15 +103,20 @@ def test_reference_llama_on_backend_fast_kernels(tmp_path, ngl):
 CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "libllama_ref_cpu.so")
 
 
+HP128 = dict(n_vocab=1000, n_embd=512, n_mult=256, n_head=4, n_layer=2, n_rot=128, ftype=2)   # head_dim 128
+
+
 @pytest.mark.skipif(not os.path.exists(CPU_LIB), reason="oracle/_ref/libllama_ref_cpu.so not built")
-def test_long_decode_full_offload_exact_bitwise(tmp_path):
-    """600 single-token steps at full offload (KV cache, rope positions and soft_max rows up to 608,
-    the rope table regrown past its first 512 positions): the last logits equal the reference's
-    CPU-only build bit for bit (both run live on this host through refllama_bench)."""
+@pytest.mark.parametrize("hp,n_prompt,n_decode", [(G.HP, 8, 600), (HP128, 40, 300)], ids=["head64", "head128"])
+def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode):
+    """Hundreds of single-token steps at full offload (KV cache, rope positions and soft_max rows up
+    to 608, the rope table regrown past its first 512 positions; LLaMA's head_dim 128 and a
+    40-token batched prompt in the second case): the last logits equal the reference's CPU-only
+    build bit for bit (both run live on this host through refllama_bench)."""
     L = ggml_hip.load()
     mp = str(tmp_path / "m.ggjt")
-    G.write(mp)
-    nv = G.HP["n_vocab"]
+    G.write(mp, hp=hp)
+    nv = hp["n_vocab"]
 
     def run(lib_path, ngl):
         lib = ctypes.CDLL(lib_path)
@@ -119,7 +124,8 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path):
         lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
         out = np.zeros(3, np.float64)
         lg = np.zeros(nv, np.float32)
-        assert lib.refllama_bench(mp.encode(), 8, 600, 1, ngl, 1024, 1, out.ctypes.data, lg.ctypes.data) == nv
+        assert lib.refllama_bench(mp.encode(), n_prompt, n_decode, 1, ngl, 1024, 1, out.ctypes.data,
+                                  lg.ctypes.data) == nv
         return lg
 
     prev = L.ggml_hip_get_exact()
@@ -133,4 +139,4 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path):
     ref = run(CPU_LIB, 0)
     assert np.isfinite(ref).all()
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    assert ran[OPS["GGML_OP_SOFT_MAX"]] >= 600 * G.HP["n_layer"]
+    assert ran[OPS["GGML_OP_SOFT_MAX"]] >= n_decode * hp["n_layer"]

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -586,6 +587,7 @@ bool same_shape(const tensor *a, const tensor *b) {
 }
 
 std::atomic<int64_t> g_op_count[gabi::OP_COUNT];      // device nodes run, per ggml op (debug stats)
+std::atomic<int64_t> g_host_ns{0};                     // host time inside the taken nodes (debug stats)
 
 void run_device_op(tensor *t) {
     const int op = t->op;
@@ -790,7 +792,19 @@ void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor 
     }
     const int64_t K = src0->ne[0], M = src0->ne[1], N = src1->ne[1];
     const int64_t nbatch = src0->ne[2] * src0->ne[3];
-    const bool split = src0->backend == gabi::BACKEND_GPU_SPLIT;
+    // a row split that puts every row on the main device (one device, or a tensor_split that gives
+    // the others nothing) is an ordinary device matrix: direct output, no gather, no synchronize
+    // (llama.cpp marks every layer matrix GPU_SPLIT, llama.cpp:1059-1076)
+    bool split = src0->backend == gabi::BACKEND_GPU_SPLIT;
+    if (split) {
+        int active = 0, only = -1;
+        for (int id = 0; id < g_device_count; id++) {
+            int64_t lo, hi;
+            split_range(M, id, &lo, &hi);
+            if (lo < hi) active++, only = id;
+        }
+        if (active == 1 && only == g_main_device) split = false;
+    }
     const bool src0_dev = on_device(src0);
     const bool src1_dev = src1->backend == gabi::BACKEND_GPU;
     const bool dst_dev = dst->backend == gabi::BACKEND_GPU;
@@ -1080,12 +1094,15 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
     if (params->ith != 0) return true;
     if (params->type == gabi::TASK_INIT || params->type == gabi::TASK_FINALIZE) return true;
     ensure_init();
+    const auto t0 = std::chrono::steady_clock::now();
     if (t->op == gabi::OP_MUL_MAT && !f16_mul_mat) {
         g_op_count[gabi::OP_MUL_MAT].fetch_add(1, std::memory_order_relaxed);
         ggml_hip_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1, (ggml_tensor *)t);
-    }
-    else
+    } else {
         run_device_op(t);
+    }
+    g_host_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
+                        std::memory_order_relaxed);
     return true;
 }
 
@@ -1516,8 +1533,11 @@ int ggml_hip_debug_set_gemv_policy(int map, int depth, int rowitems, int wg_per_
 // reset when reset != 0 (tests check which ops of a full-offload graph ran on the device)
 int ggml_hip_debug_op_stats(int64_t *counts, int n, int reset) {
     for (int i = 0; i < n && i < gabi::OP_COUNT; i++) counts[i] = g_op_count[i].load();
-    if (reset)
+    if (n > gabi::OP_COUNT) counts[gabi::OP_COUNT] = g_host_ns.load();   // one slot past the ops: host ns
+    if (reset) {
         for (auto &c : g_op_count) c.store(0);
+        g_host_ns.store(0);
+    }
     return GGML_HIP_OK;
 }
 

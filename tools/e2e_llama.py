@@ -119,7 +119,14 @@ def main():
             print("cpu", res["cpu"], file=sys.stderr, flush=True)
         for mode in ("fast", "exact"):
             gh.check(L.ggml_hip_set_exact(1 if mode == "exact" else 0))
+            L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+            st = np.zeros(69, np.int64)
+            L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
             r, lg = bench(HIP_LIB, model, args.prompt, args.decode, args.threads_gpu, 99, 3, nv)
+            L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
+            ntok = 3 * args.prompt + args.decode      # evals: 3 prompt reps + decode steps
+            r["backend_nodes_per_eval"] = round(float(st[:68].sum()) / (3 + args.decode), 1)
+            r["backend_host_ms_per_eval"] = round(float(st[68]) / 1e6 / (3 + args.decode), 3)
             r["finite"] = bool(np.isfinite(lg).all())
             if not args.no_cpu:       # same token sequence as the CPU run: compare the last logits
                 _, lg8 = bench(HIP_LIB, model, args.prompt, args.decode_cpu, args.threads_gpu, 99, 1, nv)

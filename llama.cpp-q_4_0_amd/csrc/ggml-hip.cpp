@@ -1094,6 +1094,10 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
     if (params->ith != 0) return true;
     if (params->type == gabi::TASK_INIT || params->type == gabi::TASK_FINALIZE) return true;
     ensure_init();
+    static const bool trace = getenv("GGML_HIP_TRACE_NODES") != nullptr;
+    if (trace)
+        fprintf(stderr, "node op=%d %-24s src0=%-24s src1=%s\n", t->op, t->name, t->src0 ? t->src0->name : "-",
+                t->src1 ? t->src1->name : "-");
     const auto t0 = std::chrono::steady_clock::now();
     if (t->op == gabi::OP_MUL_MAT && !f16_mul_mat) {
         g_op_count[gabi::OP_MUL_MAT].fetch_add(1, std::memory_order_relaxed);

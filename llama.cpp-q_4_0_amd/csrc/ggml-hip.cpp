@@ -741,7 +741,164 @@ void run_device_op(tensor *t) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Launch fusion of back-to-back full-offload nodes.  A decode token is ~830 dependent launches of
+// ~2.6 us host cost each (tools/host_costs.hip), so chains that ggml emits one after the other are
+// run as one kernel: add -> rms_norm -> mul(norm weight), rms_norm -> mul, scale -> diag_mask_inf
+// -> soft_max, and silu ... mul (across the one q4_0 mul_mat between them).  The producer node is
+// deferred until its consumer arrives; anything else flushes it first, and so does every other
+// backend entry point (its output is device memory, observable only through the backend).  The
+// fused kernels store every intermediate tensor as its own node would, bit for bit.
+// GGML_HIP_FUSE=0 runs every node as its own launch.
+
+bool fuse_enabled() {
+    static const bool on = !getenv("GGML_HIP_FUSE") || atoi(getenv("GGML_HIP_FUSE")) != 0;
+    return on;
+}
+
+struct Pending {
+    int n = 0;
+    tensor *node[2] = {nullptr, nullptr};
+};
+Pending g_pend;
+
+char *dptr(const tensor *t) { return (char *)((ggml_tensor_extra_gpu *)t->extra)->data_device[g_main_device]; }
+bool dev_f32(const tensor *t) {
+    return t && t->backend == gabi::BACKEND_GPU && t->type == gabi::TYPE_F32 && t->extra && is_contiguous(t);
+}
+bool host_scalar_param(const tensor *t) { return t && t->backend == gabi::BACKEND_CPU && t->data; }
+bool overlaps(const tensor *a, const tensor *b) {   // device byte ranges of two device tensors
+    if (!a || !b || a->backend != gabi::BACKEND_GPU || b->backend != gabi::BACKEND_GPU || !a->extra || !b->extra) return false;
+    const char *pa = dptr(a), *pb = dptr(b);
+    return pa < pb + gabi::nbytes(b) && pb < pa + gabi::nbytes(a);
+}
+
+bool deferrable(const tensor *t) {
+    if (!fuse_enabled() || !dev_f32(t)) return false;
+    switch (t->op) {
+        case gabi::OP_ADD:
+            return dev_f32(t->src0) && dev_f32(t->src1) && same_shape(t, t->src0) && same_shape(t, t->src1);
+        case gabi::OP_RMS_NORM:
+        case gabi::OP_SILU:
+            return dev_f32(t->src0) && same_shape(t, t->src0);
+        case gabi::OP_SCALE:
+            return dev_f32(t->src0) && same_shape(t, t->src0) && host_scalar_param(t->src1);
+        default:
+            return false;
+    }
+}
+
+void count_node(const tensor *t) { g_op_count[t->op].fetch_add(1, std::memory_order_relaxed); }
+
+void flush_pending() {
+    const Pending p = g_pend;
+    g_pend = Pending{};
+    for (int i = 0; i < p.n; i++) run_device_op(p.node[i]);
+}
+
+// t arrives while a chain is pending: extend the chain, complete it in one launch, or let a q4_0
+// mul_mat that touches none of its buffers run first.  false: t does not fit (caller flushes).
+bool try_fuse(tensor *t) {
+    Pending &p = g_pend;
+    tensor *last = p.node[p.n - 1];
+    const int id = g_main_device;
+    hipStream_t s = g_dev[id].stream;
+    // add -> rms_norm(sum): extend
+    if (p.n == 1 && last->op == gabi::OP_ADD && t->op == gabi::OP_RMS_NORM && t->src0 == last && deferrable(t)) {
+        p.node[p.n++] = t;
+        return true;
+    }
+    // scale -> diag_mask_inf(scaled): extend
+    if (p.n == 1 && last->op == gabi::OP_SCALE && t->op == gabi::OP_DIAG_MASK_INF && t->src0 == last && dev_f32(t) &&
+        same_shape(t, last) && host_scalar_param(t->src1)) {
+        p.node[p.n++] = t;
+        return true;
+    }
+    // [add ->] rms_norm -> mul(norm weight row): complete
+    if (last->op == gabi::OP_RMS_NORM && t->op == gabi::OP_MUL && t->src0 == last && dev_f32(t) && same_shape(t, last) &&
+        dev_f32(t->src1) && t->src1->ne[0] == t->ne[0] && t->src1->ne[1] == 1 && t->src1->ne[2] == 1 && t->src1->ne[3] == 1) {
+        const tensor *add = p.n == 2 ? p.node[0] : nullptr;
+        const tensor *x = add ? add : last->src0;     // the rms_norm input
+        HIP_FATAL(hipSetDevice(id));
+        HIP_FATAL(ghip::op_add_rms_norm_mul_f32(add ? (const float *)dptr(add->src0) : nullptr,
+                                                add ? (const float *)dptr(add->src1) : (const float *)dptr(x),
+                                                add ? (float *)dptr(add) : nullptr, (float *)dptr(last),
+                                                (const float *)dptr(t->src1), (float *)dptr(t), t->ne[0], gabi::nrows(t), s));
+        for (int i = 0; i < p.n; i++) count_node(p.node[i]);
+        count_node(t);
+        p = Pending{};
+        return true;
+    }
+    // scale -> diag_mask_inf -> soft_max: complete
+    if (p.n == 2 && p.node[0]->op == gabi::OP_SCALE && last->op == gabi::OP_DIAG_MASK_INF && t->op == gabi::OP_SOFT_MAX &&
+        t->src0 == last && dev_f32(t) && same_shape(t, last)) {
+        const tensor *sc = p.node[0];
+        const OpTables &tb = op_tables(id, s);
+        float *d = (float *)dptr(t);
+        HIP_FATAL(hipSetDevice(id));
+        HIP_FATAL(ghip::op_scale_mask_soft_max_f32((const float *)dptr(sc->src0),
+                                                   dptr(sc) == (char *)d ? nullptr : (float *)dptr(sc),
+                                                   dptr(last) == (char *)d ? nullptr : (float *)dptr(last), d,
+                                                   *(const float *)sc->src1->data, t->ne[0], gabi::nrows(t), t->ne[1],
+                                                   ((const int32_t *)last->src1->data)[0], tb.exp, s));
+        for (int i = 0; i < p.n; i++) count_node(p.node[i]);
+        count_node(t);
+        p = Pending{};
+        return true;
+    }
+    // silu -> mul(silu, b): complete
+    if (p.n == 1 && last->op == gabi::OP_SILU && t->op == gabi::OP_MUL && t->src0 == last && dev_f32(t) &&
+        same_shape(t, last) && dev_f32(t->src1) && same_shape(t, t->src1)) {
+        const OpTables &tb = op_tables(id, s);
+        HIP_FATAL(hipSetDevice(id));
+        HIP_FATAL(ghip::op_silu_mul_f32((const float *)dptr(last->src0), (const float *)dptr(t->src1), (float *)dptr(last),
+                                        (float *)dptr(t), t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3], tb.silu, s));
+        count_node(last);
+        count_node(t);
+        p = Pending{};
+        return true;
+    }
+    // pending silu, then a q4_0 mul_mat that neither reads nor overwrites its buffers: run it now
+    if (p.n == 1 && last->op == gabi::OP_SILU && t->op == gabi::OP_MUL_MAT && t->src0 &&
+        t->src0->type == gabi::TYPE_Q4_0 && t->backend == gabi::BACKEND_GPU && t->src1 &&
+        t->src1->backend == gabi::BACKEND_GPU && !overlaps(t->src1, last) && !overlaps(t, last) &&
+        !overlaps(t, last->src0)) {
+        count_node(t);
+        ggml_hip_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1, (ggml_tensor *)t);
+        return true;
+    }
+    return false;
+}
+
+// runs (or defers) one taken node; the ith == 0 COMPUTE phase of ggml_hip_compute_forward
+void execute_node(tensor *t) {
+    const int op = t->op;
+    if (op == gabi::OP_RESHAPE || op == gabi::OP_VIEW || op == gabi::OP_PERMUTE || op == gabi::OP_TRANSPOSE) {
+        count_node(t);                      // no data touched: a pending chain stays pending
+        return;
+    }
+    if (g_pend.n > 0) {
+        if (try_fuse(t)) return;
+        flush_pending();
+    }
+    if (deferrable(t)) {
+        g_pend.node[g_pend.n++] = t;
+        return;
+    }
+    if (t->op == gabi::OP_MUL_MAT && t->src0 && t->src0->type != gabi::TYPE_F16) {
+        count_node(t);
+        ggml_hip_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1, (ggml_tensor *)t);
+    } else {
+        run_device_op(t);
+    }
+}
+
 }  // namespace
+
+// every backend entry point that can touch device memory outside the node sequence
+static inline void flush_deferred() {
+    if (g_pend.n > 0) flush_pending();
+}
 
 // ==========================================================================================
 // C ABI
@@ -784,6 +941,7 @@ size_t ggml_hip_mul_mat_get_wsize(const struct ggml_tensor *, const struct ggml_
 void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor *src1_, struct ggml_tensor *dst_) {
     // ggml_cuda_mul_mat -> ggml_cuda_op (ggml-cuda.cu:2671-2690, 2286-2567)
     ensure_init();
+    flush_deferred();
     const tensor *src0 = (const tensor *)src0_, *src1 = (const tensor *)src1_;
     tensor *dst = (tensor *)dst_;
     if (!supported_mul_mat(src0, src1, dst)) {
@@ -909,6 +1067,7 @@ void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor 
 void ggml_hip_mul(const struct ggml_tensor *src0, const struct ggml_tensor *src1, struct ggml_tensor *dst) {
     // ggml_cuda_mul (ggml-cuda.cu:2580-2583): the MUL node on the device, whatever dst->op says
     ensure_init();
+    flush_deferred();
     tensor node = *(const tensor *)dst;
     node.op = gabi::OP_MUL;
     node.src0 = (tensor *)src0;
@@ -938,6 +1097,7 @@ void ggml_hip_host_free(void *ptr) {
 void ggml_hip_transform_tensor(void *data, struct ggml_tensor *tensor_) {
     // ggml-cuda.cu:2766-2809
     ensure_init();
+    flush_deferred();
     tensor *t = (tensor *)tensor_;
     if ((t->type != gabi::TYPE_Q4_0 && t->type != gabi::TYPE_F32 && t->type != gabi::TYPE_F16) || g_device_count == 0) {
         // A type no device op reads: ggml.c computes the ops that read it on the CPU and asserts
@@ -993,6 +1153,7 @@ void ggml_hip_transform_tensor(void *data, struct ggml_tensor *tensor_) {
 
 void ggml_hip_free_data(struct ggml_tensor *tensor_) {
     // ggml-cuda.cu:2811-2828
+    flush_deferred();
     tensor *t = (tensor *)tensor_;
     {
         std::lock_guard<std::mutex> lk(g_host_copy_mu);
@@ -1023,9 +1184,19 @@ void ggml_hip_free_data(struct ggml_tensor *tensor_) {
 // slot of the VRAM scratch ring (scratch: wraps to the start when full, as the reference does),
 // or its own zeroed buffer (no_scratch: the KV cache).  Every op of such a graph runs on the
 // device (ggml_hip_compute_forward), so activations stay resident across the layer.
-void ggml_hip_assign_buffers(struct ggml_tensor *t) { assign_buffers_impl((tensor *)t, true, false); }
-void ggml_hip_assign_buffers_no_scratch(struct ggml_tensor *t) { assign_buffers_impl((tensor *)t, false, false); }
-void ggml_hip_assign_buffers_force_inplace(struct ggml_tensor *t) { assign_buffers_impl((tensor *)t, false, true); }
+// (a pending fused chain reads its tensors' extras when it runs: flush before they are reassigned)
+void ggml_hip_assign_buffers(struct ggml_tensor *t) {
+    flush_deferred();
+    assign_buffers_impl((tensor *)t, true, false);
+}
+void ggml_hip_assign_buffers_no_scratch(struct ggml_tensor *t) {
+    flush_deferred();
+    assign_buffers_impl((tensor *)t, false, false);
+}
+void ggml_hip_assign_buffers_force_inplace(struct ggml_tensor *t) {
+    flush_deferred();
+    assign_buffers_impl((tensor *)t, false, true);
+}
 
 void ggml_hip_set_main_device(int main_device) {
     // ggml-cuda.cu:2906-2918
@@ -1042,6 +1213,7 @@ void ggml_hip_set_main_device(int main_device) {
 void ggml_hip_set_scratch_size(size_t scratch_size) { g_scratch_size = scratch_size; }
 
 void ggml_hip_free_scratch(void) {
+    flush_deferred();
     if (g_scratch) {
         HIP_FATAL(hipFree(g_scratch));
         g_scratch = nullptr;
@@ -1099,12 +1271,8 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
         fprintf(stderr, "node op=%d %-24s src0=%-24s src1=%s\n", t->op, t->name, t->src0 ? t->src0->name : "-",
                 t->src1 ? t->src1->name : "-");
     const auto t0 = std::chrono::steady_clock::now();
-    if (t->op == gabi::OP_MUL_MAT && !f16_mul_mat) {
-        g_op_count[gabi::OP_MUL_MAT].fetch_add(1, std::memory_order_relaxed);
-        ggml_hip_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1, (ggml_tensor *)t);
-    } else {
-        run_device_op(t);
-    }
+    (void)f16_mul_mat;
+    execute_node(t);
     g_host_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
                         std::memory_order_relaxed);
     return true;
@@ -1416,6 +1584,7 @@ void ggml_hip_dev_free(void *ptr) {
 }
 
 int ggml_hip_memcpy_h2d(void *dst, const void *src, size_t size, void *stream) {
+    flush_deferred();
     hipStream_t s = resolve_stream(stream);
     HIP_RET(hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, s));
     HIP_RET(hipStreamSynchronize(s));
@@ -1423,6 +1592,7 @@ int ggml_hip_memcpy_h2d(void *dst, const void *src, size_t size, void *stream) {
 }
 
 int ggml_hip_memcpy_d2h(void *dst, const void *src, size_t size, void *stream) {
+    flush_deferred();
     hipStream_t s = resolve_stream(stream);
     HIP_RET(hipMemcpyAsync(dst, src, size, hipMemcpyDeviceToHost, s));
     HIP_RET(hipStreamSynchronize(s));
@@ -1430,6 +1600,7 @@ int ggml_hip_memcpy_d2h(void *dst, const void *src, size_t size, void *stream) {
 }
 
 int ggml_hip_memcpy_d2d(void *dst, const void *src, size_t size, void *stream) {
+    flush_deferred();
     HIP_RET(hipMemcpyAsync(dst, src, size, hipMemcpyDeviceToDevice, resolve_stream(stream)));
     return GGML_HIP_OK;
 }
@@ -1440,11 +1611,13 @@ int ggml_hip_memset(void *dst, int value, size_t size, void *stream) {
 }
 
 int ggml_hip_stream_synchronize(void *stream) {
+    flush_deferred();
     HIP_RET(hipStreamSynchronize(resolve_stream(stream)));
     return GGML_HIP_OK;
 }
 
 int ggml_hip_device_synchronize(void) {
+    flush_deferred();
     HIP_RET(hipDeviceSynchronize());
     return GGML_HIP_OK;
 }

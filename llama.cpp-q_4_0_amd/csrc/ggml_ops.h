@@ -29,4 +29,16 @@ hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne
 hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11, int64_t ne02,
                               int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s);
 
+// fused chains (each stage bit-identical to its own op above; intermediates stored unless nullptr)
+// [sum = a + b] -> norm = rms_norm(sum) -> out = norm * w (w: one row); a == nullptr: rms_norm(b)
+hipError_t op_add_rms_norm_mul_f32(const float *a, const float *b, float *sum, float *norm, const float *w, float *out,
+                                   int64_t ncols, int64_t nrows, hipStream_t s);
+// scaled = x * v -> masked = diag_mask_inf(scaled, n_past) -> d = soft_max(masked)
+hipError_t op_scale_mask_soft_max_f32(const float *x, float *scaled, float *masked, float *d, float v, int64_t ncols,
+                                      int64_t nrows, int64_t rows_per_channel, int n_past, const uint16_t *table,
+                                      hipStream_t s);
+// u = silu(a) -> out = u * b (same shape)
+hipError_t op_silu_mul_f32(const float *a, const float *b, float *u, float *out, int64_t n, const uint16_t *table,
+                           hipStream_t s);
+
 }  // namespace ghip

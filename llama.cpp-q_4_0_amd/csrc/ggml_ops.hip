@@ -216,7 +216,171 @@ __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32(const char *s0, const c
     }
 }
 
+// ----------------------------------------------------------------------------------- fused chains
+// Back-to-back nodes of a LLaMA graph in one launch (ggml-hip.cpp defers the producer until its
+// consumer arrives).  Each stage computes exactly what its own node's kernel above computes, in
+// the same order, and writes that node's output too unless it shares the final output's buffer
+// (in-place nodes), so every intermediate tensor holds the value ggml.c would give it.
+
+// [sum = a + b] -> norm = sum * (1/sqrt(mean(sum^2) + eps)) -> out = norm * w  (w one row); one wave
+// per row.  a == nullptr: no add (norm of x = b).  sum / norm == nullptr: not stored.
+__global__ __launch_bounds__(TPB) void k_add_rms_norm_mul(const float *a, const float *b, float *sum, float *norm,
+                                                          const float *w, float *out, int64_t ncols, int64_t nrows) {
+    const int64_t r = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nrows) return;
+    const int64_t o = r * ncols;
+    double s = 0.0;
+    for (int64_t i = lane; i < ncols; i += 64) {
+        const float v = a ? a[o + i] + b[o + i] : b[o + i];
+        if (sum) sum[o + i] = v;
+        s += (double)(v * v);
+    }
+    s = wave_sum_d(s);
+    const float mean = (float)(s / (double)ncols);
+    const float scale = 1.0f / (float)__builtin_sqrt((double)(mean + 1e-6f));
+    for (int64_t i = lane; i < ncols; i += 64) {
+        // the same float as above (re-read from sum, which may alias a or b, written by this lane)
+        const float v = sum ? sum[o + i] : (a ? a[o + i] + b[o + i] : b[o + i]);
+        const float y = v * scale;
+        if (norm) norm[o + i] = y;
+        out[o + i] = y * w[i];
+    }
+}
+
+// scaled = x * v -> masked (i > n_past + j: -inf) -> soft_max; one wave per row
+__global__ __launch_bounds__(TPB) void k_scale_mask_soft_max(const float *x, float *scaled, float *masked, float *d,
+                                                             float v, int64_t ncols, int64_t nrows,
+                                                             int64_t rows_per_channel, int n_past, const uint16_t *table) {
+    const int64_t r = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nrows) return;
+    const int64_t o = r * ncols, j = r % rows_per_channel;
+    auto val = [&](int64_t i) __attribute__((always_inline)) {
+        const float sv = x[o + i] * v;
+        return i > n_past + j ? -INFINITY : sv;
+    };
+    float mx = -INFINITY;
+    for (int64_t i = lane; i < ncols; i += 64) mx = fmaxf(mx, val(i));
+    mx = wave_max_f(mx);
+    double s = 0.0;
+    for (int64_t i = lane; i < ncols; i += 64) {
+        const float sv = x[o + i] * v;
+        const float m = i > n_past + j ? -INFINITY : sv;
+        if (scaled) scaled[o + i] = sv;
+        if (masked) masked[o + i] = m;
+        float e = 0.0f;
+        if (m != -INFINITY) {
+            e = h2f_bits(table[f2h_bits(m - mx)]);
+            s += (double)e;
+        }
+        d[o + i] = e;
+    }
+    s = wave_sum_d(s);
+    const float inv = (float)(1.0 / s);
+    for (int64_t i = lane; i < ncols; i += 64) d[o + i] = d[o + i] * inv;
+}
+
+// The same [add ->] rms_norm [-> mul] with one 1024-thread workgroup per row: every thread loads
+// its float4 pieces of the row at once (up to NV per thread, held in registers), the double sum is
+// reduced by shuffles and LDS, and the row is written from the registers.  One wave per row walks
+// a 4096-wide row with 64 dependent load round trips (24 us per launch, measured); this form takes
+// one.  Rows with ncols % 4 != 0, more than 4096*NV values or unaligned pointers use the kernels above.
+constexpr int RN_THREADS = 1024, RN_NV = 4;
+__global__ __launch_bounds__(RN_THREADS) void k_row_norm4(const float *a, const float *b, float *sum, float *norm,
+                                                          const float *w, float *out, int64_t ncols) {
+    __shared__ double part[RN_THREADS / 64];
+    const int tid = threadIdx.x;
+    const int64_t o = (int64_t)blockIdx.x * ncols;
+    const int64_t n4 = ncols / 4;
+    float4 v[RN_NV];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < RN_NV; k++) {
+        const int64_t i4 = tid + (int64_t)k * RN_THREADS;
+        if (i4 < n4) {
+            float4 x = reinterpret_cast<const float4 *>(b + o)[i4];
+            if (a) {
+                const float4 y = reinterpret_cast<const float4 *>(a + o)[i4];
+                x = make_float4(y.x + x.x, y.y + x.y, y.z + x.z, y.w + x.w);   // a + b, as k_add_f32
+                if (sum) reinterpret_cast<float4 *>(sum + o)[i4] = x;
+            }
+            v[k] = x;
+            s += (double)(x.x * x.x);
+            s += (double)(x.y * x.y);
+            s += (double)(x.z * x.z);
+            s += (double)(x.w * x.w);
+        }
+    }
+    s = wave_sum_d(s);
+    if ((tid & 63) == 0) part[tid >> 6] = s;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < RN_THREADS / 64; i++) t += part[i];
+    const float mean = (float)(t / (double)ncols);
+    const float scale = 1.0f / (float)__builtin_sqrt((double)(mean + 1e-6f));
+#pragma unroll
+    for (int k = 0; k < RN_NV; k++) {
+        const int64_t i4 = tid + (int64_t)k * RN_THREADS;
+        if (i4 < n4) {
+            const float4 x = v[k];
+            const float4 y = make_float4(x.x * scale, x.y * scale, x.z * scale, x.w * scale);
+            if (norm) reinterpret_cast<float4 *>(norm + o)[i4] = y;
+            if (out) {
+                const float4 g = reinterpret_cast<const float4 *>(w)[i4];
+                reinterpret_cast<float4 *>(out + o)[i4] = make_float4(y.x * g.x, y.y * g.y, y.z * g.z, y.w * g.w);
+            }
+        }
+    }
+}
+
+// u = silu(a) (fp16 table) -> out = u * b
+__global__ __launch_bounds__(TPB) void k_silu_mul(const float *a, const float *b, float *u, float *out, int64_t n,
+                                                  const uint16_t *table) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const float s = h2f_bits(table[f2h_bits(a[i])]);
+    if (u) u[i] = s;
+    out[i] = s * b[i];
+}
+
+bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }   // nullptr passes (not accessed)
+
+bool row_norm4_ok(int64_t ncols, const void *a, const void *b, const void *sum, const void *norm, const void *w,
+                  const void *out) {
+    return ncols % 4 == 0 && ncols <= 4 * RN_THREADS * RN_NV && al16(a) && al16(b) && al16(sum) && al16(norm) &&
+           al16(w) && al16(out);
+}
+
 }  // namespace
+
+hipError_t op_add_rms_norm_mul_f32(const float *a, const float *b, float *sum, float *norm, const float *w, float *out,
+                                   int64_t ncols, int64_t nrows, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    if (row_norm4_ok(ncols, a, b, sum, norm, w, out))
+        hipLaunchKernelGGL(k_row_norm4, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, a, b, sum, norm, w, out, ncols);
+    else
+        hipLaunchKernelGGL(k_add_rms_norm_mul, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, a, b, sum, norm, w, out,
+                           ncols, nrows);
+    return hipGetLastError();
+}
+
+hipError_t op_scale_mask_soft_max_f32(const float *x, float *scaled, float *masked, float *d, float v, int64_t ncols,
+                                      int64_t nrows, int64_t rows_per_channel, int n_past, const uint16_t *table,
+                                      hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scale_mask_soft_max, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, scaled, masked, d, v,
+                       ncols, nrows, rows_per_channel, n_past, table);
+    return hipGetLastError();
+}
+
+hipError_t op_silu_mul_f32(const float *a, const float *b, float *u, float *out, int64_t n, const uint16_t *table,
+                           hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_silu_mul, dim3(blocks(n)), dim3(TPB), 0, s, a, b, u, out, n, table);
+    return hipGetLastError();
+}
 
 hipError_t op_add_f32(const float *a, const float *b, float *d, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
@@ -256,7 +420,11 @@ hipError_t op_diag_mask_inf_f32(const float *x, float *d, int64_t ncols, int64_t
 hipError_t op_rms_norm_f32(const float *x, float *d, int64_t ncols, int64_t nrows, int64_t ldx, int64_t ldd,
                            hipStream_t s) {
     if (nrows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rms_norm_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, ldx, ldd);
+    if (ldx == ncols && ldd == ncols && row_norm4_ok(ncols, nullptr, x, nullptr, d, nullptr, nullptr))
+        hipLaunchKernelGGL(k_row_norm4, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, nullptr, x, nullptr, d, nullptr,
+                           nullptr, ncols);
+    else
+        hipLaunchKernelGGL(k_rms_norm_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, ldx, ldd);
     return hipGetLastError();
 }
 

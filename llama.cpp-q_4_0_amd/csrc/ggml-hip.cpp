@@ -751,9 +751,14 @@ void run_device_op(tensor *t) {
 // fused kernels store every intermediate tensor as its own node would, bit for bit.
 // GGML_HIP_FUSE=0 runs every node as its own launch.
 
+std::atomic<int> g_fuse{-1};
 bool fuse_enabled() {
-    static const bool on = !getenv("GGML_HIP_FUSE") || atoi(getenv("GGML_HIP_FUSE")) != 0;
-    return on;
+    int v = g_fuse.load(std::memory_order_relaxed);
+    if (v < 0) {
+        v = (!getenv("GGML_HIP_FUSE") || atoi(getenv("GGML_HIP_FUSE")) != 0) ? 1 : 0;
+        g_fuse.store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
 }
 
 struct Pending {
@@ -1715,6 +1720,13 @@ int ggml_hip_debug_op_stats(int64_t *counts, int n, int reset) {
         for (auto &c : g_op_count) c.store(0);
         g_host_ns.store(0);
     }
+    return GGML_HIP_OK;
+}
+
+// not in the public header: launch fusion of full-offload chains on (1) / off (0) (tests run both)
+int ggml_hip_debug_set_fuse(int on) {
+    flush_deferred();
+    g_fuse.store(on ? 1 : 0, std::memory_order_relaxed);
     return GGML_HIP_OK;
 }
 

@@ -107,8 +107,9 @@ HP128 = dict(n_vocab=1000, n_embd=512, n_mult=256, n_head=4, n_layer=2, n_rot=12
 
 
 @pytest.mark.skipif(not os.path.exists(CPU_LIB), reason="oracle/_ref/libllama_ref_cpu.so not built")
+@pytest.mark.parametrize("fuse", [1, 0], ids=["fused", "unfused"])
 @pytest.mark.parametrize("hp,n_prompt,n_decode", [(G.HP, 8, 600), (HP128, 40, 300)], ids=["head64", "head128"])
-def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode):
+def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode, fuse):
     """Hundreds of single-token steps at full offload (KV cache, rope positions and soft_max rows up
     to 608, the rope table regrown past its first 512 positions; LLaMA's head_dim 128 and a
     40-token batched prompt in the second case): the last logits equal the reference's CPU-only
@@ -130,12 +131,15 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode
 
     prev = L.ggml_hip_get_exact()
     ggml_hip.check(L.ggml_hip_set_exact(1), "set_exact")
+    L.ggml_hip_debug_set_fuse.argtypes = [ctypes.c_int]
+    ggml_hip.check(L.ggml_hip_debug_set_fuse(fuse), "set_fuse")
     op_stats(L)
     try:
         got = run(HIP_LIB, 99)
         ran = op_stats(L)
     finally:
         L.ggml_hip_set_exact(prev)
+        L.ggml_hip_debug_set_fuse(1)
     ref = run(CPU_LIB, 0)
     assert np.isfinite(ref).all()
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

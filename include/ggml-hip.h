@@ -212,6 +212,13 @@ int    ggml_hip_graph_launch(ggml_hip_graph *graph, void *stream);
 int    ggml_hip_graph_destroy(ggml_hip_graph *graph);
 const char *ggml_hip_last_error(void);
 const char *ggml_hip_version(void);
+/* debug: counts[op] = device nodes run per ggml op (GGML_OP_COUNT = 68 slots), counts[68] = host ns
+   inside ggml_hip_compute_forward, counts[69 + op] = that host time per op of the arriving node,
+   counts[137 + k] = fused launches of chain k (0 add/rms_norm/mul, 1 scale/diag_mask_inf/soft_max,
+   2 silu/mul, 3 rope/cpy, 4 f16 mul_mat/permute/cpy, 5 q4_0 mul_mat run while a silu is pending) */
+int    ggml_hip_debug_op_stats(int64_t *counts, int n, int reset);
+/* debug: 1/0 = launch fusion of adjacent full-offload nodes on/off (default: env GGML_HIP_FUSE, on) */
+int    ggml_hip_debug_set_fuse(int on);
 
 #ifdef __cplusplus
 }

@@ -588,8 +588,15 @@ bool same_shape(const tensor *a, const tensor *b) {
 
 std::atomic<int64_t> g_op_count[gabi::OP_COUNT];      // device nodes run, per ggml op (debug stats)
 std::atomic<int64_t> g_host_ns{0};                     // host time inside the taken nodes (debug stats)
+std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of the node that arrived
+// fused launches by chain: add/rms_norm/mul, scale/mask/soft_max, silu/mul, rope/cpy, KQV/merge cpy,
+// q4_0 mul_mat run under a pending silu
+constexpr int N_FUSED = 6;
+std::atomic<int64_t> g_fused[N_FUSED];
 
-void run_device_op(tensor *t) {
+// fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)
+// -> contiguous cpy), checked by try_fuse; its destination is written by t's own kernel
+void run_device_op(tensor *t, const tensor *fused_cpy = nullptr) {
     const int op = t->op;
     if (op >= 0 && op < gabi::OP_COUNT) g_op_count[op].fetch_add(1, std::memory_order_relaxed);
     if (op == gabi::OP_RESHAPE || op == gabi::OP_VIEW || op == gabi::OP_PERMUTE || op == gabi::OP_TRANSPOSE) return;
@@ -699,7 +706,15 @@ void run_device_op(tensor *t) {
             }
             if (a->backend != gabi::BACKEND_GPU) nbx[1] = a->ne[0] * 4, nbx[2] = nbx[1] * a->ne[1], nbx[3] = nbx[2] * a->ne[2];
             if (t->backend != gabi::BACKEND_GPU) nbd[1] = t->ne[0] * 4, nbd[2] = nbd[1] * t->ne[1], nbd[3] = nbd[2] * t->ne[2];
-            HIP_FATAL(ghip::op_rope_f32(pa, d, a->ne, nbx, nbd, cs + (size_t)n_past * np * 2, (int)np, c.s));
+            if (fused_cpy) {
+                const tensor *cb = fused_cpy->src1;
+                HIP_FATAL(ghip::op_rope_cpy_f32(pa, d, a->ne, nbx, nbd, cs + (size_t)n_past * np * 2, (int)np,
+                                                (char *)((ggml_tensor_extra_gpu *)cb->extra)->data_device[c.id],
+                                                cb->type == gabi::TYPE_F16, cb->ne[0], cb->ne[1], cb->nb[0], cb->nb[1],
+                                                cb->nb[2], c.s));
+            } else {
+                HIP_FATAL(ghip::op_rope_f32(pa, d, a->ne, nbx, nbd, cs + (size_t)n_past * np * 2, (int)np, c.s));
+            }
             c.finish(t, d);
             return;
         }
@@ -731,8 +746,10 @@ void run_device_op(tensor *t) {
             int64_t nb11 = b->nb[1], nb12 = b->nb[2];
             if (b->backend != gabi::BACKEND_GPU) nb11 = b->ne[0] * 4, nb12 = nb11 * b->ne[1];
             char *d = c.out(t);
+            float *merged =
+                fused_cpy ? (float *)((ggml_tensor_extra_gpu *)fused_cpy->src1->extra)->data_device[c.id] : nullptr;
             HIP_FATAL(ghip::op_mul_mat_f16_f32(pa, pb, (float *)d, (int)a->ne[0], a->ne[1], b->ne[1], a->ne[2], a->nb[1],
-                                               a->nb[2], nb11, nb12, c.s));
+                                               a->nb[2], nb11, nb12, c.s, merged));
             c.finish(t, d);
             return;
         }
@@ -745,7 +762,8 @@ void run_device_op(tensor *t) {
 // Launch fusion of back-to-back full-offload nodes.  A decode token is ~830 dependent launches of
 // ~2.6 us host cost each (tools/host_costs.hip), so chains that ggml emits one after the other are
 // run as one kernel: add -> rms_norm -> mul(norm weight), rms_norm -> mul, scale -> diag_mask_inf
-// -> soft_max, and silu ... mul (across the one q4_0 mul_mat between them).  The producer node is
+// -> soft_max, silu ... mul (across the one q4_0 mul_mat between them), rope -> cpy (into the K
+// cache) and the f16 mul_mat KQV -> permute(0,2,1,3) -> contiguous cpy.  The producer node is
 // deferred until its consumer arrives; anything else flushes it first, and so does every other
 // backend entry point (its output is device memory, observable only through the backend).  The
 // fused kernels store every intermediate tensor as its own node would, bit for bit.
@@ -766,6 +784,7 @@ struct Pending {
     tensor *node[2] = {nullptr, nullptr};
 };
 Pending g_pend;
+void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst);
 
 char *dptr(const tensor *t) { return (char *)((ggml_tensor_extra_gpu *)t->extra)->data_device[g_main_device]; }
 bool dev_f32(const tensor *t) {
@@ -788,6 +807,12 @@ bool deferrable(const tensor *t) {
             return dev_f32(t->src0) && same_shape(t, t->src0);
         case gabi::OP_SCALE:
             return dev_f32(t->src0) && same_shape(t, t->src0) && host_scalar_param(t->src1);
+        case gabi::OP_ROPE:
+            return dev_f32(t->src0) && same_shape(t, t->src0) && t->ne[3] == 1 && host_scalar_param(t->src1) &&
+                   ((const int32_t *)t->src1->data)[2] == 0;
+        case gabi::OP_MUL_MAT:       // f16 x f32 (attention): the consumer may be the KQV merge copy
+            return t->src0 && t->src0->type == gabi::TYPE_F16 && t->src0->backend == gabi::BACKEND_GPU && t->src1 &&
+                   t->src1->type == gabi::TYPE_F32 && t->src1->backend == gabi::BACKEND_GPU && t->src1->extra;
         default:
             return false;
     }
@@ -831,6 +856,7 @@ bool try_fuse(tensor *t) {
                                                 (const float *)dptr(t->src1), (float *)dptr(t), t->ne[0], gabi::nrows(t), s));
         for (int i = 0; i < p.n; i++) count_node(p.node[i]);
         count_node(t);
+        g_fused[0].fetch_add(1, std::memory_order_relaxed);
         p = Pending{};
         return true;
     }
@@ -848,6 +874,7 @@ bool try_fuse(tensor *t) {
                                                    ((const int32_t *)last->src1->data)[0], tb.exp, s));
         for (int i = 0; i < p.n; i++) count_node(p.node[i]);
         count_node(t);
+        g_fused[1].fetch_add(1, std::memory_order_relaxed);
         p = Pending{};
         return true;
     }
@@ -860,8 +887,36 @@ bool try_fuse(tensor *t) {
                                         (float *)dptr(t), t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3], tb.silu, s));
         count_node(last);
         count_node(t);
+        g_fused[2].fetch_add(1, std::memory_order_relaxed);
         p = Pending{};
         return true;
+    }
+    // rope -> cpy(rope, strided device view): complete (the K cache store)
+    if (p.n == 1 && last->op == gabi::OP_ROPE && t->op == gabi::OP_CPY && t->src0 == last && t->src1 &&
+        t->src1->backend == gabi::BACKEND_GPU && t->src1->extra &&
+        (t->src1->type == gabi::TYPE_F16 || t->src1->type == gabi::TYPE_F32) && t->src1->ne[3] == 1 &&
+        t->src1->ne[0] * t->src1->ne[1] * t->src1->ne[2] == last->ne[0] * last->ne[1] * last->ne[2] &&
+        !overlaps(t->src1, last) && !overlaps(t->src1, last->src0)) {
+        p = Pending{};
+        run_device_op(last, t);
+        count_node(t);
+        g_fused[3].fetch_add(1, std::memory_order_relaxed);
+        return true;
+    }
+    // f16 mul_mat -> cpy(permute(mul_mat, 0, 2, 1, 3), contiguous f32): complete (KQV_merged_contiguous)
+    if (p.n == 1 && last->op == gabi::OP_MUL_MAT && t->op == gabi::OP_CPY && t->src0 && t->src0->op == gabi::OP_PERMUTE &&
+        t->src0->src0 == last) {
+        const tensor *m = t->src0, *cb = t->src1;
+        if (m->ne[0] == last->ne[0] && m->ne[1] == last->ne[2] && m->ne[2] == last->ne[1] && m->ne[3] == 1 &&
+            last->ne[3] == 1 && m->nb[0] == 4 && m->nb[1] == last->nb[2] && m->nb[2] == last->nb[1] && dev_f32(cb) &&
+            gabi::nbytes(cb) == gabi::nbytes(last) && !overlaps(cb, last) && !overlaps(cb, last->src0) &&
+            !overlaps(cb, last->src1)) {
+            p = Pending{};
+            run_device_op(last, t);
+            count_node(t);
+            g_fused[4].fetch_add(1, std::memory_order_relaxed);
+            return true;
+        }
     }
     // pending silu, then a q4_0 mul_mat that neither reads nor overwrites its buffers: run it now
     if (p.n == 1 && last->op == gabi::OP_SILU && t->op == gabi::OP_MUL_MAT && t->src0 &&
@@ -869,7 +924,8 @@ bool try_fuse(tensor *t) {
         t->src1->backend == gabi::BACKEND_GPU && !overlaps(t->src1, last) && !overlaps(t, last) &&
         !overlaps(t, last->src0)) {
         count_node(t);
-        ggml_hip_mul_mat((const ggml_tensor *)t->src0, (const ggml_tensor *)t->src1, (ggml_tensor *)t);
+        g_fused[5].fetch_add(1, std::memory_order_relaxed);
+        mul_mat_node(t->src0, t->src1, t);
         return true;
     }
     return false;
@@ -943,12 +999,19 @@ size_t ggml_hip_mul_mat_get_wsize(const struct ggml_tensor *, const struct ggml_
     return 0;
 }
 
-void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor *src1_, struct ggml_tensor *dst_) {
-    // ggml_cuda_mul_mat -> ggml_cuda_op (ggml-cuda.cu:2671-2690, 2286-2567)
+void ggml_hip_mul_mat(const struct ggml_tensor *src0, const struct ggml_tensor *src1, struct ggml_tensor *dst) {
     ensure_init();
     flush_deferred();
-    const tensor *src0 = (const tensor *)src0_, *src1 = (const tensor *)src1_;
-    tensor *dst = (tensor *)dst_;
+    mul_mat_node((const tensor *)src0, (const tensor *)src1, (tensor *)dst);
+}
+
+}  // extern "C"
+
+namespace {
+// the q4_0 mul_mat of one node; leaves a pending fusion chain alone (try_fuse checked that the two
+// touch disjoint buffers)
+void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
+    // ggml_cuda_mul_mat -> ggml_cuda_op (ggml-cuda.cu:2671-2690, 2286-2567)
     if (!supported_mul_mat(src0, src1, dst)) {
         fprintf(stderr, "ggml_hip_mul_mat: unsupported operands (need contiguous Q4_0 x F32 -> F32, K %% 64 == 0)\n");
         abort();
@@ -1068,6 +1131,9 @@ void ggml_hip_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor 
     }
     HIP_FATAL(hipSetDevice(saved));
 }
+}  // namespace
+
+extern "C" {
 
 void ggml_hip_mul(const struct ggml_tensor *src0, const struct ggml_tensor *src1, struct ggml_tensor *dst) {
     // ggml_cuda_mul (ggml-cuda.cu:2580-2583): the MUL node on the device, whatever dst->op says
@@ -1278,8 +1344,12 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
     const auto t0 = std::chrono::steady_clock::now();
     (void)f16_mul_mat;
     execute_node(t);
-    g_host_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
-                        std::memory_order_relaxed);
+    const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    g_host_ns.fetch_add(ns, std::memory_order_relaxed);
+    g_op_ns[t->op].fetch_add(ns, std::memory_order_relaxed);
+    if (trace)
+        fprintf(stderr, "node_ns %lld %lld\n", (long long)ns,
+                (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count());
     return true;
 }
 
@@ -1716,8 +1786,12 @@ int ggml_hip_debug_set_gemv_policy(int map, int depth, int rowitems, int wg_per_
 int ggml_hip_debug_op_stats(int64_t *counts, int n, int reset) {
     for (int i = 0; i < n && i < gabi::OP_COUNT; i++) counts[i] = g_op_count[i].load();
     if (n > gabi::OP_COUNT) counts[gabi::OP_COUNT] = g_host_ns.load();   // one slot past the ops: host ns
+    for (int i = 0; i < gabi::OP_COUNT && gabi::OP_COUNT + 1 + i < n; i++) counts[gabi::OP_COUNT + 1 + i] = g_op_ns[i].load();
+    for (int i = 0; i < N_FUSED && 2 * gabi::OP_COUNT + 1 + i < n; i++) counts[2 * gabi::OP_COUNT + 1 + i] = g_fused[i].load();
     if (reset) {
         for (auto &c : g_op_count) c.store(0);
+        for (auto &c : g_fused) c.store(0);
+        for (auto &c : g_op_ns) c.store(0);
         g_host_ns.store(0);
     }
     return GGML_HIP_OK;

@@ -162,6 +162,41 @@ __global__ __launch_bounds__(TPB) void k_rope_f32(const char *x, char *d, int64_
     o[1] = x0 * t.y + x1 * t.x;
 }
 
+// rope, then ggml_cpy of the rope output (contiguous [ne2][ne1][ne0]) into a strided view (the K
+// cache, F16): element i = i0 + ne0*(i1 + ne1*i2) of the rope output goes to the copy's
+// (i10, i11, i12) = i split by (ne10, ne11), as k_cpy_f32 maps it
+template <bool F16>
+__global__ __launch_bounds__(TPB) void k_rope_cpy(const char *x, char *d, int64_t ne0, int64_t ne1, int64_t ne2,
+                                                  int64_t nb01, int64_t nb02, int64_t nb03, int64_t nb1, int64_t nb2,
+                                                  int64_t nb3, int64_t n, const float2 *cs, int npairs, char *c,
+                                                  int64_t ne10, int64_t ne11, int64_t nb10, int64_t nb11, int64_t nb12) {
+    const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (k >= n) return;
+    const int64_t np = ne0 / 2;
+    const int64_t j = k % np;
+    const int64_t r = k / np;
+    const int64_t i1 = r % ne1, i2 = (r / ne1) % ne2, i3 = r / (ne1 * ne2);
+    const float2 t = cs[i2 * npairs + j];
+    const float *src = (const float *)(x + i3 * nb03 + i2 * nb02 + i1 * nb01) + 2 * j;
+    float *o = (float *)(d + i3 * nb3 + i2 * nb2 + i1 * nb1) + 2 * j;
+    const float x0 = src[0], x1 = src[1];
+    const float y0 = x0 * t.x - x1 * t.y;
+    const float y1 = x0 * t.y + x1 * t.x;
+    o[0] = y0;
+    o[1] = y1;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int64_t i = 2 * j + e + ne0 * (i1 + ne1 * i2);
+        const int64_t i12 = i / (ne10 * ne11), i11 = (i / ne10) % ne11, i10 = i % ne10;
+        char *dst = c + i10 * nb10 + i11 * nb11 + i12 * nb12;
+        const float v = e ? y1 : y0;
+        if (F16)
+            *(uint16_t *)dst = f2h_bits(v);
+        else
+            *(float *)dst = v;
+    }
+}
+
 // ----------------------------------------------------------------------------------- cpy (strided)
 template <bool F16>
 __global__ __launch_bounds__(TPB) void k_cpy_f32(const char *x, char *d, int64_t n, int64_t ne00, int64_t ne01,
@@ -185,9 +220,11 @@ __global__ __launch_bounds__(TPB) void k_cpy_f32(const char *x, char *d, int64_t
 // transposed V views of the KV cache).  32 lanes per output = the 4 x 8 fp32 accumulator lanes of
 // the AVX F16 loop (element e < np goes to lane e % 32, fma in order of e); then GGML_F32x8_REDUCE
 // (accumulators (0+2)+(1+3), 128-bit halves, two hadds) and the tail e >= np added in double.
+// merged != nullptr: the value is also stored at merged[(i1 * ne02 + i2) * ne01 + i0], i.e. the
+// contiguous copy of permute(dst, 0, 2, 1, 3) (llama.cpp's KQV_merged_contiguous, fused)
 __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32(const char *s0, const char *s1, float *d, int K,
                                                          int64_t ne01, int64_t ne11, int64_t ne02, int64_t nb01,
-                                                         int64_t nb02, int64_t nb11, int64_t nb12) {
+                                                         int64_t nb02, int64_t nb11, int64_t nb12, float *merged) {
     const int64_t o = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 5;   // output index
     const int l = threadIdx.x & 31;
     const int64_t nout = ne01 * ne11 * ne02;
@@ -213,6 +250,7 @@ __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32(const char *s0, const c
         double sum = (double)res;
         for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(yr[e])));
         d[o] = (float)sum;
+        if (merged) merged[(i1 * ne02 + i2) * ne01 + i0] = (float)sum;
     }
 }
 
@@ -443,6 +481,22 @@ hipError_t op_rope_f32(const void *x, void *d, const int64_t ne[4], const int64_
     return hipGetLastError();
 }
 
+hipError_t op_rope_cpy_f32(const void *x, void *d, const int64_t ne[4], const int64_t nbx[4], const int64_t nbd[4],
+                           const void *cs, int npairs, void *c, bool to_f16, int64_t ne10, int64_t ne11, int64_t nb10,
+                           int64_t nb11, int64_t nb12, hipStream_t s) {
+    const int64_t n = ne[0] / 2 * ne[1] * ne[2] * ne[3];
+    if (n <= 0) return hipSuccess;
+    if (to_f16)
+        hipLaunchKernelGGL(k_rope_cpy<true>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1],
+                           ne[2], nbx[1], nbx[2], nbx[3], nbd[1], nbd[2], nbd[3], n, (const float2 *)cs, npairs, (char *)c,
+                           ne10, ne11, nb10, nb11, nb12);
+    else
+        hipLaunchKernelGGL(k_rope_cpy<false>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1],
+                           ne[2], nbx[1], nbx[2], nbx[3], nbd[1], nbd[2], nbd[3], n, (const float2 *)cs, npairs, (char *)c,
+                           ne10, ne11, nb10, nb11, nb12);
+    return hipGetLastError();
+}
+
 hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne00, int64_t ne01, int64_t nb00,
                       int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11, int64_t nb10, int64_t nb11, int64_t nb12,
                       hipStream_t s) {
@@ -457,11 +511,11 @@ hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne
 }
 
 hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11, int64_t ne02,
-                              int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s) {
+                              int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s, float *merged) {
     const int64_t nout = ne01 * ne11 * ne02;
     if (nout <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_mul_mat_f16_f32, dim3(blocks(nout * 32)), dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d,
-                       K, ne01, ne11, ne02, nb01, nb02, nb11, nb12);
+                       K, ne01, ne11, ne02, nb01, nb02, nb11, nb12, merged);
     return hipGetLastError();
 }
 

@@ -31,11 +31,15 @@ pytestmark = [pytest.mark.gpu,
 OPS = json.load(open(os.path.join(GOLD, "ggml_op_enum.json")))
 
 
-def op_stats(L, reset=True):
+N_FUSED = 6   # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
+
+
+def op_stats(L, reset=True, fused=False):
     L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-    c = np.zeros(OPS["GGML_OP_COUNT"], np.int64)
+    n = OPS["GGML_OP_COUNT"]
+    c = np.zeros(2 * n + 1 + N_FUSED, np.int64)
     ggml_hip.check(L.ggml_hip_debug_op_stats(c.ctypes.data, c.size, 1 if reset else 0), "op stats")
-    return c
+    return (c[:n], c[2 * n + 1:]) if fused else c[:n]
 
 
 def run_llama(tmp_path, exact, ngl, stats=None):
@@ -136,7 +140,7 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode
     op_stats(L)
     try:
         got = run(HIP_LIB, 99)
-        ran = op_stats(L)
+        ran, fused = op_stats(L, fused=True)
     finally:
         L.ggml_hip_set_exact(prev)
         L.ggml_hip_debug_set_fuse(1)
@@ -144,3 +148,10 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode
     assert np.isfinite(ref).all()
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert ran[OPS["GGML_OP_SOFT_MAX"]] >= n_decode * hp["n_layer"]
+    # every chain of a LLaMA layer fused once per layer and eval when fusion is on, never when off:
+    # add/rms_norm/mul, scale/mask/soft_max, silu/mul, rope/cpy (K cache), KQV/merge, w3 under silu
+    evals = n_decode + 1
+    if fuse:
+        assert (fused >= evals * hp["n_layer"]).all(), fused
+    else:
+        assert (fused == 0).all(), fused

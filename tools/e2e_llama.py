@@ -93,6 +93,10 @@ def bench(lib_path, model, n_prompt, n_decode, threads, ngl, reps, nv):
             "n_gpu_layers": ngl}, logits
 
 
+OP_NAMES = {2: "add", 6: "mul", 23: "silu", 26: "rms_norm", 32: "mul_mat", 34: "scale", 36: "cpy", 38: "reshape",
+            39: "view", 40: "permute", 41: "transpose", 45: "diag_mask_inf", 47: "soft_max", 49: "rope"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--decode", type=int, default=64)
@@ -101,6 +105,7 @@ def main():
     ap.add_argument("--threads-cpu", type=int, default=16)
     ap.add_argument("--threads-gpu", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--modes", default="fast,exact")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import ggml_hip as gh
@@ -117,16 +122,21 @@ def main():
         if not args.no_cpu:
             res["cpu"], lg_cpu = bench(CPU_LIB, model, args.prompt, args.decode_cpu, args.threads_cpu, 0, 1, nv)
             print("cpu", res["cpu"], file=sys.stderr, flush=True)
-        for mode in ("fast", "exact"):
+        for mode in args.modes.split(","):
             gh.check(L.ggml_hip_set_exact(1 if mode == "exact" else 0))
             L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-            st = np.zeros(69, np.int64)
+            st = np.zeros(69 + 68, np.int64)
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
             r, lg = bench(HIP_LIB, model, args.prompt, args.decode, args.threads_gpu, 99, 3, nv)
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
             ntok = 3 * args.prompt + args.decode      # evals: 3 prompt reps + decode steps
             r["backend_nodes_per_eval"] = round(float(st[:68].sum()) / (3 + args.decode), 1)
             r["backend_host_ms_per_eval"] = round(float(st[68]) / 1e6 / (3 + args.decode), 3)
+            # per op of the arriving node: nodes per eval and host us per eval (fused chains are
+            # charged to the node that completes them)
+            r["backend_per_op"] = {OP_NAMES.get(i, str(i)): [round(float(st[i]) / (3 + args.decode), 1),
+                                                             round(float(st[69 + i]) / 1e3 / (3 + args.decode), 1)]
+                                   for i in range(68) if st[i] or st[69 + i]}
             r["finite"] = bool(np.isfinite(lg).all())
             if not args.no_cpu:       # same token sequence as the CPU run: compare the last logits
                 _, lg8 = bench(HIP_LIB, model, args.prompt, args.decode_cpu, args.threads_gpu, 99, 1, nv)

@@ -217,6 +217,11 @@ const char *ggml_hip_version(void);
    counts[137 + k] = fused launches of chain k (0 add/rms_norm/mul, 1 scale/diag_mask_inf/soft_max,
    2 silu/mul, 3 rope/cpy, 4 f16 mul_mat/permute/cpy, 5 q4_0 mul_mat run while a silu is pending) */
 int    ggml_hip_debug_op_stats(int64_t *counts, int n, int reset);
+/* debug: the attention's f16 x f32 mul_mat on device pointers (synchronous); tiled = 0 one 32-lane
+   group per output, 1 the LDS-tiled kernel, -1 the backend's choice (bit-identical either way) */
+int    ggml_hip_debug_f16_mul_mat(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11,
+                                  int64_t ne02, int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12,
+                                  float *merged, int tiled);
 /* debug: 1/0 = launch fusion of adjacent full-offload nodes on/off (default: env GGML_HIP_FUSE, on) */
 int    ggml_hip_debug_set_fuse(int on);
 

@@ -1797,6 +1797,21 @@ int ggml_hip_debug_op_stats(int64_t *counts, int n, int reset) {
     return GGML_HIP_OK;
 }
 
+// debug: the f16 x f32 mul_mat of the attention on device pointers (tests/test_gpu_f16_mul_mat.py):
+// tiled 0 = one 32-lane group per output, 1 = the LDS-tiled kernel, -1 = the backend's choice
+int ggml_hip_debug_f16_mul_mat(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11,
+                               int64_t ne02, int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, float *merged,
+                               int tiled) {
+    ensure_init();
+    if (g_device_count == 0) return GGML_HIP_ERR_UNSUPPORTED;
+    flush_deferred();
+    HIP_FATAL(hipSetDevice(g_main_device));
+    hipStream_t s = g_dev[g_main_device].stream;
+    HIP_FATAL(ghip::op_mul_mat_f16_f32(s0, s1, d, K, ne01, ne11, ne02, nb01, nb02, nb11, nb12, s, merged, tiled));
+    HIP_FATAL(hipStreamSynchronize(s));
+    return GGML_HIP_OK;
+}
+
 // not in the public header: launch fusion of full-offload chains on (1) / off (0) (tests run both)
 int ggml_hip_debug_set_fuse(int on) {
     flush_deferred();

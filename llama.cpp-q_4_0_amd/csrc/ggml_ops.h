@@ -29,7 +29,7 @@ hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne
 // merged != nullptr: also the contiguous copy of permute(dst, 0, 2, 1, 3) (fused KQV_merged_contiguous)
 hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11, int64_t ne02,
                               int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s,
-                              float *merged = nullptr);
+                              float *merged = nullptr, int tiled = -1);   // tiled: -1 auto, 0 / 1 force
 // rope (as op_rope_f32) whose output is then copied (ggml_cpy, F32 -> F32/F16) into the strided view c
 hipError_t op_rope_cpy_f32(const void *x, void *d, const int64_t ne[4], const int64_t nbx[4], const int64_t nbd[4],
                            const void *cs, int npairs, void *c, bool to_f16, int64_t ne10, int64_t ne11, int64_t nb10,

@@ -254,6 +254,109 @@ __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32(const char *s0, const c
     }
 }
 
+// The same dot products for many src1 rows (prefill attention: KQ and KQV over N tokens), tiled.
+// A workgroup owns FT x FT outputs of one channel i2; the four threads of a group own the four
+// 8-lane AVX accumulators j = 0..3 (chains 8j..8j+7: element e < np goes to chain e % 32, fma in
+// order of e) of a 2 x 2 output block, reading 8 fp16 values per row per 32-element step from LDS
+// (src0 rows as stored, src1 rows rounded to fp16 on staging).  Afterwards (s0+s2)+(s1+s3) comes
+// from two xor-shuffles within the group, each thread finishes one output of the block with the
+// in-vector tree of GGML_F32x8_REDUCE and the double tail: the same operations in the same order
+// as k_mul_mat_f16_f32, so both kernels give the same bits.
+constexpr int FT = 16;                 // outputs per tile side
+constexpr int FKC = 128;               // K elements per LDS stage (4 AVX steps)
+constexpr int FLD = FKC + 8;           // LDS row pitch in halves (16-byte aligned, staggered banks)
+
+__global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32_tiled(const char *s0, const char *s1, float *d, int K,
+                                                               int64_t ne01, int64_t ne11, int64_t ne02, int64_t nb01,
+                                                               int64_t nb02, int64_t nb11, int64_t nb12,
+                                                               float *merged) {
+    __shared__ __attribute__((aligned(16))) uint16_t xs[FT * FLD];
+    __shared__ __attribute__((aligned(16))) uint16_t ys[FT * FLD];
+    const int t = threadIdx.x;
+    const int j = t & 3, g = t >> 2;                       // accumulator group, 2 x 2 output block
+    const int br = (g & 7) * 2, bc = (g >> 3) * 2;         // block origin in the tile (rows, cols)
+    const int64_t r0 = (int64_t)blockIdx.x * FT, c0 = (int64_t)blockIdx.y * FT, i2 = blockIdx.z;
+    const char *x0 = s0 + i2 * nb02;
+    const char *y0 = s1 + i2 * nb12;
+    const int np = K & ~31;
+    // staging role: row sr of the tile, 8 consecutive elements from se
+    const int sr = t >> 4, se = (t & 15) * 8;
+    const int64_t xrow = r0 + sr < ne01 ? r0 + sr : ne01 - 1;   // clamped: loaded, never stored
+    const int64_t yrow = c0 + sr < ne11 ? c0 + sr : ne11 - 1;
+    const uint16_t *xg = (const uint16_t *)(x0 + xrow * nb01);
+    const float *yg = (const float *)(y0 + yrow * nb11);
+
+    float acc[2][2][8];
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc[r][c][e] = 0.0f;
+
+    for (int k0 = 0; k0 < np; k0 += FKC) {
+        __syncthreads();                                   // previous stage consumed
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const int k = k0 + se + e;
+            xs[sr * FLD + se + e] = k < np ? xg[k] : (uint16_t)0;
+            ys[sr * FLD + se + e] = k < np ? f2h_bits(yg[k]) : (uint16_t)0;
+        }
+        __syncthreads();
+        const int steps = (np - k0) / 32 < FKC / 32 ? (np - k0) / 32 : FKC / 32;
+        for (int s = 0; s < steps; s++) {
+            const int off = 32 * s + 8 * j;
+            uint4 xv[2], yv[2];
+#pragma unroll
+            for (int r = 0; r < 2; r++) xv[r] = *reinterpret_cast<const uint4 *>(xs + (br + r) * FLD + off);
+#pragma unroll
+            for (int c = 0; c < 2; c++) yv[c] = *reinterpret_cast<const uint4 *>(ys + (bc + c) * FLD + off);
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const uint32_t xw[4] = {xv[r].x, xv[r].y, xv[r].z, xv[r].w};
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    const uint32_t yw[4] = {yv[c].x, yv[c].y, yv[c].z, yv[c].w};
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        const uint16_t xb = (uint16_t)(xw[e >> 1] >> (16 * (e & 1)));
+                        const uint16_t yb = (uint16_t)(yw[e >> 1] >> (16 * (e & 1)));
+                        acc[r][c][e] = fmaf(h2f_bits(xb), h2f_bits(yb), acc[r][c][e]);
+                    }
+                }
+            }
+        }
+    }
+    // (s0+s2)+(s1+s3) per lane e, for all four outputs of the block, in every thread of the group
+    float cv[2][2][8];
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const float a = acc[r][c][e] + __shfl_xor(acc[r][c][e], 2);
+                cv[r][c][e] = a + __shfl_xor(a, 1);
+            }
+    // thread j finishes output (j >> 1, j & 1) of the block
+    const int orr = j >> 1, occ = j & 1;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++)
+        v[e] = orr == 0 ? (occ == 0 ? cv[0][0][e] : cv[0][1][e]) : (occ == 0 ? cv[1][0][e] : cv[1][1][e]);
+    const float t0 = v[0] + v[4], t1 = v[1] + v[5], t2 = v[2] + v[6], t3 = v[3] + v[7];
+    const float res = (t0 + t1) + (t2 + t3);
+    const int64_t i0 = r0 + br + orr, i1 = c0 + bc + occ;
+    if (i0 < ne01 && i1 < ne11) {
+        const uint16_t *xr = (const uint16_t *)(x0 + i0 * nb01);
+        const float *yr = (const float *)(y0 + i1 * nb11);
+        double sum = (double)res;
+        for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(yr[e])));
+        d[(i2 * ne11 + i1) * ne01 + i0] = (float)sum;
+        if (merged) merged[(i1 * ne02 + i2) * ne01 + i0] = (float)sum;
+    }
+}
+
 // ----------------------------------------------------------------------------------- fused chains
 // Back-to-back nodes of a LLaMA graph in one launch (ggml-hip.cpp defers the producer until its
 // consumer arrives).  Each stage computes exactly what its own node's kernel above computes, in
@@ -511,9 +614,20 @@ hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne
 }
 
 hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11, int64_t ne02,
-                              int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s, float *merged) {
+                              int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s, float *merged,
+                              int tiled) {
     const int64_t nout = ne01 * ne11 * ne02;
     if (nout <= 0) return hipSuccess;
+    static const int tiled_min = getenv("GGML_HIP_F16_TILED_MIN") ? atoi(getenv("GGML_HIP_F16_TILED_MIN")) : 8;
+    const bool fits = ne02 <= 65535 && (ne11 + FT - 1) / FT <= 65535;
+    if (fits && (tiled > 0 || (tiled < 0 && tiled_min > 0 && ne11 >= tiled_min))) {
+        // many src1 rows (prefill): tiled through LDS, same bits
+        hipLaunchKernelGGL(k_mul_mat_f16_f32_tiled, dim3((unsigned)((ne01 + FT - 1) / FT), (unsigned)((ne11 + FT - 1) / FT),
+                                                         (unsigned)ne02),
+                           dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d, K, ne01, ne11, ne02, nb01, nb02, nb11,
+                           nb12, merged);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_mul_mat_f16_f32, dim3(blocks(nout * 32)), dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d,
                        K, ne01, ne11, ne02, nb01, nb02, nb11, nb12, merged);
     return hipGetLastError();

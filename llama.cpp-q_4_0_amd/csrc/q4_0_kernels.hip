@@ -457,6 +457,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
 #pragma unroll
             for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
         } else {
+#ifdef GEMV_WSLEEP
+            __builtin_amdgcn_s_sleep(GEMV_WSLEEP);                   // A/B knob: x loads enter first
+#endif
 #pragma unroll
             for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
         }

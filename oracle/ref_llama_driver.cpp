@@ -91,6 +91,8 @@ extern "C" int refllama_logits(const char *path, const int *tokens, int n_tokens
 extern "C" int refllama_bench(const char *path, int n_prompt, int n_decode, int n_threads, int n_gpu_layers, int n_ctx,
                               int reps, double *out, float *last_logits) {
     using clk = std::chrono::steady_clock;
+    // llama_eval does not check n_past + N <= n_ctx; past it the KV-cache views run off the cache
+    if (n_prompt < 1 || n_decode < 0 || n_prompt + n_decode > n_ctx || n_prompt > 512) return -5;
     llama_init_backend(false);
     llama_context_params p = llama_context_default_params();
     p.n_ctx = n_ctx;

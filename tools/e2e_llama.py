@@ -83,7 +83,9 @@ def bench(lib_path, model, n_prompt, n_decode, threads, ngl, reps, nv):
     lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
     out = np.zeros(3, np.float64)
     logits = np.zeros(nv, np.float32)
-    rc = lib.refllama_bench(model.encode(), n_prompt, n_decode, threads, ngl, 512, reps, out.ctypes.data,
+    # the KV cache must hold every position (llama.cpp does not check n_past + N <= n_ctx)
+    n_ctx = max(512, -(-(n_prompt + n_decode) // 512) * 512)
+    rc = lib.refllama_bench(model.encode(), n_prompt, n_decode, threads, ngl, n_ctx, reps, out.ctypes.data,
                             logits.ctypes.data)
     if rc != nv:
         raise RuntimeError(f"refllama_bench({lib_path}) failed: {rc}")
@@ -117,7 +119,8 @@ def main():
     print(f"model {size / 1e9:.2f} GB written in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     nv = HP7B["n_vocab"]
     res = {"model": "LLaMA-7B shape, GGJT v3 q4_0, random valid blocks (synthetic)", "model_bytes": size,
-           "caller": "reference llama.cpp + ggml.c (oracle/_ref builds, unmodified sources)", "n_ctx": 512}
+           "caller": "reference llama.cpp + ggml.c (oracle/_ref builds, unmodified sources)",
+           "n_ctx": max(512, -(-(args.prompt + args.decode) // 512) * 512)}
     try:
         if not args.no_cpu:
             res["cpu"], lg_cpu = bench(CPU_LIB, model, args.prompt, args.decode_cpu, args.threads_cpu, 0, 1, nv)

@@ -257,103 +257,152 @@ __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32(const char *s0, const c
 // The same dot products for many src1 rows (prefill attention: KQ and KQV over N tokens), tiled.
 // A workgroup owns FT x FT outputs of one channel i2; the four threads of a group own the four
 // 8-lane AVX accumulators j = 0..3 (chains 8j..8j+7: element e < np goes to chain e % 32, fma in
-// order of e) of a 2 x 2 output block, reading 8 fp16 values per row per 32-element step from LDS
-// (src0 rows as stored, src1 rows rounded to fp16 on staging).  Afterwards (s0+s2)+(s1+s3) comes
-// from two xor-shuffles within the group, each thread finishes one output of the block with the
-// in-vector tree of GGML_F32x8_REDUCE and the double tail: the same operations in the same order
-// as k_mul_mat_f16_f32, so both kernels give the same bits.
-constexpr int FT = 16;                 // outputs per tile side
+// order of e) of a 4 x 4 output block, reading 8 fp16 values per row per 32-element step from LDS
+// (src0 rows as stored, src1 rows rounded to fp16 on staging) and multiplying them with
+// v_fma_mix_f32 (fp16 operands, exact widening, one fp32 rounding: the same value as fmaf on the
+// widened operands).  Afterwards (s0+s2)+(s1+s3) comes from two quad DPP exchanges within the
+// group, thread j finishes column j of the block with the in-vector tree of GGML_F32x8_REDUCE and
+// the double tail: the same operations in the same order as k_mul_mat_f16_f32, so both kernels
+// give the same bits.
+constexpr int FT = 32;                 // outputs per tile side
+constexpr int FB = 4;                  // outputs per block side (per group of 4 threads)
 constexpr int FKC = 128;               // K elements per LDS stage (4 AVX steps)
-constexpr int FLD = FKC + 8;           // LDS row pitch in halves (16-byte aligned, staggered banks)
+constexpr int FLD = FKC + 8;           // LDS row pitch in halves (16-byte rows, staggered banks)
+static_assert((FT / FB) * (FT / FB) * 4 == TPB, "one group of four threads per output block");
 
-__global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32_tiled(const char *s0, const char *s1, float *d, int K,
+__device__ __forceinline__ void fma_mix_lo(uint32_t a, uint32_t b, float &c) {   // c = fp16 a.lo * b.lo + c
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,1,0]" : "+v"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void fma_mix_hi(uint32_t a, uint32_t b, float &c) {   // c = fp16 a.hi * b.hi + c
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "+v"(c) : "v"(a), "v"(b));
+}
+template <int CTRL>
+__device__ __forceinline__ float quad_dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__global__ __launch_bounds__(TPB, 2) void k_mul_mat_f16_f32_tiled(const char *s0, const char *s1, float *d, int K,
                                                                int64_t ne01, int64_t ne11, int64_t ne02, int64_t nb01,
                                                                int64_t nb02, int64_t nb11, int64_t nb12,
                                                                float *merged) {
     __shared__ __attribute__((aligned(16))) uint16_t xs[FT * FLD];
     __shared__ __attribute__((aligned(16))) uint16_t ys[FT * FLD];
     const int t = threadIdx.x;
-    const int j = t & 3, g = t >> 2;                       // accumulator group, 2 x 2 output block
-    const int br = (g & 7) * 2, bc = (g >> 3) * 2;         // block origin in the tile (rows, cols)
+    const int j = t & 3, g = t >> 2;                       // accumulator group, output block
+    const int br = (g & 7) * FB, bc = (g >> 3) * FB;       // block origin in the tile (rows, cols)
     const int64_t r0 = (int64_t)blockIdx.x * FT, c0 = (int64_t)blockIdx.y * FT, i2 = blockIdx.z;
     const char *x0 = s0 + i2 * nb02;
     const char *y0 = s1 + i2 * nb12;
     const int np = K & ~31;
-    // staging role: row sr of the tile, 8 consecutive elements from se
+    // staging role: rows sr and sr + 16 of the tile, 8 consecutive elements from se
     const int sr = t >> 4, se = (t & 15) * 8;
-    const int64_t xrow = r0 + sr < ne01 ? r0 + sr : ne01 - 1;   // clamped: loaded, never stored
-    const int64_t yrow = c0 + sr < ne11 ? c0 + sr : ne11 - 1;
-    const uint16_t *xg = (const uint16_t *)(x0 + xrow * nb01);
-    const float *yg = (const float *)(y0 + yrow * nb11);
+    const uint16_t *xg[2];
+    const float *yg[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int64_t xr = r0 + sr + 16 * q < ne01 ? r0 + sr + 16 * q : ne01 - 1;   // clamped: loaded, not stored
+        const int64_t yr = c0 + sr + 16 * q < ne11 ? c0 + sr + 16 * q : ne11 - 1;
+        xg[q] = (const uint16_t *)(x0 + xr * nb01);
+        yg[q] = (const float *)(y0 + yr * nb11);
+    }
 
-    float acc[2][2][8];
+    float acc[FB][FB][8];
 #pragma unroll
-    for (int r = 0; r < 2; r++)
+    for (int r = 0; r < FB; r++)
 #pragma unroll
-        for (int c = 0; c < 2; c++)
+        for (int c = 0; c < FB; c++)
 #pragma unroll
             for (int e = 0; e < 8; e++) acc[r][c][e] = 0.0f;
 
     for (int k0 = 0; k0 < np; k0 += FKC) {
+        const int k = k0 + se;
+        uint4 xv[2], yv[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            uint32_t xw[4], yw[4];
+            if (k + 8 <= np && ((uintptr_t)(xg[q] + k) & 15) == 0) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(xg[q] + k);
+                xw[0] = v.x, xw[1] = v.y, xw[2] = v.z, xw[3] = v.w;
+            } else {
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    const uint32_t lo = k + 2 * w < np ? xg[q][k + 2 * w] : 0u;
+                    const uint32_t hi = k + 2 * w + 1 < np ? xg[q][k + 2 * w + 1] : 0u;
+                    xw[w] = lo | (hi << 16);
+                }
+            }
+            float yf[8];
+            if (k + 8 <= np && ((uintptr_t)(yg[q] + k) & 15) == 0) {
+                const float4 a = *reinterpret_cast<const float4 *>(yg[q] + k);
+                const float4 b = *reinterpret_cast<const float4 *>(yg[q] + k + 4);
+                yf[0] = a.x, yf[1] = a.y, yf[2] = a.z, yf[3] = a.w, yf[4] = b.x, yf[5] = b.y, yf[6] = b.z, yf[7] = b.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) yf[e] = k + e < np ? yg[q][k + e] : 0.0f;
+            }
+#pragma unroll
+            for (int w = 0; w < 4; w++) yw[w] = (uint32_t)f2h_bits(yf[2 * w]) | ((uint32_t)f2h_bits(yf[2 * w + 1]) << 16);
+            xv[q] = make_uint4(xw[0], xw[1], xw[2], xw[3]);
+            yv[q] = make_uint4(yw[0], yw[1], yw[2], yw[3]);
+        }
         __syncthreads();                                   // previous stage consumed
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            const int k = k0 + se + e;
-            xs[sr * FLD + se + e] = k < np ? xg[k] : (uint16_t)0;
-            ys[sr * FLD + se + e] = k < np ? f2h_bits(yg[k]) : (uint16_t)0;
+        for (int q = 0; q < 2; q++) {
+            *reinterpret_cast<uint4 *>(xs + (sr + 16 * q) * FLD + se) = xv[q];
+            *reinterpret_cast<uint4 *>(ys + (sr + 16 * q) * FLD + se) = yv[q];
         }
         __syncthreads();
         const int steps = (np - k0) / 32 < FKC / 32 ? (np - k0) / 32 : FKC / 32;
         for (int s = 0; s < steps; s++) {
             const int off = 32 * s + 8 * j;
-            uint4 xv[2], yv[2];
+            uint4 xr[FB];
 #pragma unroll
-            for (int r = 0; r < 2; r++) xv[r] = *reinterpret_cast<const uint4 *>(xs + (br + r) * FLD + off);
+            for (int r = 0; r < FB; r++) xr[r] = *reinterpret_cast<const uint4 *>(xs + (br + r) * FLD + off);
 #pragma unroll
-            for (int c = 0; c < 2; c++) yv[c] = *reinterpret_cast<const uint4 *>(ys + (bc + c) * FLD + off);
+            for (int c = 0; c < FB; c++) {
+                const uint4 yc = *reinterpret_cast<const uint4 *>(ys + (bc + c) * FLD + off);
+                const uint32_t yw[4] = {yc.x, yc.y, yc.z, yc.w};
 #pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const uint32_t xw[4] = {xv[r].x, xv[r].y, xv[r].z, xv[r].w};
+                for (int r = 0; r < FB; r++) {
+                    const uint32_t xw[4] = {xr[r].x, xr[r].y, xr[r].z, xr[r].w};
 #pragma unroll
-                for (int c = 0; c < 2; c++) {
-                    const uint32_t yw[4] = {yv[c].x, yv[c].y, yv[c].z, yv[c].w};
-#pragma unroll
-                    for (int e = 0; e < 8; e++) {
-                        const uint16_t xb = (uint16_t)(xw[e >> 1] >> (16 * (e & 1)));
-                        const uint16_t yb = (uint16_t)(yw[e >> 1] >> (16 * (e & 1)));
-                        acc[r][c][e] = fmaf(h2f_bits(xb), h2f_bits(yb), acc[r][c][e]);
+                    for (int w = 0; w < 4; w++) {
+                        fma_mix_lo(xw[w], yw[w], acc[r][c][2 * w]);
+                        fma_mix_hi(xw[w], yw[w], acc[r][c][2 * w + 1]);
                     }
                 }
             }
         }
     }
-    // (s0+s2)+(s1+s3) per lane e, for all four outputs of the block, in every thread of the group
-    float cv[2][2][8];
+    // (s0+s2)+(s1+s3) per lane e: quad_perm [2,3,0,1] (xor 2), then [1,0,3,2] (xor 1)
 #pragma unroll
-    for (int r = 0; r < 2; r++)
+    for (int r = 0; r < FB; r++)
 #pragma unroll
-        for (int c = 0; c < 2; c++)
+        for (int c = 0; c < FB; c++)
 #pragma unroll
             for (int e = 0; e < 8; e++) {
-                const float a = acc[r][c][e] + __shfl_xor(acc[r][c][e], 2);
-                cv[r][c][e] = a + __shfl_xor(a, 1);
+                const float a = acc[r][c][e] + quad_dpp<0x4E>(acc[r][c][e]);
+                acc[r][c][e] = a + quad_dpp<0xB1>(a);
             }
-    // thread j finishes output (j >> 1, j & 1) of the block
-    const int orr = j >> 1, occ = j & 1;
-    float v[8];
+    // thread j finishes column j of the block
 #pragma unroll
-    for (int e = 0; e < 8; e++)
-        v[e] = orr == 0 ? (occ == 0 ? cv[0][0][e] : cv[0][1][e]) : (occ == 0 ? cv[1][0][e] : cv[1][1][e]);
-    const float t0 = v[0] + v[4], t1 = v[1] + v[5], t2 = v[2] + v[6], t3 = v[3] + v[7];
-    const float res = (t0 + t1) + (t2 + t3);
-    const int64_t i0 = r0 + br + orr, i1 = c0 + bc + occ;
-    if (i0 < ne01 && i1 < ne11) {
-        const uint16_t *xr = (const uint16_t *)(x0 + i0 * nb01);
-        const float *yr = (const float *)(y0 + i1 * nb11);
-        double sum = (double)res;
-        for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(yr[e])));
-        d[(i2 * ne11 + i1) * ne01 + i0] = (float)sum;
-        if (merged) merged[(i1 * ne02 + i2) * ne01 + i0] = (float)sum;
+    for (int c = 0; c < FB; c++) {
+        if (c != j) continue;
+#pragma unroll
+        for (int r = 0; r < FB; r++) {
+            const float *v = acc[r][c];
+            const float t0 = v[0] + v[4], t1 = v[1] + v[5], t2 = v[2] + v[6], t3 = v[3] + v[7];
+            const float res = (t0 + t1) + (t2 + t3);
+            const int64_t i0 = r0 + br + r, i1 = c0 + bc + c;
+            if (i0 < ne01 && i1 < ne11) {
+                const uint16_t *xr = (const uint16_t *)(x0 + i0 * nb01);
+                const float *yr = (const float *)(y0 + i1 * nb11);
+                double sum = (double)res;
+                for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(yr[e])));
+                d[(i2 * ne11 + i1) * ne01 + i0] = (float)sum;
+                if (merged) merged[(i1 * ne02 + i2) * ne01 + i0] = (float)sum;
+            }
+        }
     }
 }
 

@@ -112,11 +112,13 @@ HP128 = dict(n_vocab=1000, n_embd=512, n_mult=256, n_head=4, n_layer=2, n_rot=12
 
 @pytest.mark.skipif(not os.path.exists(CPU_LIB), reason="oracle/_ref/libllama_ref_cpu.so not built")
 @pytest.mark.parametrize("fuse", [1, 0], ids=["fused", "unfused"])
-@pytest.mark.parametrize("hp,n_prompt,n_decode", [(G.HP, 8, 600), (HP128, 40, 300)], ids=["head64", "head128"])
+@pytest.mark.parametrize("hp,n_prompt,n_decode", [(G.HP, 8, 600), (HP128, 40, 300), (HP128, 300, 20)],
+                         ids=["head64", "head128", "head128_prompt300"])
 def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode, fuse):
     """Hundreds of single-token steps at full offload (KV cache, rope positions and soft_max rows up
     to 608, the rope table regrown past its first 512 positions; LLaMA's head_dim 128 and a
-    40-token batched prompt in the second case): the last logits equal the reference's CPU-only
+    40-token batched prompt in the second case; a 300-token prompt, whose attention runs through the
+    LDS-tiled f16 mul_mat over several K stages with a tail, in the third): the last logits equal the reference's CPU-only
     build bit for bit (both run live on this host through refllama_bench)."""
     L = ggml_hip.load()
     mp = str(tmp_path / "m.ggjt")

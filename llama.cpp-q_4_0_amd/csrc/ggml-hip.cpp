@@ -590,8 +590,8 @@ std::atomic<int64_t> g_op_count[gabi::OP_COUNT];      // device nodes run, per g
 std::atomic<int64_t> g_host_ns{0};                     // host time inside the taken nodes (debug stats)
 std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of the node that arrived
 // fused launches by chain: add/rms_norm/mul, scale/mask/soft_max, silu/mul, rope/cpy, KQV/merge cpy,
-// q4_0 mul_mat run under a pending silu
-constexpr int N_FUSED = 6;
+// q4_0 mul_mat run under a pending silu, sibling q4_0 GEMVs (wq|wk|wv, w1|w3) run as one group
+constexpr int N_FUSED = 7;
 std::atomic<int64_t> g_fused[N_FUSED];
 
 // fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)
@@ -931,6 +931,127 @@ bool try_fuse(tensor *t) {
     return false;
 }
 
+// ---- sibling q4_0 GEMVs.  ggml visits a LLaMA layer depth first, so the mul_mats that share an
+// input are not adjacent (wk, rope K, cpy K, wv, cpy V, wq, ...; w1, silu, w3).  A decode q4_0
+// mul_mat (one token, device operands) opens a group; the device-only nodes that follow are held
+// behind it ("after" nodes, replayed in arrival order once the group has run), and a later q4_0
+// mul_mat with the same src1 joins the group when running it ahead of the held nodes is safe: it
+// reads none of their outputs and its output overlaps none of their operands.  The group is one
+// multi-matrix GEMV launch (ggml_hip_mul_mat_q4_0_multi), bit-identical to separate launches.
+struct Group {
+    int n = 0, na = 0;
+    tensor *mm[4] = {};
+    tensor *after[16] = {};
+};
+Group g_grp;
+void execute_node(tensor *t);
+
+// last byte + 1 of a device tensor's storage, strides included (views, permutes)
+size_t span_bytes(const tensor *t) {
+    if (gabi::blck_size(t->type) != 1) return gabi::nbytes(t);
+    size_t last = gabi::type_size(t->type);
+    for (int i = 0; i < 4; i++) last += (size_t)(t->ne[i] - 1) * t->nb[i];
+    return last;
+}
+bool dev_overlap(const tensor *a, const tensor *b) {
+    if (!a || !b || a->backend != gabi::BACKEND_GPU || b->backend != gabi::BACKEND_GPU || !a->extra || !b->extra) return false;
+    const char *pa = dptr(a), *pb = dptr(b);
+    return pa < pb + span_bytes(b) && pb < pa + span_bytes(a);
+}
+
+bool main_device_only_split(int64_t M) {
+    int active = 0, only = -1;
+    for (int id = 0; id < g_device_count; id++) {
+        int64_t lo, hi;
+        split_range(M, id, &lo, &hi);
+        if (lo < hi) active++, only = id;
+    }
+    return active == 1 && only == g_main_device;
+}
+
+bool group_mm_ok(const tensor *t) {
+    if (!fuse_enabled() || t->op != gabi::OP_MUL_MAT || !t->src0 || t->src0->type != gabi::TYPE_Q4_0) return false;
+    const tensor *a = t->src0, *b = t->src1;
+    if (!b || t->backend != gabi::BACKEND_GPU || !t->extra || b->backend != gabi::BACKEND_GPU || !b->extra || !a->extra)
+        return false;
+    if (!supported_mul_mat(a, b, t) || !is_contiguous(a) || !is_contiguous(b) || !is_contiguous(t)) return false;
+    if (b->ne[1] != 1 || b->ne[2] != 1 || b->ne[3] != 1 || a->ne[2] != 1 || a->ne[3] != 1) return false;
+    if (a->backend == gabi::BACKEND_GPU) return true;
+    return a->backend == gabi::BACKEND_GPU_SPLIT && main_device_only_split(a->ne[1]);
+}
+
+bool group_after_ok(const tensor *t) {
+    auto dev = [](const tensor *x) { return x && x->backend == gabi::BACKEND_GPU && x->extra; };
+    // a CPY node is a view of its target (src1) that llama.cpp does not hand to assign_buffers:
+    // its own backend says nothing, the target's does
+    if (t->op != gabi::OP_CPY && !dev(t)) return false;
+    switch (t->op) {
+        case gabi::OP_ADD:
+        case gabi::OP_MUL:
+            return dev(t->src0) && dev(t->src1);
+        case gabi::OP_SILU:
+        case gabi::OP_RMS_NORM:
+        case gabi::OP_SOFT_MAX:
+            return dev(t->src0);
+        case gabi::OP_SCALE:
+        case gabi::OP_DIAG_MASK_INF:
+        case gabi::OP_ROPE:
+            return dev(t->src0) && host_scalar_param(t->src1);
+        case gabi::OP_CPY:
+            return dev(t->src0) && dev(t->src1);
+        case gabi::OP_MUL_MAT:
+            return t->src0 && t->src0->type == gabi::TYPE_F16 && dev(t->src0) && dev(t->src1);
+        default:
+            return false;
+    }
+}
+
+// may q4_0 mul_mat m run before every held node and beside the current members?
+bool group_join_ok(const tensor *m) {
+    const Group &g = g_grp;
+    if (g.n >= 4 || m->src1 != g.mm[0]->src1 || m->src0->ne[0] != g.mm[0]->src0->ne[0]) return false;
+    for (int i = 0; i < g.n; i++)
+        if (dev_overlap(m, g.mm[i]) || dev_overlap(m, g.mm[i]->src1)) return false;
+    for (int i = 0; i < g.na; i++) {
+        const tensor *A = g.after[i];
+        if (dev_overlap(m, A) || dev_overlap(m, A->src0) || dev_overlap(m, A->src1)) return false;
+        if (dev_overlap(A, m->src1) || dev_overlap(A, m->src0)) return false;
+        if (A->op == gabi::OP_CPY && (dev_overlap(A->src1, m->src1) || dev_overlap(A->src1, m->src0))) return false;
+    }
+    return true;
+}
+
+bool trace_nodes() {
+    static const bool on = getenv("GGML_HIP_TRACE_NODES") != nullptr;
+    return on;
+}
+
+void flush_group() {
+    const Group g = g_grp;
+    g_grp = Group{};
+    if (trace_nodes()) fprintf(stderr, "group flush: %d mul_mats (%s ...), %d held nodes\n", g.n, g.mm[0]->name, g.na);
+    if (g.n == 1) {
+        count_node(g.mm[0]);
+        mul_mat_node(g.mm[0]->src0, g.mm[0]->src1, g.mm[0]);
+    } else if (g.n > 1) {
+        const void *w[4];
+        int64_t m[4];
+        float *y[4];
+        for (int i = 0; i < g.n; i++) {
+            w[i] = dptr(g.mm[i]->src0);
+            m[i] = g.mm[i]->src0->ne[1];
+            y[i] = (float *)dptr(g.mm[i]);
+            count_node(g.mm[i]);
+        }
+        HIP_FATAL(hipSetDevice(g_main_device));
+        const int rc = ggml_hip_mul_mat_q4_0_multi(g.n, w, m, g.mm[0]->src0->ne[0], (const float *)dptr(g.mm[0]->src1), 1, y,
+                                                   g_dev[g_main_device].stream);
+        if (rc != GGML_HIP_OK) op_abort(g.mm[0], "sibling q4_0 GEMV group failed");
+        g_fused[6].fetch_add(1, std::memory_order_relaxed);
+    }
+    for (int i = 0; i < g.na; i++) execute_node(g.after[i]);      // the ordinary path, fusion included
+}
+
 // runs (or defers) one taken node; the ith == 0 COMPUTE phase of ggml_hip_compute_forward
 void execute_node(tensor *t) {
     const int op = t->op;
@@ -938,9 +1059,34 @@ void execute_node(tensor *t) {
         count_node(t);                      // no data touched: a pending chain stays pending
         return;
     }
+    if (g_grp.n > 0) {
+        if (group_mm_ok(t) && group_join_ok(t)) {
+            g_grp.mm[g_grp.n++] = t;
+            return;
+        }
+        if (trace_nodes())
+            fprintf(stderr, "group: %s not joined (mm_ok %d, join_ok %d, after_ok %d)\n", t->name, (int)group_mm_ok(t),
+                    group_mm_ok(t) ? (int)group_join_ok(t) : -1, (int)group_after_ok(t));
+        if (!(op == gabi::OP_MUL_MAT && t->src0 && t->src0->type != gabi::TYPE_F16) && group_after_ok(t) &&
+            g_grp.na < 16) {
+            g_grp.after[g_grp.na++] = t;
+            return;
+        }
+        flush_group();
+    }
+    if (g_pend.n == 0 && group_mm_ok(t)) {
+        g_grp.mm[0] = t;
+        g_grp.n = 1;
+        return;
+    }
     if (g_pend.n > 0) {
         if (try_fuse(t)) return;
         flush_pending();
+        if (group_mm_ok(t)) {
+            g_grp.mm[0] = t;
+            g_grp.n = 1;
+            return;
+        }
     }
     if (deferrable(t)) {
         g_pend.node[g_pend.n++] = t;
@@ -958,6 +1104,7 @@ void execute_node(tensor *t) {
 
 // every backend entry point that can touch device memory outside the node sequence
 static inline void flush_deferred() {
+    if (g_grp.n > 0) flush_group();
     if (g_pend.n > 0) flush_pending();
 }
 

@@ -300,8 +300,10 @@ bool exact_mode() {
     return v == 1;
 }
 
+// x_quantized: the workspace already holds q8_0(x) from the previous call on this stream (siblings
+// that share x: ggml_hip_mul_mat_q4_0_multi quantizes once); ignored by the fused GEMV
 int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, float *y, int64_t ldy, int algo,
-                hipStream_t s) {
+                hipStream_t s, bool x_quantized = false) {
     if (!w || !x || !y || K <= 0 || M <= 0 || N < 0) return fail(GGML_HIP_ERR_INVALID, "null pointer or bad shape");
     if (N == 0) return GGML_HIP_OK;
     if (K % 64 != 0) return fail(GGML_HIP_ERR_INVALID, "K must be a multiple of 64 (ggml.c:2344 nb % 2 == 0)");
@@ -328,7 +330,7 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
     }
     int8_t *qs = (int8_t *)g_dev[id].ws;
     float *xd = (float *)((char *)g_dev[id].ws + ((size_t)(N * K + 255) & ~(size_t)255));
-    HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s));
+    if (!x_quantized) HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s));
     if (algo == 4)
         HIP_RET(ghip::mm_exact_q4_0(w, K, M, qs, xd, N, y, ldy, s));
     else if (algo == 3)
@@ -1554,8 +1556,8 @@ int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *
     }
     if (N == 0) return GGML_HIP_OK;
     if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30) || exact_mode()) {
-        for (int i = 0; i < n; i++) {       // GEMM / exact path (x re-quantized per matrix: prefill is MFMA-bound)
-            int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 0, s);
+        for (int i = 0; i < n; i++) {       // GEMM / exact path: x quantized once, one launch per matrix
+            int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 0, s, i > 0);
             if (rc != GGML_HIP_OK) return rc;
         }
         return GGML_HIP_OK;

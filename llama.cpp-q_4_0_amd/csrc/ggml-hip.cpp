@@ -592,8 +592,9 @@ std::atomic<int64_t> g_op_count[gabi::OP_COUNT];      // device nodes run, per g
 std::atomic<int64_t> g_host_ns{0};                     // host time inside the taken nodes (debug stats)
 std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of the node that arrived
 // fused launches by chain: add/rms_norm/mul, scale/mask/soft_max, silu/mul, rope/cpy, KQV/merge cpy,
-// q4_0 mul_mat run under a pending silu, sibling q4_0 GEMVs (wq|wk|wv, w1|w3) run as one group
-constexpr int N_FUSED = 7;
+// q4_0 mul_mat run under a pending silu, sibling q4_0 GEMVs (wq|wk|wv, w1|w3) run as one group,
+// independent rope / rope->cpy / cpy nodes held behind a group run as one launch
+constexpr int N_FUSED = 8;
 std::atomic<int64_t> g_fused[N_FUSED];
 
 // fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)
@@ -1028,6 +1029,108 @@ bool trace_nodes() {
     return on;
 }
 
+// ---- the independent elementwise nodes a group holds (rope K -> K cache, V -> V cache, rope Q):
+// one launch for up to four of them when none reads or writes what another writes
+struct ElemRW {
+    const tensor *r[2];
+    const tensor *w[2];
+};
+bool dev_t(const tensor *x) { return x && x->backend == gabi::BACKEND_GPU && x->extra; }
+
+bool rope_elem(const tensor *t, ghip::ElemOp &op) {
+    const tensor *a = t->src0, *b = t->src1;
+    if (t->op != gabi::OP_ROPE || !dev_t(a) || !dev_t(t) || a->type != gabi::TYPE_F32 || t->type != gabi::TYPE_F32 ||
+        !host_scalar_param(b))
+        return false;
+    const int n_past = ((const int32_t *)b->data)[0], n_dims = ((const int32_t *)b->data)[1];
+    if (((const int32_t *)b->data)[2] != 0 || !same_shape(a, t) || a->nb[0] != 4 || t->nb[0] != 4 || a->ne[0] % 2 ||
+        n_dims % 2 || n_past < 0)
+        return false;
+    const int64_t np = a->ne[0] / 2;
+    const float *cs = rope_table(g_main_device, a->ne[0], n_dims, (int64_t)n_past + a->ne[2], g_dev[g_main_device].stream);
+    op = ghip::ElemOp{};
+    op.kind = 0;
+    op.x = dptr(a);
+    op.d = dptr(t);
+    op.cs = (const float2 *)(cs + (size_t)n_past * np * 2);
+    op.npairs = (int)np;
+    op.n = np * a->ne[1] * a->ne[2] * a->ne[3];
+    op.ne0 = a->ne[0], op.ne1 = a->ne[1], op.ne2 = a->ne[2];
+    op.nbx1 = a->nb[1], op.nbx2 = a->nb[2], op.nbx3 = a->nb[3];
+    op.nbd1 = t->nb[1], op.nbd2 = t->nb[2], op.nbd3 = t->nb[3];
+    return true;
+}
+bool cpy_target_ok(const tensor *t) {     // a CPY node F32 -> F32/F16 between device tensors, 3-d
+    const tensor *a = t->src0, *b = t->src1;
+    return t->op == gabi::OP_CPY && dev_t(a) && dev_t(b) && a->type == gabi::TYPE_F32 &&
+           (b->type == gabi::TYPE_F32 || b->type == gabi::TYPE_F16) && a->ne[3] == 1 && b->ne[3] == 1 &&
+           a->ne[0] * a->ne[1] * a->ne[2] == b->ne[0] * b->ne[1] * b->ne[2];
+}
+void set_copy_target(ghip::ElemOp &op, const tensor *b) {
+    op.c = dptr(b);
+    op.f16 = b->type == gabi::TYPE_F16;
+    op.ne10 = b->ne[0], op.ne11 = b->ne[1], op.nb10 = b->nb[0], op.nb11 = b->nb[1], op.nb12 = b->nb[2];
+}
+
+// batches a prefix of the held list; returns how many held nodes it ran
+int run_elem_prefix(tensor *const *held, int nh) {
+    if (!fuse_enabled()) return 0;
+    ghip::ElemBatch b{};
+    ElemRW rw[ghip::ELEM_MAX];
+    int used = 0;
+    while (b.nops < ghip::ELEM_MAX && used < nh) {
+        tensor *t = held[used];
+        ghip::ElemOp op;
+        ElemRW e{{nullptr, nullptr}, {nullptr, nullptr}};
+        int take = 0;
+        if (rope_elem(t, op)) {
+            e.r[0] = t->src0;
+            e.w[0] = t;
+            take = 1;
+            if (used + 1 < nh && held[used + 1]->src0 == t && cpy_target_ok(held[used + 1]) &&
+                t->ne[3] == 1 && !dev_overlap(held[used + 1]->src1, t) && !dev_overlap(held[used + 1]->src1, t->src0)) {
+                set_copy_target(op, held[used + 1]->src1);
+                e.w[1] = held[used + 1]->src1;
+                take = 2;
+            }
+        } else if (cpy_target_ok(t)) {
+            const tensor *a = t->src0;
+            op = ghip::ElemOp{};
+            op.kind = 1;
+            op.x = dptr(a);
+            op.n = a->ne[0] * a->ne[1] * a->ne[2];
+            op.ne0 = a->ne[0], op.ne1 = a->ne[1];
+            op.nbx1 = a->nb[0], op.nbx2 = a->nb[1], op.nbx3 = a->nb[2];
+            set_copy_target(op, t->src1);
+            e.r[0] = a;
+            e.w[0] = t->src1;
+            take = 1;
+        } else {
+            break;
+        }
+        // independent of every entry already in the batch (they run concurrently)
+        bool ok = true;
+        for (int q = 0; q < b.nops && ok; q++)
+            for (const tensor *w : rw[q].w)
+                for (const tensor *x : {e.r[0], e.r[1], e.w[0], e.w[1]})
+                    if (w && x && dev_overlap(w, x)) ok = false;
+        for (int q = 0; q < b.nops && ok; q++)
+            for (const tensor *w : e.w)
+                for (const tensor *x : rw[q].r)
+                    if (w && x && dev_overlap(w, x)) ok = false;
+        if (!ok) break;
+        rw[b.nops] = e;
+        b.op[b.nops++] = op;
+        used += take;
+    }
+    if (b.nops < 2) return 0;
+    HIP_FATAL(hipSetDevice(g_main_device));
+    HIP_FATAL(ghip::op_elem_batch(b, g_dev[g_main_device].stream));
+    for (int i = 0; i < used; i++) count_node(held[i]);
+    g_fused[7].fetch_add(1, std::memory_order_relaxed);
+    return used;
+}
+
 void flush_group() {
     const Group g = g_grp;
     g_grp = Group{};
@@ -1051,7 +1154,8 @@ void flush_group() {
         if (rc != GGML_HIP_OK) op_abort(g.mm[0], "sibling q4_0 GEMV group failed");
         g_fused[6].fetch_add(1, std::memory_order_relaxed);
     }
-    for (int i = 0; i < g.na; i++) execute_node(g.after[i]);      // the ordinary path, fusion included
+    const int done = run_elem_prefix(g.after, g.na);
+    for (int i = done; i < g.na; i++) execute_node(g.after[i]);   // the ordinary path, fusion included
 }
 
 // runs (or defers) one taken node; the ith == 0 COMPUTE phase of ggml_hip_compute_forward

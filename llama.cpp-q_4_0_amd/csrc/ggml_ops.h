@@ -35,6 +35,29 @@ hipError_t op_rope_cpy_f32(const void *x, void *d, const int64_t ne[4], const in
                            const void *cs, int npairs, void *c, bool to_f16, int64_t ne10, int64_t ne11, int64_t nb10,
                            int64_t nb11, int64_t nb12, hipStream_t s);
 
+// independent rope / rope->cpy / cpy nodes in one launch (each element as its own op computes it)
+constexpr int ELEM_MAX = 4;
+struct ElemOp {
+    int kind;              // 0 rope (mode 0; then the copy into c when c != nullptr), 1 cpy x -> c
+    int f16;               // the copy's target is F16 (else F32)
+    const char *x;         // source
+    char *d;               // rope output
+    char *c;               // copy target (strided view) or nullptr
+    const float2 *cs;      // rope (cos, sin) rows from position n_past
+    int npairs;
+    int64_t n;             // work items: rope pairs or copied elements
+    int64_t ne0, ne1, ne2;                 // rope: x/d shape; cpy: ne00, ne01 (ne2 unused)
+    int64_t nbx1, nbx2, nbx3;              // rope: x strides 1..3; cpy: nb00, nb01, nb02
+    int64_t nbd1, nbd2, nbd3;              // rope: d strides 1..3
+    int64_t ne10, ne11, nb10, nb11, nb12;  // the copy target's shape / strides
+};
+struct ElemBatch {
+    ElemOp op[ELEM_MAX];
+    int nops;
+    unsigned block_begin[ELEM_MAX];       // filled by op_elem_batch
+};
+hipError_t op_elem_batch(const ElemBatch &b, hipStream_t s);
+
 // fused chains (each stage bit-identical to its own op above; intermediates stored unless nullptr)
 // [sum = a + b] -> norm = rms_norm(sum) -> out = norm * w (w: one row); a == nullptr: rms_norm(b)
 hipError_t op_add_rms_norm_mul_f32(const float *a, const float *b, float *sum, float *norm, const float *w, float *out,

@@ -214,6 +214,62 @@ __global__ __launch_bounds__(TPB) void k_cpy_f32(const char *x, char *d, int64_t
         *(float *)o = v;
 }
 
+// ----------------------------------------------------------------------------------- batched
+// Up to ELEM_MAX independent rope / rope->cpy / cpy nodes in one launch (the nodes a LLaMA layer
+// runs between its q4_0 sibling group and the attention: rope K -> K cache, V -> V cache, rope Q).
+// Each block belongs to one op (block_begin prefix sums); every element is computed by the same
+// expression as the op's own kernel above.
+__global__ __launch_bounds__(TPB) void k_elem_batch(const ElemBatch b) {
+    int o = 0;
+#pragma unroll
+    for (int q = 1; q < ELEM_MAX; q++) o += (q < b.nops && blockIdx.x >= b.block_begin[q]) ? 1 : 0;
+    // constant-index copies: no dynamic indexing into the kernarg struct
+    ElemOp op = b.op[0];
+#pragma unroll
+    for (int q = 1; q < ELEM_MAX; q++)
+        if (o == q) op = b.op[q];
+    const int64_t k = (int64_t)(blockIdx.x - b.block_begin[o]) * TPB + threadIdx.x;
+    if (k >= op.n) return;
+    if (op.kind == 1) {                                   // cpy, as k_cpy_f32
+        const int64_t i = k;
+        const int64_t i02 = i / (op.ne0 * op.ne1), i01 = (i / op.ne0) % op.ne1, i00 = i % op.ne0;
+        const int64_t i12 = i / (op.ne10 * op.ne11), i11 = (i / op.ne10) % op.ne11, i10 = i % op.ne10;
+        const float v = *(const float *)(op.x + i00 * op.nbx1 + i01 * op.nbx2 + i02 * op.nbx3);
+        char *dst = op.c + i10 * op.nb10 + i11 * op.nb11 + i12 * op.nb12;
+        if (op.f16)
+            *(uint16_t *)dst = f2h_bits(v);
+        else
+            *(float *)dst = v;
+        return;
+    }
+    // rope (mode 0), as k_rope_f32; then (c != nullptr) the copy of k_rope_cpy
+    const int64_t np = op.ne0 / 2;
+    const int64_t j = k % np;
+    const int64_t r = k / np;
+    const int64_t i1 = r % op.ne1, i2 = (r / op.ne1) % op.ne2, i3 = r / (op.ne1 * op.ne2);
+    const float2 t = op.cs[i2 * op.npairs + j];
+    const float *src = (const float *)(op.x + i3 * op.nbx3 + i2 * op.nbx2 + i1 * op.nbx1) + 2 * j;
+    float *out = (float *)(op.d + i3 * op.nbd3 + i2 * op.nbd2 + i1 * op.nbd1) + 2 * j;
+    const float x0 = src[0], x1 = src[1];
+    const float y0 = x0 * t.x - x1 * t.y;
+    const float y1 = x0 * t.y + x1 * t.x;
+    out[0] = y0;
+    out[1] = y1;
+    if (op.c) {
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int64_t i = 2 * j + e + op.ne0 * (i1 + op.ne1 * i2);
+            const int64_t i12 = i / (op.ne10 * op.ne11), i11 = (i / op.ne10) % op.ne11, i10 = i % op.ne10;
+            char *dst = op.c + i10 * op.nb10 + i11 * op.nb11 + i12 * op.nb12;
+            const float v = e ? y1 : y0;
+            if (op.f16)
+                *(uint16_t *)dst = f2h_bits(v);
+            else
+                *(float *)dst = v;
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------- f16 x f32 mul_mat
 // dst[i2][i1][i0] = ggml_vec_dot_f16(K, src0[i2][i0][:], fp16(src1[i2][i1][:])), src0 rows f16
 // (nb00 = 2), src1 rows f32 (nb10 = 4), arbitrary row/channel strides (the permuted K and the
@@ -659,6 +715,20 @@ hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne
     else
         hipLaunchKernelGGL(k_cpy_f32<false>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, n, ne00, ne01,
                            nb00, nb01, nb02, ne10, ne11, nb10, nb11, nb12);
+    return hipGetLastError();
+}
+
+hipError_t op_elem_batch(const ElemBatch &b, hipStream_t s) {
+    if (b.nops < 1 || b.nops > ELEM_MAX) return hipErrorInvalidValue;
+    ElemBatch bb = b;
+    unsigned total = 0;
+    for (int q = 0; q < bb.nops; q++) {
+        bb.block_begin[q] = total;
+        total += blocks(bb.op[q].n);
+    }
+    for (int q = bb.nops; q < ELEM_MAX; q++) bb.block_begin[q] = total;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_elem_batch, dim3(total), dim3(TPB), 0, s, bb);
     return hipGetLastError();
 }
 

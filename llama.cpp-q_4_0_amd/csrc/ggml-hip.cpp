@@ -935,8 +935,8 @@ bool try_fuse(tensor *t) {
 }
 
 // ---- sibling q4_0 GEMVs.  ggml visits a LLaMA layer depth first, so the mul_mats that share an
-// input are not adjacent (wk, rope K, cpy K, wv, cpy V, wq, ...; w1, silu, w3).  A decode q4_0
-// mul_mat (one token, device operands) opens a group; the device-only nodes that follow are held
+// input are not adjacent (wk, rope K, cpy K, wv, cpy V, wq, ...; w1, silu, w3).  A q4_0 mul_mat
+// with device operands opens a group; the device-only nodes that follow are held
 // behind it ("after" nodes, replayed in arrival order once the group has run), and a later q4_0
 // mul_mat with the same src1 joins the group when running it ahead of the held nodes is safe: it
 // reads none of their outputs and its output overlaps none of their operands.  The group is one
@@ -978,7 +978,7 @@ bool group_mm_ok(const tensor *t) {
     if (!b || t->backend != gabi::BACKEND_GPU || !t->extra || b->backend != gabi::BACKEND_GPU || !b->extra || !a->extra)
         return false;
     if (!supported_mul_mat(a, b, t) || !is_contiguous(a) || !is_contiguous(b) || !is_contiguous(t)) return false;
-    if (b->ne[1] != 1 || b->ne[2] != 1 || b->ne[3] != 1 || a->ne[2] != 1 || a->ne[3] != 1) return false;
+    if (b->ne[1] < 1 || b->ne[2] != 1 || b->ne[3] != 1 || a->ne[2] != 1 || a->ne[3] != 1) return false;
     if (a->backend == gabi::BACKEND_GPU) return true;
     return a->backend == gabi::BACKEND_GPU_SPLIT && main_device_only_split(a->ne[1]);
 }
@@ -1149,8 +1149,8 @@ void flush_group() {
             count_node(g.mm[i]);
         }
         HIP_FATAL(hipSetDevice(g_main_device));
-        const int rc = ggml_hip_mul_mat_q4_0_multi(g.n, w, m, g.mm[0]->src0->ne[0], (const float *)dptr(g.mm[0]->src1), 1, y,
-                                                   g_dev[g_main_device].stream);
+        const int rc = ggml_hip_mul_mat_q4_0_multi(g.n, w, m, g.mm[0]->src0->ne[0], (const float *)dptr(g.mm[0]->src1),
+                                                   g.mm[0]->src1->ne[1], y, g_dev[g_main_device].stream);
         if (rc != GGML_HIP_OK) op_abort(g.mm[0], "sibling q4_0 GEMV group failed");
         g_fused[6].fetch_add(1, std::memory_order_relaxed);
     }

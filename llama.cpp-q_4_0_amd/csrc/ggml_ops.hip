@@ -370,31 +370,32 @@ __global__ __launch_bounds__(TPB, 2) void k_mul_mat_f16_f32_tiled(const char *s0
 #pragma unroll
             for (int e = 0; e < 8; e++) acc[r][c][e] = 0.0f;
 
-    for (int k0 = 0; k0 < np; k0 += FKC) {
+    // stages cover [0, K): the tail e >= np lies in the last one and is read back from LDS below
+    for (int k0 = 0; k0 < K; k0 += FKC) {
         const int k = k0 + se;
         uint4 xv[2], yv[2];
 #pragma unroll
         for (int q = 0; q < 2; q++) {
             uint32_t xw[4], yw[4];
-            if (k + 8 <= np && ((uintptr_t)(xg[q] + k) & 15) == 0) {
+            if (k + 8 <= K && ((uintptr_t)(xg[q] + k) & 15) == 0) {
                 const uint4 v = *reinterpret_cast<const uint4 *>(xg[q] + k);
                 xw[0] = v.x, xw[1] = v.y, xw[2] = v.z, xw[3] = v.w;
             } else {
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
-                    const uint32_t lo = k + 2 * w < np ? xg[q][k + 2 * w] : 0u;
-                    const uint32_t hi = k + 2 * w + 1 < np ? xg[q][k + 2 * w + 1] : 0u;
+                    const uint32_t lo = k + 2 * w < K ? xg[q][k + 2 * w] : 0u;
+                    const uint32_t hi = k + 2 * w + 1 < K ? xg[q][k + 2 * w + 1] : 0u;
                     xw[w] = lo | (hi << 16);
                 }
             }
             float yf[8];
-            if (k + 8 <= np && ((uintptr_t)(yg[q] + k) & 15) == 0) {
+            if (k + 8 <= K && ((uintptr_t)(yg[q] + k) & 15) == 0) {
                 const float4 a = *reinterpret_cast<const float4 *>(yg[q] + k);
                 const float4 b = *reinterpret_cast<const float4 *>(yg[q] + k + 4);
                 yf[0] = a.x, yf[1] = a.y, yf[2] = a.z, yf[3] = a.w, yf[4] = b.x, yf[5] = b.y, yf[6] = b.z, yf[7] = b.w;
             } else {
 #pragma unroll
-                for (int e = 0; e < 8; e++) yf[e] = k + e < np ? yg[q][k + e] : 0.0f;
+                for (int e = 0; e < 8; e++) yf[e] = k + e < K ? yg[q][k + e] : 0.0f;
             }
 #pragma unroll
             for (int w = 0; w < 4; w++) yw[w] = (uint32_t)f2h_bits(yf[2 * w]) | ((uint32_t)f2h_bits(yf[2 * w + 1]) << 16);
@@ -408,7 +409,8 @@ __global__ __launch_bounds__(TPB, 2) void k_mul_mat_f16_f32_tiled(const char *s0
             *reinterpret_cast<uint4 *>(ys + (sr + 16 * q) * FLD + se) = yv[q];
         }
         __syncthreads();
-        const int steps = (np - k0) / 32 < FKC / 32 ? (np - k0) / 32 : FKC / 32;
+        const int rem = np - k0;
+        const int steps = rem <= 0 ? 0 : (rem / 32 < FKC / 32 ? rem / 32 : FKC / 32);
         for (int s = 0; s < steps; s++) {
             const int off = 32 * s + 8 * j;
             uint4 xr[FB];
@@ -451,10 +453,12 @@ __global__ __launch_bounds__(TPB, 2) void k_mul_mat_f16_f32_tiled(const char *s0
             const float res = (t0 + t1) + (t2 + t3);
             const int64_t i0 = r0 + br + r, i1 = c0 + bc + c;
             if (i0 < ne01 && i1 < ne11) {
-                const uint16_t *xr = (const uint16_t *)(x0 + i0 * nb01);
-                const float *yr = (const float *)(y0 + i1 * nb11);
+                // the tail from the last stage in LDS (src1 already rounded to fp16 there)
+                const int kl = K > 0 ? ((K - 1) / FKC) * FKC : 0;
+                const uint16_t *xt = xs + (br + r) * FLD - kl;
+                const uint16_t *yt = ys + (bc + c) * FLD - kl;
                 double sum = (double)res;
-                for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(yr[e])));
+                for (int e = np; e < K; e++) sum += (double)(h2f_bits(xt[e]) * h2f_bits(yt[e]));
                 d[(i2 * ne11 + i1) * ne01 + i0] = (float)sum;
                 if (merged) merged[(i1 * ne02 + i2) * ne01 + i0] = (float)sum;
             }

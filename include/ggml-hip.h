@@ -217,7 +217,8 @@ const char *ggml_hip_version(void);
    counts[137 + k] = fused launches of chain k (0 add/rms_norm/mul, 1 scale/diag_mask_inf/soft_max,
    2 silu/mul, 3 rope/cpy, 4 f16 mul_mat/permute/cpy, 5 q4_0 mul_mat run while a silu is pending,
    6 sibling q4_0 GEMVs sharing src1 run as one group: wq|wk|wv, w1|w3, 7 independent rope /
-   rope->cpy / cpy nodes held behind a group run as one launch) */
+   rope->cpy / cpy nodes held behind a group run as one launch, 8 decode scale -> diag_mask_inf ->
+   soft_max -> KQV -> merged copy as one launch) */
 int    ggml_hip_debug_op_stats(int64_t *counts, int n, int reset);
 /* debug: the attention's f16 x f32 mul_mat on device pointers (synchronous); tiled = 0 one 32-lane
    group per output, 1 the LDS-tiled kernel, -1 the backend's choice (bit-identical either way) */

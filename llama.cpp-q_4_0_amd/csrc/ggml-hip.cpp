@@ -593,8 +593,9 @@ std::atomic<int64_t> g_host_ns{0};                     // host time inside the t
 std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of the node that arrived
 // fused launches by chain: add/rms_norm/mul, scale/mask/soft_max, silu/mul, rope/cpy, KQV/merge cpy,
 // q4_0 mul_mat run under a pending silu, sibling q4_0 GEMVs (wq|wk|wv, w1|w3) run as one group,
-// independent rope / rope->cpy / cpy nodes held behind a group run as one launch
-constexpr int N_FUSED = 8;
+// independent rope / rope->cpy / cpy nodes held behind a group run as one launch, the decode
+// soft_max chain with its KQV and merged copy as one launch
+constexpr int N_FUSED = 9;
 std::atomic<int64_t> g_fused[N_FUSED];
 
 // fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)
@@ -784,7 +785,7 @@ bool fuse_enabled() {
 
 struct Pending {
     int n = 0;
-    tensor *node[2] = {nullptr, nullptr};
+    tensor *node[4] = {};
 };
 Pending g_pend;
 void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst);
@@ -823,10 +824,35 @@ bool deferrable(const tensor *t) {
 
 void count_node(const tensor *t) { g_op_count[t->op].fetch_add(1, std::memory_order_relaxed); }
 
+// the pending scale -> diag_mask_inf -> soft_max chain (nodes 0..2 of p) in one launch
+void launch_softmax_chain(const Pending &p) {
+    const tensor *sc = p.node[0], *mk = p.node[1], *t = p.node[2];
+    const int id = g_main_device;
+    hipStream_t s = g_dev[id].stream;
+    const OpTables &tb = op_tables(id, s);
+    float *d = (float *)dptr(t);
+    HIP_FATAL(hipSetDevice(id));
+    HIP_FATAL(ghip::op_scale_mask_soft_max_f32((const float *)dptr(sc->src0), dptr(sc) == (char *)d ? nullptr : (float *)dptr(sc),
+                                               dptr(mk) == (char *)d ? nullptr : (float *)dptr(mk), d,
+                                               *(const float *)sc->src1->data, t->ne[0], gabi::nrows(t), t->ne[1],
+                                               ((const int32_t *)mk->src1->data)[0], tb.exp, s));
+    for (int i = 0; i < 3; i++) count_node(p.node[i]);
+    g_fused[1].fetch_add(1, std::memory_order_relaxed);
+}
+bool softmax_chain(const Pending &p) {
+    return p.n >= 3 && p.node[0]->op == gabi::OP_SCALE && p.node[1]->op == gabi::OP_DIAG_MASK_INF &&
+           p.node[2]->op == gabi::OP_SOFT_MAX;
+}
+
 void flush_pending() {
     const Pending p = g_pend;
     g_pend = Pending{};
-    for (int i = 0; i < p.n; i++) run_device_op(p.node[i]);
+    int i = 0;
+    if (softmax_chain(p)) {             // held lazily for a possible KQV: complete it as one launch
+        launch_softmax_chain(p);
+        i = 3;
+    }
+    for (; i < p.n; i++) run_device_op(p.node[i]);
 }
 
 // t arrives while a chain is pending: extend the chain, complete it in one launch, or let a q4_0
@@ -863,23 +889,46 @@ bool try_fuse(tensor *t) {
         p = Pending{};
         return true;
     }
-    // scale -> diag_mask_inf -> soft_max: complete
+    // scale -> diag_mask_inf -> soft_max: held (completed as one launch by flush_pending, or with
+    // the KQV that follows at decode)
     if (p.n == 2 && p.node[0]->op == gabi::OP_SCALE && last->op == gabi::OP_DIAG_MASK_INF && t->op == gabi::OP_SOFT_MAX &&
         t->src0 == last && dev_f32(t) && same_shape(t, last)) {
-        const tensor *sc = p.node[0];
-        const OpTables &tb = op_tables(id, s);
-        float *d = (float *)dptr(t);
-        HIP_FATAL(hipSetDevice(id));
-        HIP_FATAL(ghip::op_scale_mask_soft_max_f32((const float *)dptr(sc->src0),
-                                                   dptr(sc) == (char *)d ? nullptr : (float *)dptr(sc),
-                                                   dptr(last) == (char *)d ? nullptr : (float *)dptr(last), d,
-                                                   *(const float *)sc->src1->data, t->ne[0], gabi::nrows(t), t->ne[1],
-                                                   ((const int32_t *)last->src1->data)[0], tb.exp, s));
-        for (int i = 0; i < p.n; i++) count_node(p.node[i]);
-        count_node(t);
-        g_fused[1].fetch_add(1, std::memory_order_relaxed);
-        p = Pending{};
+        p.node[p.n++] = t;
         return true;
+    }
+    // soft_max chain -> KQV (f16 V^T . softmax, one query row per head): extend
+    if (p.n == 3 && softmax_chain(p) && t->op == gabi::OP_MUL_MAT && t->src1 == last && t->src0 &&
+        t->src0->type == gabi::TYPE_F16 && t->src0->backend == gabi::BACKEND_GPU && t->src0->extra &&
+        t->src0->nb[0] == 2 && t->src0->ne[3] == 1 && last->ne[1] == 1 && last->ne[3] == 1 &&
+        t->src0->ne[0] == last->ne[0] && t->src0->ne[2] == last->ne[2] && last->ne[0] <= 16384 && dev_f32(t) &&
+        t->ne[1] == 1 && t->ne[0] == t->src0->ne[1] && dev_f32(p.node[0]->src0)) {
+        p.node[p.n++] = t;
+        return true;
+    }
+    // soft_max chain -> KQV -> cpy(permute(KQV)) (the merged heads): complete as one launch
+    if (p.n == 4 && softmax_chain(p) && t->op == gabi::OP_CPY && t->src0 && t->src0->op == gabi::OP_PERMUTE &&
+        t->src0->src0 == last) {
+        const tensor *m = t->src0, *cb = t->src1;
+        if (m->ne[0] == last->ne[0] && m->ne[1] == last->ne[2] && m->ne[2] == last->ne[1] && m->ne[3] == 1 &&
+            m->nb[0] == 4 && m->nb[1] == last->nb[2] && m->nb[2] == last->nb[1] && dev_f32(cb) &&
+            gabi::nbytes(cb) == gabi::nbytes(last) && !overlaps(cb, last) && !overlaps(cb, last->src0) &&
+            !overlaps(cb, p.node[2]) && !overlaps(cb, p.node[0]->src0)) {
+            const tensor *sc = p.node[0], *mk = p.node[1], *sm = p.node[2], *kqv = last, *vv = kqv->src0;
+            const char *kq = dptr(sc->src0);
+            // stores into the buffer the workgroups read (the in-place chain) are skipped: see
+            // k_softmax_kqv; no node reads them, KQV consumes the softmax inside the launch
+            auto out = [&](const tensor *x) { return overlaps(x, sc->src0) ? nullptr : (float *)dptr(x); };
+            const OpTables &tb = op_tables(id, s);
+            HIP_FATAL(hipSetDevice(id));
+            HIP_FATAL(ghip::op_softmax_kqv((const float *)kq, out(sc), out(mk), out(sm), *(const float *)sc->src1->data,
+                                           ((const int32_t *)mk->src1->data)[0], tb.exp, sm->ne[0], sm->ne[2], dptr(vv),
+                                           vv->nb[1], vv->nb[2], vv->ne[1], (float *)dptr(kqv), (float *)dptr(cb), s));
+            for (int i = 0; i < p.n; i++) count_node(p.node[i]);
+            count_node(t);
+            g_fused[8].fetch_add(1, std::memory_order_relaxed);
+            p = Pending{};
+            return true;
+        }
     }
     // silu -> mul(silu, b): complete
     if (p.n == 1 && last->op == gabi::OP_SILU && t->op == gabi::OP_MUL && t->src0 == last && dev_f32(t) &&

@@ -66,6 +66,12 @@ hipError_t op_add_rms_norm_mul_f32(const float *a, const float *b, float *sum, f
 hipError_t op_scale_mask_soft_max_f32(const float *x, float *scaled, float *masked, float *d, float v, int64_t ncols,
                                       int64_t nrows, int64_t rows_per_channel, int n_past, const uint16_t *table,
                                       hipStream_t s);
+// decode attention's second half, one query row per head: scaled/masked/sm = scale -> diag_mask_inf
+// -> soft_max of kq's rows (as op_scale_mask_soft_max_f32), kqv (+ merged) = V.fp16(sm) (as
+// op_mul_mat_f16_f32 with N = 1); V^T rows of nkv f16 at nb01v, heads at nb02v; nullptr = not stored
+hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm, float v, int n_past,
+                          const uint16_t *table, int64_t nkv, int64_t nhead, const void *vs, int64_t nb01v, int64_t nb02v,
+                          int64_t nout, float *kqv, float *merged, hipStream_t s);
 // u = silu(a) -> out = u * b (same shape)
 hipError_t op_silu_mul_f32(const float *a, const float *b, float *u, float *out, int64_t n, const uint16_t *table,
                            hipStream_t s);

@@ -531,6 +531,85 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max(const float *x, flo
     for (int64_t i = lane; i < ncols; i += 64) d[o + i] = d[o + i] * inv;
 }
 
+// Decode attention's second half: scale -> diag_mask_inf -> soft_max of each head's KQ row (one
+// query row per head) and KQV = V.fp16(softmax) with its merged copy.  SM_SPLIT workgroups per head
+// each recompute the row's softmax (max, the exp table, the double sum of exactly representable
+// terms: order-free, so every workgroup gets the same bits as k_scale_mask_soft_max) and take
+// 32 of the head's KQV outputs, 32 lanes per output as k_mul_mat_f16_f32 does.  Workgroup 0 of a
+// head stores the softmax row (and scaled / masked) unless nullptr: the caller passes nullptr for a
+// buffer that aliases kq (the in-place chain), which the other workgroups are still reading.
+constexpr int SM_THREADS = 1024, SM_OUT = SM_THREADS / 32;
+__global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm,
+                                                            float v, int n_past, const uint16_t *table, int64_t nkv,
+                                                            const char *vs, int64_t nb01v, int64_t nb02v, int64_t nout,
+                                                            int splits, float *kqv, float *merged) {
+    extern __shared__ float row[];                     // [nkv]
+    __shared__ float redf[SM_THREADS / 64];
+    __shared__ double redd[SM_THREADS / 64];
+    const int64_t i2 = blockIdx.x / splits;
+    const int part = blockIdx.x % splits;
+    const int tid = threadIdx.x, g = tid >> 5, l = tid & 31, wave = tid >> 6, lane = tid & 63;
+    const int64_t o = i2 * nkv;
+    const bool store = part == 0;
+    float mx = -INFINITY;
+    for (int64_t i = tid; i < nkv; i += SM_THREADS) mx = fmaxf(mx, i > n_past ? -INFINITY : kq[o + i] * v);
+    mx = wave_max_f(mx);
+    if (lane == 0) redf[wave] = mx;
+    __syncthreads();
+    mx = redf[0];
+    for (int w = 1; w < SM_THREADS / 64; w++) mx = fmaxf(mx, redf[w]);
+    double ssum = 0.0;
+    for (int64_t i = tid; i < nkv; i += SM_THREADS) {
+        const float sv = kq[o + i] * v;
+        const float m = i > n_past ? -INFINITY : sv;
+        float e = 0.0f;
+        if (m != -INFINITY) {
+            e = h2f_bits(table[f2h_bits(m - mx)]);
+            ssum += (double)e;
+        }
+        row[i] = e;
+        if (store) {
+            if (scaled) scaled[o + i] = sv;
+            if (masked) masked[o + i] = m;
+        }
+    }
+    ssum = wave_sum_d(ssum);
+    if (lane == 0) redd[wave] = ssum;
+    __syncthreads();
+    ssum = 0.0;
+    for (int w = 0; w < SM_THREADS / 64; w++) ssum += redd[w];
+    const float inv = (float)(1.0 / ssum);
+    for (int64_t i = tid; i < nkv; i += SM_THREADS) {
+        const float pv = row[i] * inv;
+        row[i] = pv;
+        if (store && sm) sm[o + i] = pv;
+    }
+    __syncthreads();
+    // KQV output r of this head: V^T row r (nkv f16) . fp16(softmax row)
+    const int64_t r = (int64_t)part * SM_OUT + g;
+    if (r >= nout) return;
+    const uint16_t *xr = (const uint16_t *)(vs + i2 * nb02v + r * nb01v);
+    const int K = (int)nkv;
+    const int np = K & ~31;
+    float acc = 0.0f;
+    for (int e = l; e < np; e += 32) acc = fmaf(h2f_bits(xr[e]), h2f_bits(f2h_bits(row[e])), acc);
+    const float p16 = __shfl_xor(acc, 16, 32);
+    const float a = acc + p16;
+    const float p8 = __shfl_xor(a, 8, 32);
+    const float c = a + p8;
+    const float c4 = __shfl_xor(c, 4, 32);
+    const float t0 = c + c4;
+    const float t01 = t0 + __shfl_xor(t0, 1, 32);
+    const float t23 = __shfl(t01, 2, 32);
+    const float res = t01 + t23;
+    if (l == 0) {
+        double sum = (double)res;
+        for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(row[e])));
+        kqv[i2 * nout + r] = (float)sum;
+        if (merged) merged[i2 * nout + r] = (float)sum;
+    }
+}
+
 // The same [add ->] rms_norm [-> mul] with one 1024-thread workgroup per row: every thread loads
 // its float4 pieces of the row at once (up to NV per thread, held in registers), the double sum is
 // reduced by shuffles and LDS, and the row is written from the registers.  One wave per row walks
@@ -622,6 +701,16 @@ hipError_t op_scale_mask_soft_max_f32(const float *x, float *scaled, float *mask
     if (nrows <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_scale_mask_soft_max, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, scaled, masked, d, v,
                        ncols, nrows, rows_per_channel, n_past, table);
+    return hipGetLastError();
+}
+
+hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm, float v, int n_past,
+                          const uint16_t *table, int64_t nkv, int64_t nhead, const void *vs, int64_t nb01v, int64_t nb02v,
+                          int64_t nout, float *kqv, float *merged, hipStream_t s) {
+    if (nhead <= 0 || nkv <= 0 || nout <= 0) return hipSuccess;
+    const int splits = (int)((nout + SM_OUT - 1) / SM_OUT);
+    hipLaunchKernelGGL(k_softmax_kqv, dim3((unsigned)(nhead * splits)), dim3(SM_THREADS), (size_t)nkv * 4, s, kq, scaled,
+                       masked, sm, v, n_past, table, nkv, (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged);
     return hipGetLastError();
 }
 

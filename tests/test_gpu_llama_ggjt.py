@@ -31,7 +31,7 @@ pytestmark = [pytest.mark.gpu,
 OPS = json.load(open(os.path.join(GOLD, "ggml_op_enum.json")))
 
 
-N_FUSED = 8   # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
+N_FUSED = 9   # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
 
 
 def op_stats(L, reset=True, fused=False):
@@ -156,7 +156,10 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode
     # under a pending silu, is what the prompt eval's unfused-group path leaves)
     evals = n_decode + 1
     if fuse:
-        assert (fused[[0, 1, 2, 4]] >= evals * hp["n_layer"]).all(), fused
+        assert (fused[[0, 2]] >= evals * hp["n_layer"]).all(), fused
+        # scale/mask/soft_max and the KQV merge: alone (prompt) or as the decode softmax+KQV launch
+        assert fused[1] + fused[8] >= evals * hp["n_layer"] and fused[4] + fused[8] >= evals * hp["n_layer"], fused
+        assert fused[8] >= n_decode * hp["n_layer"], fused
         assert fused[3] + fused[7] >= evals * hp["n_layer"], fused   # rope->cpy alone or in a batch
         assert fused[6] >= 2 * n_decode * hp["n_layer"], fused
         assert fused[7] >= n_decode * hp["n_layer"], fused      # rope K->cache, V->cache, rope Q

@@ -165,3 +165,36 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode
         assert fused[7] >= n_decode * hp["n_layer"], fused      # rope K->cache, V->cache, rope Q
     else:
         assert (fused == 0).all(), fused
+
+
+@pytest.mark.parametrize("hp,n_prompt,n_decode", [(HP128, 40, 60), (G.HP, 8, 40)], ids=["head128", "head64"])
+def test_fast_mode_fusion_bitwise_vs_unfused(tmp_path, hp, n_prompt, n_decode):
+    """Fast kernels at full offload: every launch fusion (the chains, the sibling GEMV groups, the
+    rope/cpy batch, soft_max+KQV) gives the same logits bit for bit as one launch per node."""
+    L = ggml_hip.load()
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp, hp=hp)
+    nv = hp["n_vocab"]
+    lib = ctypes.CDLL(HIP_LIB)
+    lib.refllama_bench.restype = ctypes.c_int
+    lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    L.ggml_hip_debug_set_fuse.argtypes = [ctypes.c_int]
+    prev = L.ggml_hip_get_exact()
+    ggml_hip.check(L.ggml_hip_set_exact(0), "set_exact")
+    out = {}
+    try:
+        for fuse in (1, 0):
+            ggml_hip.check(L.ggml_hip_debug_set_fuse(fuse), "set_fuse")
+            op_stats(L)
+            lg = np.zeros(nv, np.float32)
+            res = np.zeros(3, np.float64)
+            assert lib.refllama_bench(mp.encode(), n_prompt, n_decode, 1, 99, 1024, 1, res.ctypes.data, lg.ctypes.data) == nv
+            out[fuse] = (lg, op_stats(L, fused=True)[1])
+    finally:
+        L.ggml_hip_set_exact(prev)
+        L.ggml_hip_debug_set_fuse(1)
+    assert np.isfinite(out[1][0]).all()
+    assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
+    fused = out[1][1]
+    assert fused[6] >= 2 * n_decode * hp["n_layer"] and fused[8] >= n_decode * hp["n_layer"], fused
+    assert (out[0][1] == 0).all()

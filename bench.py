@@ -59,15 +59,37 @@ def log(*a):
 
 # ---------------------------------------------------------------------------------------------
 def setup_dist(n_gpus):
-    """torchrun env -> (rank, world, local_rank, dist module or None)."""
+    """torchrun env -> (rank, world, local_rank).  No torch in this process: torch bundles its own
+    libamdhip64 / librccl, and a second HIP runtime next to /opt/rocm's (which libggml_hip.so is
+    built against) corrupts the process; ranks talk through RCCL only (comm_allreduce_host)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or n_gpus > 1:
-        import torch.distributed as dist
-        rank = int(os.environ["RANK"])
-        local = int(os.environ.get("LOCAL_RANK", rank))
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        return rank, world, local, dist
-    return 0, 1, 0, None
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if n_gpus > 1 and world == 1:
+        log(f"--gpus {n_gpus} without a launcher: running 1 rank (use torch.distributed.run, see bench doc)")
+    return rank, world, local
+
+
+def exchange_unique_id(gh, L, rank, world):
+    """RCCL unique id from rank 0 to the other ranks of this node through a file named after the
+    launcher (torchrun's agent is every worker's parent) and its rendezvous port."""
+    path = os.environ.get("GGML_HIP_UID_FILE") or os.path.join(
+        "/tmp", f"ggml_hip_uid_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}")
+    uid = ctypes.create_string_buffer(128)
+    if rank == 0:
+        gh.check(L.ggml_hip_comm_unique_id(uid))
+        with open(path + ".tmp", "wb") as f:
+            f.write(uid.raw)
+        os.replace(path + ".tmp", path)
+    elif world > 1:
+        t0 = time.time()
+        while not os.path.exists(path):
+            if time.time() - t0 > 300:
+                raise SystemExit(f"rank {rank}: no RCCL unique id at {path}")
+            time.sleep(0.02)
+        time.sleep(0.05)
+        uid = ctypes.create_string_buffer(open(path, "rb").read(), 128)
+    return uid, path
 
 
 class Stack:
@@ -118,9 +140,9 @@ def main():
                     help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
     args = ap.parse_args()
 
-    rank, world, local, dist = setup_dist(args.gpus)
     import ggml_hip as gh
-    L = gh.load()
+    L = gh.load()                            # /opt/rocm HIP + RCCL (no torch in this process)
+    rank, world, local = setup_dist(args.gpus)
     ndev = L.ggml_hip_device_count()
     if ndev < 1:
         raise SystemExit("no HIP device")
@@ -129,15 +151,22 @@ def main():
 
     comm = None
     if world > 1 or args.force_split:
-        uid = ctypes.create_string_buffer(128)
-        if rank == 0:
-            gh.check(L.ggml_hip_comm_unique_id(uid))
-        if dist is not None:
-            obj = [uid.raw if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            uid = ctypes.create_string_buffer(obj[0], 128)
+        uid, uid_path = exchange_unique_id(gh, L, rank, world)
         comm = ctypes.c_void_p()
         gh.check(L.ggml_hip_comm_init(ctypes.byref(comm), world, rank, uid), "comm_init")
+        if rank == 0 and world > 1:
+            try:
+                os.remove(uid_path)      # every rank has joined (comm init is collective)
+            except OSError:
+                pass
+
+    def allreduce(vals, op):
+        """sum (0) / max (1) / min (2) of host doubles over the ranks (RCCL; also a barrier)"""
+        if comm is None:
+            return list(vals)
+        buf = (ctypes.c_double * len(vals))(*vals)
+        gh.check(L.ggml_hip_comm_allreduce_host(comm, buf, len(vals), op), "allreduce")
+        return list(buf)
 
     t0 = time.time()
     stack = Stack(gh, L, rank, world, args.layers)
@@ -164,7 +193,7 @@ def main():
         for row in stack.mats:
             for g in groups:
                 if len(g) == 1 or not batch:
-                    out.append(("one" if use_comm else "local", tuple(row[g[0]]) + (yb[g[0]],)))
+                    out.append(("one" if use_comm else "local", tuple(row[g[0]]) + (yb[g[0]], ysplit[g[0]])))
                 elif not use_comm:
                     n = len(g)
                     wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
@@ -192,14 +221,14 @@ def main():
                 n, wp, mt, rp, K, yp = a
                 gh.check(L.ggml_hip_mul_mat_q4_0_split_multi(comm, n, wp, mt, rp, K, xs[K].ptr, 1, yp, stream))
                 continue
-            name, K, M, m_loc, buf, rb, ylocal = a
+            name, K, M, m_loc, buf, rb, ylocal, yfull = a
             if kind == "local":      # this rank's slice only, no collective
                 gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, 1, ylocal.ptr, m_loc, 0, stream))
             elif comm is None:
                 gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, M, xs[K].ptr, 1, ys[M].ptr, M, 0, stream))
             else:
                 gh.check(L.ggml_hip_mul_mat_q4_0_split(comm, buf.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
-                                                       xs[K].ptr, 1, ys[M].ptr, stream))
+                                                       xs[K].ptr, 1, yfull.ptr, stream))
 
     graph = None
     if not args.eager:
@@ -217,8 +246,7 @@ def main():
 
     def barrier():
         gh.check(L.ggml_hip_device_synchronize())
-        if dist is not None:
-            dist.barrier()
+        allreduce([0.0], 0)
 
     for _ in range(args.warmup):
         run_step()
@@ -228,11 +256,7 @@ def main():
         run_step()
     barrier()
     elapsed = time.perf_counter() - t_start
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = allreduce([elapsed], 1)[0]     # max over ranks
     ms_per_step = elapsed / args.steps * 1e3
     tok_s = args.steps / elapsed * 32 / args.layers if args.layers else 0.0   # per full 32-layer token
 
@@ -265,13 +289,15 @@ def main():
             g2.launch()
         barrier()
         el = time.perf_counter() - t0
-        if dist is not None:
-            import torch
-            t = torch.tensor([el], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
+        el = allreduce([el], 1)[0]
         result["config"]["compute_only_tok_s"] = round(args.steps / el * 32 / args.layers, 2)
         result["config"]["collective_us_per_token"] = round((elapsed - el) / args.steps * 1e6 * 32 / args.layers, 1)
+
+    if comm is not None:
+        result["config"]["split_check"] = split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream)
+        if not all(result["config"]["split_check"][k] for k in ("own_rows_bitwise", "gather_checksum")):
+            log(f"[rank {rank}] SPLIT CHECK FAILED: {result['config']['split_check']}")
+    result["config"]["runtime_libs"] = gh.mapped_runtime_libs()
 
     if rank == 0 and world == 1 and comm is None:
         result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
@@ -288,11 +314,37 @@ def main():
         print(json.dumps(result), flush=True)
     if comm is not None:
         L.ggml_hip_comm_destroy(comm)
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 # ---------------------------------------------------------------------------------------------
+def _bits_checksum(a, offset):
+    """order-independent exact checksum of float32 values at global positions offset + i"""
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64).ravel()
+    pos = np.arange(offset, offset + u.size, dtype=np.uint64)
+    return int(np.sum((u + np.uint64(1)) * (pos * np.uint64(2654435761) + np.uint64(97)), dtype=np.uint64))
+
+
+def split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream):
+    """Self-check of the sharded run (after the timed region): the decode step leaves the last
+    layer's gathered outputs in ysplit and the local-only graph its slices in yb.  (1) this rank's
+    rows of every gathered y equal its own slice bitwise; (2) the exact checksum of every gathered y
+    equals the sum over ranks of the slice checksums (every rank's slice landed at its rows)."""
+    MOD = 1 << 44                            # sums of <= 256 ranks stay exact in a double
+    row = stack.mats[-1]
+    ok_own, mine, full = True, [], []
+    for i, (name, K, M, m_loc, buf, rb) in enumerate(row):
+        g = ysplit[i].download((M,), np.float32, stream=stream)
+        loc = yb[i].download((m_loc,), np.float32, stream=stream)
+        lo = int(rb[rank])
+        ok_own &= bool(np.array_equal(g[lo:lo + m_loc].view(np.uint32), loc.view(np.uint32)))
+        mine.append(float(_bits_checksum(loc, lo) % MOD))
+        full.append(_bits_checksum(g, 0) % MOD)
+    tot = allreduce(mine, 0)
+    ok_own = allreduce([1.0 if ok_own else 0.0], 2)[0] == 1.0
+    ok_sum = all((fu - int(tt)) % MOD == 0 for fu, tt in zip(full, tot))
+    return {"own_rows_bitwise": ok_own, "gather_checksum": ok_sum, "matrices": len(row)}
+
+
 def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
     """Dominant kernel = the decode GEMV (k_gemv_q4_0<1,...>).  For each launch position of a
     layer (fused wq|wk|wv, wo, fused w1|w3, w2) the 32 launches of that position (one per layer,
@@ -423,7 +475,7 @@ def run_launch(gh, L, kind, a, xs, stream):
         n, wp, mp, K, yp = a
         gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, 1, yp, stream))
     else:
-        name, K, M, m_loc, buf, rb, yb = a
+        name, K, M, m_loc, buf, rb, yb, _ = a
         gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, 1, yb.ptr, m_loc, 1, stream))
 
 

@@ -164,6 +164,16 @@ typedef struct ggml_hip_comm ggml_hip_comm;
 int ggml_hip_comm_unique_id(char out[GGML_HIP_UNIQUE_ID_BYTES]);
 int ggml_hip_comm_init(ggml_hip_comm **comm, int nranks, int rank, const char id[GGML_HIP_UNIQUE_ID_BYTES]);
 int ggml_hip_comm_destroy(ggml_hip_comm *comm);
+/* In-process loopback group (testing / single-process multi-device): creates nranks
+ * communicators comms[0..nranks-1] whose all-gather has ncclAllGather's semantics, for nranks
+ * host threads of this process that each drive one rank (rank r on devices[r], or all on the
+ * current device when devices is NULL; give each rank its own stream).  Every split entry point
+ * below runs the same code on either transport.  Destroy each comm with ggml_hip_comm_destroy. */
+int ggml_hip_comm_init_local(ggml_hip_comm **comms, int nranks, const int *devices);
+int ggml_hip_comm_rank(const ggml_hip_comm *comm, int *rank, int *nranks);
+/* All-reduce of n <= 64 host doubles in place (op 0 sum, 1 max, 2 min) over the comm; synchronous,
+ * so it is also a barrier (bench harness: max-over-ranks timing without a second runtime). */
+int ggml_hip_comm_allreduce_host(ggml_hip_comm *comm, double *vals, int n, int op);
 /* Row split of M rows over nranks by cumulative fractions (NULL = equal split), the same
  * rule as the reference's tensor_split (ggml-cuda.cu:1863-1882, 2361-2368).  row_begin has
  * nranks+1 entries. */
@@ -199,6 +209,8 @@ int    ggml_hip_memset(void *dst, int value, size_t size, void *stream);
 int    ggml_hip_stream_synchronize(void *stream);
 int    ggml_hip_device_synchronize(void);
 void  *ggml_hip_default_stream(void);          /* the backend's stream on the current device */
+void  *ggml_hip_stream_create(void);           /* a non-blocking stream on the current device */
+int    ggml_hip_stream_destroy(void *stream);  /* synchronizes, frees its mul_mat workspace */
 int    ggml_hip_fill_gaussian(float *dev_dst, int64_t n, uint64_t seed, float mean, float stdv, void *stream);
 /* timing and HIP-graph capture on a stream (bench harness; launch-bound decode chains) */
 void  *ggml_hip_event_create(void);

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -82,8 +83,12 @@ struct Device {
     size_t total_mem = 0;
     std::mutex mu;
     std::vector<PoolBuf> pool;           // free temporaries (first-fit best size)
-    void *ws = nullptr;                  // mul_mat workspace (q8_0 activations)
+    void *ws = nullptr;                  // mul_mat workspace (q8_0 activations) of `stream`
     size_t ws_size = 0;
+    // workspaces of other streams on this device (callers that run mul_mats on their own streams
+    // concurrently, e.g. the ranks of an in-process loopback group): one per stream, never shared
+    std::unordered_map<hipStream_t, PoolBuf> stream_ws;
+    hipEvent_t ev_a = nullptr, ev_b = nullptr;   // split mul_mat ordering between device streams
 };
 
 std::once_flag g_init_once;
@@ -117,6 +122,8 @@ void init_impl() {
     for (int id = 0; id < g_device_count; id++) {
         HIP_FATAL(hipSetDevice(id));
         HIP_FATAL(hipStreamCreateWithFlags(&g_dev[id].stream, hipStreamNonBlocking));
+        HIP_FATAL(hipEventCreateWithFlags(&g_dev[id].ev_a, hipEventDisableTiming));
+        HIP_FATAL(hipEventCreateWithFlags(&g_dev[id].ev_b, hipEventDisableTiming));
     }
     if (g_device_count > 0) HIP_FATAL(hipSetDevice(cur));
 }
@@ -168,21 +175,48 @@ size_t workspace_bytes(int64_t K, int64_t N) {
     return qs + (size_t)N * (K / QK) * 4;
 }
 
-int reserve_workspace(int id, size_t bytes) {
+int reserve_workspace(int id, size_t bytes, hipStream_t s = nullptr) {
     Device &d = g_dev[id];
     std::lock_guard<std::mutex> lk(d.mu);
-    if (d.ws_size >= bytes) return GGML_HIP_OK;
+    if (!s) s = d.stream;
+    void *&ws = s == d.stream ? d.ws : d.stream_ws[s].ptr;
+    size_t &ws_size = s == d.stream ? d.ws_size : d.stream_ws[s].size;
+    if (ws_size >= bytes) return GGML_HIP_OK;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(d.stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
+    if (hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
         return fail(GGML_HIP_ERR_INVALID, "workspace must be reserved before stream capture");
-    if (d.ws) {
+    if (ws) {
         HIP_RET(hipDeviceSynchronize());
-        HIP_RET(hipFree(d.ws));
-        d.ws = nullptr;
-        d.ws_size = 0;
+        HIP_RET(hipFree(ws));
+        ws = nullptr;
+        ws_size = 0;
     }
-    HIP_RET(hipMalloc(&d.ws, bytes));
-    d.ws_size = bytes;
+    HIP_RET(hipMalloc(&ws, bytes));
+    ws_size = bytes;
+    return GGML_HIP_OK;
+}
+
+// the workspace of stream s on device id (grown on demand outside capture)
+int stream_workspace(int id, hipStream_t s, size_t need, void **out) {
+    Device &d = g_dev[id];
+    {
+        std::lock_guard<std::mutex> lk(d.mu);
+        if (s == d.stream && d.ws_size >= need) {
+            *out = d.ws;
+            return GGML_HIP_OK;
+        }
+        if (s != d.stream) {
+            auto it = d.stream_ws.find(s);
+            if (it != d.stream_ws.end() && it->second.size >= need) {
+                *out = it->second.ptr;
+                return GGML_HIP_OK;
+            }
+        }
+    }
+    const int rc = reserve_workspace(id, need, s);
+    if (rc != GGML_HIP_OK) return rc;
+    std::lock_guard<std::mutex> lk(d.mu);
+    *out = s == d.stream ? d.ws : d.stream_ws[s].ptr;
     return GGML_HIP_OK;
 }
 
@@ -323,13 +357,11 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
         return GGML_HIP_OK;
     }
     if (algo < 2 || algo > 4) return fail(GGML_HIP_ERR_INVALID, "algo must be 0, 1, 2, 3 or 4");
-    const size_t need = workspace_bytes(K, N);
-    if (g_dev[id].ws_size < need) {
-        int rc = reserve_workspace(id, need);
-        if (rc != GGML_HIP_OK) return rc;
-    }
-    int8_t *qs = (int8_t *)g_dev[id].ws;
-    float *xd = (float *)((char *)g_dev[id].ws + ((size_t)(N * K + 255) & ~(size_t)255));
+    void *ws = nullptr;
+    const int wrc = stream_workspace(id, s, workspace_bytes(K, N), &ws);
+    if (wrc != GGML_HIP_OK) return wrc;
+    int8_t *qs = (int8_t *)ws;
+    float *xd = (float *)((char *)ws + ((size_t)(N * K + 255) & ~(size_t)255));
     if (!x_quantized) HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s));
     if (algo == 4)
         HIP_RET(ghip::mm_exact_q4_0(w, K, M, qs, xd, N, y, ldy, s));
@@ -1338,28 +1370,41 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
     const bool dst_dev = dst->backend == gabi::BACKEND_GPU;
     const size_t wrow = (size_t)(K / QK) * Q4B;
     const int saved = current_device();
+    const int main_id = g_main_device;
     uint64_t call_id;
     {
         std::lock_guard<std::mutex> lk(g_wc_mu);
         call_id = ++g_wc_clock;
     }
-
+    // Row split over devices (ggml_cuda_op, ggml-cuda.cu:2286-2567): every device's slice is
+    // enqueued before anything waits, so the devices run concurrently; the host synchronizes each
+    // device once at the end (the reference: main-device sync first, per-device sync last,
+    // 2348-2351 / 2546-2552).  Other devices start after the main stream's work that produced
+    // src1 (event); a non-main slice [N][rows] comes back with ONE contiguous peer copy into a
+    // main-device staging buffer and ONE 2-D copy into dst on the main stream (which waits for it).
+    if (split) {
+        HIP_FATAL(hipSetDevice(main_id));
+        HIP_FATAL(hipEventRecord(g_dev[main_id].ev_a, g_dev[main_id].stream));
+    }
+    std::vector<std::vector<std::pair<void *, size_t>>> tmps(g_device_count);
+    std::vector<bool> used(g_device_count, false);
+    bool need_sync = !dst_dev || split || !src0_dev;   // host dst, gathers, host weights (cache)
     for (int id = 0; id < g_device_count; id++) {
-        if (!split && id != g_main_device) continue;
+        if (!split && id != main_id) continue;
         int64_t lo = 0, hi = M;
         if (split) split_range(M, id, &lo, &hi);
         if (lo == hi) continue;
+        used[id] = true;
         const int64_t rows = hi - lo;
         HIP_FATAL(hipSetDevice(id));
         hipStream_t s = g_dev[id].stream;
-        std::vector<std::pair<void *, size_t>> tmp;
-        auto tmp_alloc = [&](size_t bytes) {
+        auto tmp_alloc = [&](int dev, size_t bytes) {
             size_t a = 0;
-            void *p = pool_malloc(id, bytes, &a);
-            tmp.push_back({p, a});
+            void *p = pool_malloc(dev, bytes, &a);
+            tmps[dev].push_back({p, a});
             return p;
         };
-        bool need_sync = !dst_dev || split || !src0_dev;   // host dst, gathers, host weights (cache)
+        if (split && id != main_id) HIP_FATAL(hipStreamWaitEvent(s, g_dev[main_id].ev_a, 0));
         for (int64_t b = 0; b < nbatch; b++) {
             // weights: resident slice, or upload the row slice (the reference re-uploads every
             // call too, ggml-cuda.cu:2496-2502)
@@ -1371,7 +1416,7 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
                 w = wcache_get(id, (const char *)src0->data + (size_t)b * src0->nb[2] + lo * wrow, rows * wrow, s,
                                call_id);
             } else {
-                void *p = tmp_alloc(rows * wrow);
+                void *p = tmp_alloc(id, rows * wrow);
                 HIP_FATAL(hipMemcpyAsync(p, (const char *)src0->data + (size_t)b * src0->nb[2] + lo * wrow, rows * wrow,
                                          hipMemcpyHostToDevice, s));
                 w = p;
@@ -1379,17 +1424,17 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
             // activations
             const float *x;
             const size_t xbytes = (size_t)N * K * 4;
-            if (src1_dev && id == g_main_device) {
+            if (src1_dev && id == main_id) {
                 x = (const float *)((const char *)((const ggml_tensor_extra_gpu *)src1->extra)->data_device[id] +
                                     (size_t)b * src1->nb[2]);
             } else if (src1_dev) {
-                void *p = tmp_alloc(xbytes);
-                const char *srcp = (const char *)((const ggml_tensor_extra_gpu *)src1->extra)->data_device[g_main_device] +
+                void *p = tmp_alloc(id, xbytes);
+                const char *srcp = (const char *)((const ggml_tensor_extra_gpu *)src1->extra)->data_device[main_id] +
                                    (size_t)b * src1->nb[2];
-                HIP_FATAL(hipMemcpyPeerAsync(p, id, srcp, g_main_device, xbytes, s));
+                HIP_FATAL(hipMemcpyPeerAsync(p, id, srcp, main_id, xbytes, s));
                 x = (const float *)p;
             } else {
-                void *p = tmp_alloc(xbytes);
+                void *p = tmp_alloc(id, xbytes);
                 HIP_FATAL(hipMemcpyAsync(p, (const char *)src1->data + (size_t)b * src1->nb[2], xbytes,
                                          hipMemcpyHostToDevice, s));
                 x = (const float *)p;
@@ -1397,39 +1442,51 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
             // output
             float *y;
             int64_t ldy;
-            const bool direct = dst_dev && !split && id == g_main_device;
+            const bool direct = dst_dev && !split && id == main_id;
             if (direct) {
                 y = (float *)((char *)((ggml_tensor_extra_gpu *)dst->extra)->data_device[id] + (size_t)b * dst->nb[2]);
                 ldy = M;
             } else {
-                y = (float *)tmp_alloc((size_t)N * rows * 4);
+                y = (float *)tmp_alloc(id, (size_t)N * rows * 4);
                 ldy = rows;
             }
             if (mul_mat_dev(w, K, rows, x, N, y, ldy, 0, s) != GGML_HIP_OK) {
                 fprintf(stderr, "ggml_hip_mul_mat: %s\n", g_last_error.c_str());
                 abort();
             }
-            if (!direct) {
-                // y slice [N][rows] -> dst[n*M + lo + i]
-                if (dst_dev) {
-                    char *dbase = (char *)((ggml_tensor_extra_gpu *)dst->extra)->data_device[g_main_device] +
-                                  (size_t)b * dst->nb[2] + lo * 4;
-                    if (id == g_main_device) {
-                        HIP_FATAL(hipMemcpy2DAsync(dbase, M * 4, y, rows * 4, rows * 4, N, hipMemcpyDeviceToDevice, s));
-                    } else {
-                        for (int64_t n = 0; n < N; n++)
-                            HIP_FATAL(hipMemcpyPeerAsync(dbase + n * M * 4, g_main_device, y + n * rows, id, rows * 4, s));
-                    }
-                } else {
-                    char *dbase = (char *)dst->data + (size_t)b * dst->nb[2] + lo * 4;
-                    HIP_FATAL(hipMemcpy2DAsync(dbase, M * 4, y, rows * 4, rows * 4, N, hipMemcpyDeviceToHost, s));
-                }
+            if (direct) continue;
+            // y slice [N][rows] -> dst[n*M + lo + i]
+            if (!dst_dev) {
+                char *dbase = (char *)dst->data + (size_t)b * dst->nb[2] + lo * 4;
+                HIP_FATAL(hipMemcpy2DAsync(dbase, M * 4, y, rows * 4, rows * 4, N, hipMemcpyDeviceToHost, s));
+                continue;
             }
+            char *dbase = (char *)((ggml_tensor_extra_gpu *)dst->extra)->data_device[main_id] + (size_t)b * dst->nb[2] +
+                          lo * 4;
+            if (id == main_id) {
+                HIP_FATAL(hipMemcpy2DAsync(dbase, M * 4, y, rows * 4, rows * 4, N, hipMemcpyDeviceToDevice, s));
+                continue;
+            }
+            void *stage = tmp_alloc(main_id, (size_t)N * rows * 4);
+            HIP_FATAL(hipMemcpyPeerAsync(stage, main_id, y, id, (size_t)N * rows * 4, s));
+            HIP_FATAL(hipEventRecord(g_dev[id].ev_b, s));
+            HIP_FATAL(hipSetDevice(main_id));
+            HIP_FATAL(hipStreamWaitEvent(g_dev[main_id].stream, g_dev[id].ev_b, 0));
+            HIP_FATAL(hipMemcpy2DAsync(dbase, M * 4, stage, rows * 4, rows * 4, N, hipMemcpyDeviceToDevice,
+                                       g_dev[main_id].stream));
+            HIP_FATAL(hipSetDevice(id));
         }
-        // temporaries are reusable after this (ggml-cuda.cu:2546-2566); a call whose operands were all
-        // device resident stays stream-ordered (full offload: the next op runs on the same stream)
-        if (need_sync || !tmp.empty()) HIP_FATAL(hipStreamSynchronize(s));
-        for (auto &t : tmp) pool_free(id, t.first, t.second);
+    }
+    // temporaries are reusable after this (ggml-cuda.cu:2546-2566); a call whose operands were all
+    // device resident stays stream-ordered (full offload: the next op runs on the same stream)
+    for (int id = 0; id < g_device_count; id++) {
+        const bool main_staged = id == main_id && !tmps[id].empty();
+        if (!used[id] && !main_staged) continue;
+        if (need_sync || !tmps[id].empty()) {
+            HIP_FATAL(hipSetDevice(id));
+            HIP_FATAL(hipStreamSynchronize(g_dev[id].stream));
+        }
+        for (auto &t : tmps[id]) pool_free(id, t.first, t.second);
     }
     HIP_FATAL(hipSetDevice(saved));
 }
@@ -1739,17 +1796,60 @@ int ggml_hip_reserve_workspace(int64_t K, int64_t N) {
 }
 
 // ------------------------------------------------------------------------------------------
-// multi-GPU (one process per GPU) over RCCL
+// multi-GPU (one process per GPU) over RCCL.
+//
+// Transport: a communicator is either an RCCL communicator (ggml_hip_comm_init: one rank per
+// process and GPU, the production path) or an in-process loopback group
+// (ggml_hip_comm_init_local: R ranks driven by R host threads in ONE process, on one device or
+// several).  The loopback all-gather has ncclAllGather's exact semantics (recv[r*count ...] =
+// rank r's send, in place allowed, stream-ordered on every rank's stream); everything above the
+// transport (the row partition, the in-place / padded-slab layouts, the compaction kernel, the
+// grouped sibling all-gather) is the same code for both, so R > 1 runs on a 1-GPU box too.
+
+}  // extern "C"
+
+namespace {
+
+struct LocalGroup {
+    int R = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<const float *> send;
+    std::vector<size_t> count;
+    std::vector<hipEvent_t> ready, done;       // per rank: send written / copies out of it enqueued
+    std::vector<double> red;                   // host all-reduce scratch [R][n]
+    int refs = 0;
+
+    // every rank calls this with the same sequence number of collectives; blocks until all arrived
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == R) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+
+}  // namespace
 
 struct ggml_hip_comm {
-    ncclComm_t comm;
+    ncclComm_t comm = nullptr;
+    LocalGroup *local = nullptr;  // loopback transport when set
     int nranks;
     int rank;
     int device;
     float *slab = nullptr;        // [nranks][N][max_rows] gather buffer
     size_t slab_bytes = 0;
-    int64_t *row_begin_dev = nullptr;
+    double *red_dev = nullptr;    // host-value all-reduce staging (64 doubles)
 };
+
+namespace {
 
 #define NCCL_RET(expr)                                                                               \
     do {                                                                                             \
@@ -1759,6 +1859,46 @@ struct ggml_hip_comm {
             return GGML_HIP_ERR_COMM;                                                                \
         }                                                                                            \
     } while (0)
+
+// ncclAllGather(send, recv, count floats) on the comm's transport, stream-ordered on s
+int comm_allgather(ggml_hip_comm *c, const float *send, float *recv, size_t count, hipStream_t s) {
+    if (!c->local) {
+        NCCL_RET(ncclAllGather(send, recv, count, ncclFloat32, c->comm, s));
+        return GGML_HIP_OK;
+    }
+    LocalGroup &g = *c->local;
+    const int me = c->rank;
+    g.send[me] = send;
+    g.count[me] = count;
+    HIP_RET(hipEventRecord(g.ready[me], s));
+    g.barrier();                                             // every rank's send is published
+    bool agree = true;
+    for (int r = 0; r < g.R; r++) agree = agree && g.count[r] == count;
+    for (int r = 0; agree && r < g.R; r++) {
+        float *dst = recv + (size_t)r * count;
+        if (count == 0 || (r == me && dst == send)) continue;  // in place: already there
+        if (r != me) HIP_RET(hipStreamWaitEvent(s, g.ready[r], 0));
+        HIP_RET(hipMemcpyAsync(dst, g.send[r], count * 4, hipMemcpyDefault, s));
+    }
+    HIP_RET(hipEventRecord(g.done[me], s));
+    g.barrier();                                             // every rank's copies are enqueued
+    for (int r = 0; r < g.R; r++)
+        if (r != me) HIP_RET(hipStreamWaitEvent(s, g.done[r], 0));   // no rank reuses send early
+    g.barrier();                                             // events may be re-recorded now
+    return agree ? GGML_HIP_OK : fail(GGML_HIP_ERR_COMM, "loopback all-gather: ranks disagree on count");
+}
+int comm_group_start(ggml_hip_comm *c) {
+    if (!c->local) NCCL_RET(ncclGroupStart());
+    return GGML_HIP_OK;
+}
+int comm_group_end(ggml_hip_comm *c) {
+    if (!c->local) NCCL_RET(ncclGroupEnd());
+    return GGML_HIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int ggml_hip_comm_unique_id(char out[GGML_HIP_UNIQUE_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == GGML_HIP_UNIQUE_ID_BYTES, "ncclUniqueId size");
@@ -1771,6 +1911,7 @@ int ggml_hip_comm_unique_id(char out[GGML_HIP_UNIQUE_ID_BYTES]) {
 int ggml_hip_comm_init(ggml_hip_comm **comm, int nranks, int rank, const char id[GGML_HIP_UNIQUE_ID_BYTES]) {
     ensure_init();
     if (!comm || nranks < 1 || rank < 0 || rank >= nranks) return fail(GGML_HIP_ERR_INVALID, "bad comm arguments");
+    if (nranks > ghip::SCATTER_MAX_RANKS) return fail(GGML_HIP_ERR_UNSUPPORTED, "too many ranks");
     auto *c = new (std::nothrow) ggml_hip_comm;
     if (!c) return GGML_HIP_ERR_NOMEM;
     ncclUniqueId uid;
@@ -1783,17 +1924,101 @@ int ggml_hip_comm_init(ggml_hip_comm **comm, int nranks, int rank, const char id
         delete c;
         return fail(GGML_HIP_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     }
-    HIP_RET(hipMalloc(&c->row_begin_dev, sizeof(int64_t) * (GGML_HIP_MAX_DEVICES * 16 + 1)));
     *comm = c;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_comm_init_local(ggml_hip_comm **comms, int nranks, const int *devices) {
+    ensure_init();
+    if (!comms || nranks < 1 || nranks > ghip::SCATTER_MAX_RANKS) return fail(GGML_HIP_ERR_INVALID, "bad comm arguments");
+    auto *g = new LocalGroup;
+    g->R = nranks;
+    g->send.assign(nranks, nullptr);
+    g->count.assign(nranks, 0);
+    g->ready.assign(nranks, nullptr);
+    g->done.assign(nranks, nullptr);
+    g->refs = nranks;
+    const int saved = current_device();
+    for (int r = 0; r < nranks; r++) {
+        const int dev = devices ? devices[r] : saved;
+        if (dev < 0 || dev >= g_device_count) return fail(GGML_HIP_ERR_INVALID, "bad device");
+        HIP_RET(hipSetDevice(dev));
+        HIP_RET(hipEventCreateWithFlags(&g->ready[r], hipEventDisableTiming));
+        HIP_RET(hipEventCreateWithFlags(&g->done[r], hipEventDisableTiming));
+        auto *c = new ggml_hip_comm;
+        c->local = g;
+        c->nranks = nranks;
+        c->rank = r;
+        c->device = dev;
+        comms[r] = c;
+    }
+    HIP_RET(hipSetDevice(saved));
     return GGML_HIP_OK;
 }
 
 int ggml_hip_comm_destroy(ggml_hip_comm *c) {
     if (!c) return GGML_HIP_OK;
-    ncclCommDestroy(c->comm);
+    if (c->comm) ncclCommDestroy(c->comm);
     if (c->slab) (void)hipFree(c->slab);
-    if (c->row_begin_dev) (void)hipFree(c->row_begin_dev);
+    if (c->red_dev) (void)hipFree(c->red_dev);
+    if (c->local) {
+        LocalGroup *g = c->local;
+        bool last;
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            last = --g->refs == 0;
+        }
+        if (last) {
+            for (auto e : g->ready) (void)hipEventDestroy(e);
+            for (auto e : g->done) (void)hipEventDestroy(e);
+            delete g;
+        }
+    }
     delete c;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_comm_allreduce_host(ggml_hip_comm *c, double *vals, int n, int op) {
+    if (!c || !vals || n < 1 || n > 64 || op < 0 || op > 2) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    if (c->local) {
+        LocalGroup &g = *c->local;
+        {
+            std::lock_guard<std::mutex> lk(g.mu);
+            if (g.red.size() < (size_t)g.R * 64) g.red.assign((size_t)g.R * 64, 0.0);
+            for (int i = 0; i < n; i++) g.red[(size_t)c->rank * 64 + i] = vals[i];
+        }
+        g.barrier();
+        double out[64];
+        {
+            std::lock_guard<std::mutex> lk(g.mu);
+            for (int i = 0; i < n; i++) {
+                double v = g.red[i];
+                for (int r = 1; r < g.R; r++) {
+                    const double w = g.red[(size_t)r * 64 + i];
+                    v = op == 0 ? v + w : op == 1 ? std::max(v, w) : std::min(v, w);
+                }
+                out[i] = v;
+            }
+        }
+        g.barrier();
+        memcpy(vals, out, sizeof(double) * n);
+        return GGML_HIP_OK;
+    }
+    HIP_RET(hipSetDevice(c->device));
+    if (!c->red_dev) HIP_RET(hipMalloc(&c->red_dev, sizeof(double) * 64));
+    hipStream_t s = g_dev[c->device].stream;
+    HIP_RET(hipMemcpyAsync(c->red_dev, vals, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    const ncclRedOp_t ops[3] = {ncclSum, ncclMax, ncclMin};
+    NCCL_RET(ncclAllReduce(c->red_dev, c->red_dev, (size_t)n, ncclFloat64, ops[op], c->comm, s));
+    HIP_RET(hipMemcpyAsync(vals, c->red_dev, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIP_RET(hipStreamSynchronize(s));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_comm_rank(const ggml_hip_comm *c, int *rank, int *nranks) {
+    if (!c) return fail(GGML_HIP_ERR_INVALID, "null comm");
+    if (rank) *rank = c->rank;
+    if (nranks) *nranks = c->nranks;
     return GGML_HIP_OK;
 }
 
@@ -1823,17 +2048,17 @@ int ggml_hip_mul_mat_q4_0_split(ggml_hip_comm *c, const void *dev_w_local, int64
                                 const int64_t *row_begin, const float *dev_x, int64_t N, float *dev_y_full,
                                 void *stream) {
     if (!c || !row_begin || !dev_y_full) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
-    if (c->nranks > GGML_HIP_MAX_DEVICES * 16) return fail(GGML_HIP_ERR_UNSUPPORTED, "too many ranks");
     hipStream_t s = resolve_stream(stream);
     const int R = c->nranks;
     int64_t max_rows = 0;
     bool equal = true;
+    if (row_begin[0] != 0 || row_begin[R] != M_total) return fail(GGML_HIP_ERR_INVALID, "row_begin must cover [0, M)");
     for (int r = 0; r < R; r++) {
         const int64_t rows = row_begin[r + 1] - row_begin[r];
+        if (rows < 0) return fail(GGML_HIP_ERR_INVALID, "row_begin must be non-decreasing");
         max_rows = std::max(max_rows, rows);
         if (rows != row_begin[1] - row_begin[0]) equal = false;
     }
-    if (row_begin[0] != 0 || row_begin[R] != M_total) return fail(GGML_HIP_ERR_INVALID, "row_begin must cover [0, M)");
     const int64_t my_rows = row_begin[c->rank + 1] - row_begin[c->rank];
     if (equal && N == 1) {
         // y_full[M] = concat of the equal rank slices: compute in place, gather in place
@@ -1842,14 +2067,21 @@ int ggml_hip_mul_mat_q4_0_split(ggml_hip_comm *c, const void *dev_w_local, int64
             int rc = mul_mat_dev(dev_w_local, K, my_rows, dev_x, N, mine, my_rows, 0, s);
             if (rc != GGML_HIP_OK) return rc;
         }
-        NCCL_RET(ncclAllGather(mine, dev_y_full, (size_t)my_rows, ncclFloat32, c->comm, s));
-        return GGML_HIP_OK;
+        return comm_allgather(c, mine, dev_y_full, (size_t)my_rows, s);
     }
     // padded slabs [R][N][max_rows] -> compaction into y_full[n][M]
     const size_t slab = (size_t)N * max_rows;
     const size_t need = slab * R * 4 + slab * 4;
     if (c->slab_bytes < need) {
-        if (c->slab) HIP_RET(hipFree(c->slab));
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
+            return fail(GGML_HIP_ERR_INVALID, "split gather buffer must grow outside stream capture (run once first)");
+        if (c->slab) {
+            HIP_RET(hipStreamSynchronize(s));
+            HIP_RET(hipFree(c->slab));
+            c->slab = nullptr;
+            c->slab_bytes = 0;
+        }
         HIP_RET(hipMalloc(&c->slab, need));
         c->slab_bytes = need;
     }
@@ -1858,9 +2090,11 @@ int ggml_hip_mul_mat_q4_0_split(ggml_hip_comm *c, const void *dev_w_local, int64
         int rc = mul_mat_dev(dev_w_local, K, my_rows, dev_x, N, send, max_rows, 0, s);
         if (rc != GGML_HIP_OK) return rc;
     }
-    NCCL_RET(ncclAllGather(send, c->slab, slab, ncclFloat32, c->comm, s));
-    HIP_RET(hipMemcpyAsync(c->row_begin_dev, row_begin, sizeof(int64_t) * (R + 1), hipMemcpyHostToDevice, s));
-    HIP_RET(ghip::scatter_slabs(c->slab, R, max_rows, c->row_begin_dev, N, dev_y_full, M_total, s));
+    int rc = comm_allgather(c, send, c->slab, slab, s);
+    if (rc != GGML_HIP_OK) return rc;
+    ghip::RowBegins rb;
+    for (int r = 0; r <= R; r++) rb.v[r] = row_begin[r];
+    HIP_RET(ghip::scatter_slabs(c->slab, R, max_rows, rb, N, dev_y_full, M_total, s));
     return GGML_HIP_OK;
 }
 
@@ -1893,18 +2127,17 @@ int ggml_hip_mul_mat_q4_0_split_multi(ggml_hip_comm *c, int n, const void *const
         m_loc[i] = row_begin[i][c->rank + 1] - row_begin[i][c->rank];
         mine[i] = dev_y_full[i] + row_begin[i][c->rank];
     }
-    const int rc = ggml_hip_mul_mat_q4_0_multi(n, dev_w_local, m_loc, K, dev_x, N, mine, s);
+    int rc = ggml_hip_mul_mat_q4_0_multi(n, dev_w_local, m_loc, K, dev_x, N, mine, s);
     if (rc != GGML_HIP_OK) return rc;
-    NCCL_RET(ncclGroupStart());
+    if ((rc = comm_group_start(c)) != GGML_HIP_OK) return rc;
     for (int i = 0; i < n; i++) {
-        const ncclResult_t r = ncclAllGather(mine[i], dev_y_full[i], (size_t)m_loc[i], ncclFloat32, c->comm, s);
-        if (r != ncclSuccess) {
-            (void)ncclGroupEnd();
-            NCCL_RET(r);
+        rc = comm_allgather(c, mine[i], dev_y_full[i], (size_t)m_loc[i], s);
+        if (rc != GGML_HIP_OK) {
+            (void)comm_group_end(c);
+            return rc;
         }
     }
-    NCCL_RET(ncclGroupEnd());
-    return GGML_HIP_OK;
+    return comm_group_end(c);
 }
 
 int ggml_hip_weight_cache_stats(int64_t *hits, int64_t *misses, int64_t *resident_bytes) {
@@ -2000,6 +2233,33 @@ int ggml_hip_device_synchronize(void) {
 }
 
 void *ggml_hip_default_stream(void) { return (void *)resolve_stream(nullptr); }
+
+void *ggml_hip_stream_create(void) {
+    ensure_init();
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        g_last_error = "hipStreamCreateWithFlags failed";
+        return nullptr;
+    }
+    return (void *)s;
+}
+
+int ggml_hip_stream_destroy(void *stream) {
+    if (!stream) return GGML_HIP_OK;
+    hipStream_t s = (hipStream_t)stream;
+    HIP_RET(hipStreamSynchronize(s));
+    for (int id = 0; id < g_device_count; id++) {
+        Device &d = g_dev[id];
+        std::lock_guard<std::mutex> lk(d.mu);
+        auto it = d.stream_ws.find(s);
+        if (it != d.stream_ws.end()) {
+            if (it->second.ptr) HIP_RET(hipFree(it->second.ptr));
+            d.stream_ws.erase(it);
+        }
+    }
+    HIP_RET(hipStreamDestroy(s));
+    return GGML_HIP_OK;
+}
 
 int ggml_hip_fill_gaussian(float *dev_dst, int64_t n, uint64_t seed, float mean, float stdv, void *stream) {
     HIP_RET(ghip::fill_gaussian(dev_dst, n, seed, mean, stdv, resolve_stream(stream)));

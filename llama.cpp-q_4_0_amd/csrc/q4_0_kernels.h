@@ -64,7 +64,12 @@ hipError_t mm_exact_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs,
                          float *y, int64_t ldy, hipStream_t s);
 
 // Multi-GPU helper: y[n*ldy + row0[r] + i] = slab[r][n][i] for i < rows[r] (gather compaction).
-hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const int64_t *row_begin_dev,
+// row_begin travels as a kernel argument (no host->device copy, capture-safe)
+static constexpr int SCATTER_MAX_RANKS = 256;
+struct RowBegins {
+    int64_t v[SCATTER_MAX_RANKS + 1];
+};
+hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const RowBegins &row_begin,
                          int64_t N, float *y, int64_t ldy, hipStream_t s);
 
 // Synthetic inputs for the bench (splitmix64 + Box-Muller on device).

@@ -326,6 +326,10 @@ struct GemvMats {
 // VAR bit 0 (GLB): weight loads are plain global loads with clamped lane addresses
 // VAR bit 1 (XSPLIT): only the first XW waves load and quantize x; the other waves issue their
 //                     weight loads at once (the x loads enter the CU's queue first)
+// VAR bit 2 (XFIRST, with XSPLIT): a workgroup barrier between the x-waves' x load ISSUE and every
+//                     wave's first weight issue, so the x loads are ahead of all of the workgroup's
+//                     weight loads in the CU's memory pipeline (phase stamps: without it the x data
+//                     returned together with the weights, and the prologue barrier gated compute)
 // PPL > 0 ("row items", decode, K <= 12288): lane l takes pairs l, l+64, ..., l+64*(PPL-1) of the
 //                     row (PPL = ceil(pairs/64)), so one item is a whole row: all of its loads are
 //                     in flight together and it is reduced once (a row of K=4160 no longer costs two
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
         }
     };
     auto item_row = [&](int it) __attribute__((always_inline)) { return row0 + (it / nchunk) * rstride; };
-    constexpr bool GLB = (VAR & 1) != 0, XSPLIT = (VAR & 2) != 0;
+    constexpr bool GLB = (VAR & 1) != 0, XSPLIT = (VAR & 2) != 0, XFIRST = (VAR & 4) != 0;
     static_assert(PPL == 0 || GLB, "row items use the global-load form");
     auto issue = [&](int it) __attribute__((always_inline)) {
         const bool valid = it < nitems;                             // past the end: zero-size descriptor
@@ -444,7 +448,30 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
         const int XW0 = (total + 64 * GEMV_XPRO - 1) / (64 * GEMV_XPRO);
         const int XW = XW0 < WAVES ? XW0 : WAVES;
         const int XT = XW * 64;
-        if (wave < XW) {
+        if constexpr (XFIRST) {
+            u32x4 xw[GEMV_XPRO];
+            if (wave < XW) {
+#pragma unroll
+                for (int i = 0; i < GEMV_XPRO; i++)
+                    xw[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * XT), 0, 0);
+            }
+            __builtin_amdgcn_s_barrier();                           // x loads issued before any weight
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+            GEMV_STAMP(1);
+            if (wave < XW) {
+#pragma unroll
+                for (int i = 0; i < GEMV_XPRO; i++) quantize_into_lds(xw[i], tid + i * XT);
+                for (int base = GEMV_XPRO * XT; base < total; base += GEMV_XPRO * XT) {
+#pragma unroll
+                    for (int i = 0; i < GEMV_XPRO; i++)
+                        xw[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * XT), 0, 0);
+#pragma unroll
+                    for (int i = 0; i < GEMV_XPRO; i++) quantize_into_lds(xw[i], base + tid + i * XT);
+                }
+            }
+        } else if (wave < XW) {
             u32x4 xw[GEMV_XPRO];
             for (int base = 0; base < total; base += GEMV_XPRO * XT) {
 #pragma unroll
@@ -463,7 +490,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
 #pragma unroll
             for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
         }
-        GEMV_STAMP(1);
+        if constexpr (!XFIRST) GEMV_STAMP(1);
         GEMV_STAMP(2);
     } else {
 #pragma unroll
@@ -624,19 +651,31 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     return hipGetLastError();
 }
 
+template <int NT, int DIAG, int VAR>
+static hipError_t launch_gemv_rows(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s,
+                                   int ppl, int rd) {
+    switch (ppl) {
+        case 1: return rd == 1 ? launch_gemv_w<NT, DIAG, 16, 1, VAR, 1>(m, K, x, dev, s)
+                               : launch_gemv_w<NT, DIAG, 16, 2, VAR, 1>(m, K, x, dev, s);
+        case 2: return rd == 1 ? launch_gemv_w<NT, DIAG, 16, 1, VAR, 2>(m, K, x, dev, s)
+                               : launch_gemv_w<NT, DIAG, 16, 2, VAR, 2>(m, K, x, dev, s);
+        default: return rd == 1 ? launch_gemv_w<NT, DIAG, 16, 1, VAR, 3>(m, K, x, dev, s)
+                                : launch_gemv_w<NT, DIAG, 16, 2, VAR, 3>(m, K, x, dev, s);
+    }
+}
+
 template <int NT>
 static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
     // Production: VAR 3 (global weight loads + x-wave prologue), ring depth 1 for single-chunk
     // rows (K <= 4096) and 2 when a row spans several 64-pair chunks (measured per shape,
-    // tools/gemv_ab.sh).  GGML_HIP_GEMV_VAR=0 / GGML_HIP_GEMV_DEPTH=1|2 select the A/B variants;
-    // GGML_HIP_GEMV_DIAG=7 the phase-stamp build, 8/9/10 the timing knockouts (invalid results).
+    // tools/gemv_ab.sh).  GGML_HIP_GEMV_VAR=0 / 7 / GGML_HIP_GEMV_DEPTH=1|2 select the A/B variants;
+    // GGML_HIP_GEMV_DIAG=7 the phase-stamp build (row items as in production), 8/9/10 the timing
+    // knockouts (invalid results).
     static const int diag = env_int("GGML_HIP_GEMV_DIAG", 0);
     static const int var = env_int("GGML_HIP_GEMV_VAR", 3);
     const int depth_env = gemv_policy().depth;
     const int depth = depth_env ? depth_env : (K / 64 > 64 ? 2 : 1);
     if constexpr (NT == 1) {
-        if (diag == 7) return depth == 1 ? launch_gemv_w<NT, 7, 16, 1, 3>(m, K, x, dev, s)
-                                         : launch_gemv_w<NT, 7, 16, 2, 3>(m, K, x, dev, s);
         if (diag == 8) return launch_gemv_w<NT, 8, 16, 1>(m, K, x, dev, s);
         if (diag == 9) return launch_gemv_w<NT, 9, 16, 1>(m, K, x, dev, s);
         if (diag == 10) return launch_gemv_w<NT, 10, 16, 1>(m, K, x, dev, s);
@@ -644,26 +683,25 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
     if constexpr (NT == 1) {                        // decode: one item per row (PPL pairs per lane)
         const int rowitems = gemv_policy().rowitems;
         const int ppl = (int)((K / 64 + 63) / 64);
-        if (rowitems && var == 3 && diag == 0) {
+        if (rowitems && (var == 3 || var == 7) && ppl <= 3) {
             // two rows in flight per wave, except the multi-round strided case (M > 2*CUs*16 with
             // the leftover rows a whole round per CU, e.g. the fused LLaMA-7B wq|wk|wv, M = 12288)
             const int64_t M = m.row_begin[m.n], r1 = 2 * (int64_t)dev.num_cus * 16;
             const bool strided_multi = M > r1 && (M % r1) % (r1 / 2) == 0;
             const int rd = depth_env ? depth_env : (strided_multi ? 1 : 2);
-            switch (ppl) {
-                case 1: return rd == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 1>(m, K, x, dev, s)
-                                       : launch_gemv_w<NT, 0, 16, 2, 3, 1>(m, K, x, dev, s);
-                case 2: return rd == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 2>(m, K, x, dev, s)
-                                       : launch_gemv_w<NT, 0, 16, 2, 3, 2>(m, K, x, dev, s);
-                case 3: return rd == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 3>(m, K, x, dev, s)
-                                       : launch_gemv_w<NT, 0, 16, 2, 3, 3>(m, K, x, dev, s);
-                default: break;                     // K > 12288: chunked items below (measured
-                                                    // equal or faster at 4-5 pairs per lane)
-            }
+            if (diag == 7) return var == 7 ? launch_gemv_rows<NT, 7, 7>(m, K, x, dev, s, ppl, rd)
+                                           : launch_gemv_rows<NT, 7, 3>(m, K, x, dev, s, ppl, rd);
+            return var == 7 ? launch_gemv_rows<NT, 0, 7>(m, K, x, dev, s, ppl, rd)
+                            : launch_gemv_rows<NT, 0, 3>(m, K, x, dev, s, ppl, rd);
         }
+        // K > 12288: chunked items below (measured equal or faster at 4-5 pairs per lane)
+        if (diag == 7) return depth == 1 ? launch_gemv_w<NT, 7, 16, 1, 3>(m, K, x, dev, s)
+                                         : launch_gemv_w<NT, 7, 16, 2, 3>(m, K, x, dev, s);
     }
     if (var == 0) return depth == 1 ? launch_gemv_w<NT, 0, 16, 1, 0>(m, K, x, dev, s)
                                     : launch_gemv_w<NT, 0, 16, 2, 0>(m, K, x, dev, s);
+    if (var == 7) return depth == 1 ? launch_gemv_w<NT, 0, 16, 1, 7>(m, K, x, dev, s)
+                                    : launch_gemv_w<NT, 0, 16, 2, 7>(m, K, x, dev, s);
     return depth == 1 ? launch_gemv_w<NT, 0, 16, 1, 3>(m, K, x, dev, s)
                       : launch_gemv_w<NT, 0, 16, 2, 3>(m, K, x, dev, s);
 }
@@ -1811,7 +1849,7 @@ hipError_t mm_exact_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs,
 // multi-GPU gather compaction: slabs [nranks][N][max_rows] -> y[n][row_begin[r] + i]
 
 __global__ __launch_bounds__(256) void k_scatter_slabs(const float *__restrict__ slabs, int nranks,
-                                                         int64_t max_rows, const int64_t *__restrict__ row_begin,
+                                                         int64_t max_rows, const RowBegins row_begin,
                                                          int64_t N, float *__restrict__ y, int64_t ldy) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)nranks * N * max_rows;
@@ -1819,17 +1857,18 @@ __global__ __launch_bounds__(256) void k_scatter_slabs(const float *__restrict__
     const int64_t i = t % max_rows;
     const int64_t n = (t / max_rows) % N;
     const int r = (int)(t / (max_rows * N));
-    const int64_t rows = row_begin[r + 1] - row_begin[r];
-    if (i < rows) y[n * ldy + row_begin[r] + i] = slabs[t];
+    const int64_t rb = row_begin.v[r], rows = row_begin.v[r + 1] - rb;
+    if (i < rows) y[n * ldy + rb + i] = slabs[t];
 }
 
-hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const int64_t *row_begin_dev, int64_t N,
+hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const RowBegins &row_begin, int64_t N,
                          float *y, int64_t ldy, hipStream_t s) {
     const int64_t total = (int64_t)nranks * N * max_rows;
     if (total == 0) return hipSuccess;
+    if (nranks > SCATTER_MAX_RANKS) return hipErrorInvalidValue;
     (void)hipGetLastError();  // report only this launch's error
     hipLaunchKernelGGL(k_scatter_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, slabs, nranks,
-                       max_rows, row_begin_dev, N, y, ldy);
+                       max_rows, row_begin, N, y, ldy);
     return hipGetLastError();
 }
 

@@ -4,9 +4,10 @@ This is the ctypes stub a Python host would add for the backend (INTEGRATION.md 
 same for ggml.c itself).  Nothing here computes: every operation is a C-ABI call into the
 HIP library, and loading fails loudly when the library is missing.
 
-Runtime note: the library links libamdhip64.so.7 / librccl.so.1.  If torch is importable it is
-imported first so that the process has exactly one HIP runtime (torch's bundled one satisfies
-the same sonames); set GGML_HIP_NO_TORCH=1 to use /opt/rocm's runtime without torch.
+Runtime note: the library links libamdhip64.so.7 / librccl.so.1 from /opt/rocm (its RUNPATH), the
+runtime it was built against.  torch bundles its own copies; a process that loads this library
+must not import torch first (the first mapped soname wins process-wide).  bench.py and the GPU
+tests never import torch (tests/conftest.py loads this library before any test module).
 """
 import ctypes
 import os
@@ -59,6 +60,11 @@ def _bind(L):
         "ggml_hip_comm_unique_id": ([vp], i32),
         "ggml_hip_comm_init": ([vp, i32, i32, vp], i32),
         "ggml_hip_comm_destroy": ([vp], i32),
+        "ggml_hip_comm_init_local": ([vp, i32, vp], i32),
+        "ggml_hip_comm_rank": ([vp, vp, vp], i32),
+        "ggml_hip_comm_allreduce_host": ([vp, vp, i32, i32], i32),
+        "ggml_hip_stream_create": ([], vp),
+        "ggml_hip_stream_destroy": ([vp], i32),
         "ggml_hip_split_rows": ([i64, i32, vp, vp], i32),
         "ggml_hip_mul_mat_q4_0_split": ([vp, vp, i64, i64, vp, vp, i64, vp, vp], i32),
         "ggml_hip_mul_mat_q4_0_split_multi": ([vp, i32, vp, vp, vp, i64, vp, i64, vp, vp], i32),
@@ -112,11 +118,10 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise GgmlHipError(f"{LIB_PATH} not built: run `make -C llama.cpp-q_4_0_amd` (or __graft_entry__.build())")
-    if not os.environ.get("GGML_HIP_NO_TORCH"):
-        try:
-            import torch  # noqa: F401  (one HIP runtime per process, see module doc)
-        except Exception:
-            pass
+    if "torch" in sys.modules and os.environ.get("GGML_HIP_ALLOW_TORCH_RUNTIME") != "1":
+        import warnings
+        warnings.warn("torch was imported before libggml_hip.so: the process may run on torch's bundled "
+                      "HIP/RCCL runtime instead of /opt/rocm's (see ggml_hip module doc)")
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     _bind(L)
     _lib = L
@@ -130,6 +135,19 @@ def check(rc, what="ggml_hip"):
 
 def device_count():
     return load().ggml_hip_device_count()
+
+
+def mapped_runtime_libs():
+    """Paths of the HIP / RCCL runtime libraries mapped into this process (/proc/self/maps)."""
+    libs = set()
+    try:
+        for line in open("/proc/self/maps"):
+            p = line.split()[-1] if "/" in line else ""
+            if any(n in p for n in ("librccl", "libamdhip64", "libhsa-runtime64", "libggml_hip")):
+                libs.add(p)
+    except OSError:
+        pass
+    return sorted(libs)
 
 
 class DeviceBuffer:

@@ -96,3 +96,33 @@ def test_declined_node_runs_reference_cpu_op(ref):
     y, be = ggml_mul_mat(ref, wq, 4096, x, 0, 2)
     assert be == GGML_BACKEND_CPU
     assert np.array_equal(y.view(np.uint32), load("avx2", "y4096_mul_mat").view(np.uint32))
+
+
+def _device_count():
+    try:
+        from hip_env import ggml_hip
+        return ggml_hip.device_count()
+    except Exception:
+        return 0
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="needs >= 2 HIP devices (GPU_SPLIT across devices)")
+@pytest.mark.parametrize("fractions", [None, (1.0, 3.0)])
+@pytest.mark.parametrize("N", [4, 64])
+def test_gpu_split_across_devices(ref, fractions, N):
+    """GGML_BACKEND_GPU_SPLIT with the rows on 2+ devices (llama.cpp -ts, ggml-cuda.cu:2286-2567):
+    every device's slice is enqueued before the single per-device synchronize, slices gathered
+    by one peer copy + one 2-D copy each; y within the bound of the reference's CPU result."""
+    ndev = _device_count()
+    if fractions is not None:
+        fr = (ctypes.c_float * 16)(*(list(fractions) + [0.0] * (16 - len(fractions))))
+        ref.ggml_cuda_set_tensor_split(fr)
+    try:
+        K, M = 4096, 1000 + 8 * ndev
+        wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED7300 + N, 0.0, 0.02).reshape(M, K))
+        x = O.gaussian(N * K, 0x5EED7400 + N, 0.0, 1.0).reshape(N, K)
+        y, _ = ggml_mul_mat(ref, wq, K, x, 2, 4)
+        assert_close(wq, x, K, y, O.mul_mat(wq, K, x))
+    finally:
+        if fractions is not None:
+            ref.ggml_cuda_set_tensor_split((ctypes.c_float * 16)(*([1.0] * ndev + [0.0] * (16 - ndev))))

@@ -1,0 +1,247 @@
+"""Multi-GPU row split (BASELINE config 4) through the product's own split code.
+
+* LLaMA-13B per-rank shard shapes of the 8-way split (K=5120 -> M/8 = 640 / 1728, K=13824 -> 640)
+  against the oracle, decode and small/large batches.
+* R = 2..8 ranks through ggml_hip_mul_mat_q4_0_split / _split_multi on ONE device: the
+  in-process loopback transport (ggml_hip_comm_init_local, one host thread per rank, each on its
+  own stream) has ncclAllGather's semantics, so the partition, the in-place gather, the padded
+  slabs and the compaction kernel (k_scatter_slabs) run exactly as on 8 GPUs, with equal and
+  uneven (reference tensor_split, ggml-cuda.cu:1863-1882) partitions.  Every rank's y_full must
+  equal, bitwise, the concatenation of the per-slice products computed alone.
+* The RCCL transport with one process per GPU (skipped below 2 visible devices): tests/
+  split_worker.py ranks, unique id through a file, no torch import.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+import tempfile
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+from hip_env import ggml_hip, gpu_available
+from parity import block_terms, check_y
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs a HIP device and libggml_hip.so")]
+
+DB = ggml_hip.DeviceBuffer
+RTOL, ATOL_BLOCKS = 1e-3, 1e-5
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def make_case(K, M, N, seed):
+    wf = O.gaussian(M * K, 0x5EED3000 + seed, 0.0, 0.02).reshape(M, K)
+    wq, _ = O.quantize_q4_0(wf)
+    x = O.gaussian(N * K, 0x5EED4000 + seed, 0.0, 1.0).reshape(N, K)
+    return wq, x
+
+
+def split_rows(M, R, fractions=None):
+    L = ggml_hip.load()
+    rb = np.zeros(R + 1, np.int64)
+    fp = None
+    if fractions is not None:
+        fr = np.asarray(fractions, np.float32)
+        fp = fr.ctypes.data_as(ctypes.c_void_p)
+    ggml_hip.check(L.ggml_hip_split_rows(M, R, fp, rb.ctypes.data_as(ctypes.c_void_p)))
+    return rb
+
+
+def gpu_y(wq, K, x):
+    N, M = x.shape[0], wq.shape[0]
+    wd, xd, yd = DB.from_array(wq), DB.from_array(x), DB(max(N * M, 1) * 4)
+    ggml_hip.mul_mat(wd, K, M, xd, N, yd)
+    return yd.download((N, M), np.float32)
+
+
+# ------------------------------------------------------------------ 13B per-rank shard shapes
+@pytest.mark.parametrize("K,M", [(5120, 640), (5120, 1728), (13824, 640)])
+@pytest.mark.parametrize("N", [1, 3, 64])
+def test_llama13b_shard_shapes(K, M, N):
+    """One rank's slice of the LLaMA-13B 8-way split (wq/wk/wv/wo 5120/8, w1/w3 13824/8, w2 at
+    K=13824): y within the parity bound of the oracle (ggml.c:11226-11424 semantics)."""
+    wq, x = make_case(K, M, N, seed=K + M + N)
+    y = gpu_y(wq, K, x)
+    _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
+    check_y(y, O.mul_mat(wq, K, x, nthreads=8), s_abs, RTOL, ATOL_BLOCKS)
+
+
+# ------------------------------------------------------------------ R ranks, loopback transport
+def run_ranks(R, fn):
+    """fn(rank, comm, stream) in R threads (ctypes releases the GIL); re-raises the first error."""
+    L = ggml_hip.load()
+    comms = (ctypes.c_void_p * R)()
+    ggml_hip.check(L.ggml_hip_comm_init_local(comms, R, None), "comm_init_local")
+    streams = [L.ggml_hip_stream_create() for _ in range(R)]
+    errs = [None] * R
+    out = [None] * R
+
+    def body(r):
+        try:
+            out[r] = fn(r, ctypes.c_void_p(comms[r]), streams[r])
+            ggml_hip.check(L.ggml_hip_stream_synchronize(streams[r]))
+        except BaseException as e:           # noqa: BLE001 - reported below
+            errs[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(R)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    alive = any(t.is_alive() for t in th)
+    for s in streams:
+        L.ggml_hip_stream_destroy(s)
+    for r in range(R):
+        L.ggml_hip_comm_destroy(ctypes.c_void_p(comms[r]))
+    assert not alive, "a rank thread hung"
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
+
+
+FRACTIONS = {2: [0.3, 0.7], 3: [1.0, 2.0, 1.0], 4: [0.1, 0.2, 0.3, 0.4],
+             8: [1.0, 1.0, 2.0, 0.5, 0.5, 1.0, 3.0, 1.0]}
+
+
+@pytest.mark.parametrize("R", [2, 3, 4, 8])
+@pytest.mark.parametrize("uneven", [False, True])
+@pytest.mark.parametrize("N", [1, 3, 40])
+def test_split_loopback_ranks(R, uneven, N):
+    """ggml_hip_mul_mat_q4_0_split at R ranks: equal N=1 takes the in-place all-gather, the rest the
+    padded slabs + k_scatter_slabs.  y_full on EVERY rank == concat of the slice products, bitwise."""
+    if uneven and R not in FRACTIONS:
+        pytest.skip("no uneven split for this R")
+    K, M = 4096, 1000 if uneven else 1024
+    wq, x = make_case(K, M, N, seed=100 * R + N + uneven)
+    rb = split_rows(M, R, FRACTIONS[R] if uneven else None)
+    assert rb[0] == 0 and rb[-1] == M and np.all(np.diff(rb) >= 0)
+    slices = [wq[rb[r]:rb[r + 1]] for r in range(R)]
+    expect = np.concatenate([gpu_y(s, K, x) if len(s) else np.zeros((N, 0), np.float32) for s in slices], axis=1)
+    L = ggml_hip.load()
+    xd = DB.from_array(x)
+    wds = [DB.from_array(s) if len(s) else DB(16) for s in slices]
+    yds = [DB(N * M * 4) for _ in range(R)]
+    for y in yds:
+        L.ggml_hip_memset(y.ptr, 0x7F, y.nbytes, None)
+    ggml_hip.synchronize()
+
+    def rank(r, comm, stream):
+        ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split(comm, wds[r].ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
+                                                     xd.ptr, N, yds[r].ptr, stream), f"split rank {r}")
+
+    run_ranks(R, rank)
+    for r in range(R):
+        got = yds[r].download((N, M), np.float32)
+        assert np.array_equal(got.view(np.uint32), expect.view(np.uint32)), f"rank {r}"
+    _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
+    check_y(expect, O.mul_mat(wq, K, x, nthreads=8), s_abs, RTOL, ATOL_BLOCKS)
+
+
+@pytest.mark.parametrize("R", [2, 4, 8])
+@pytest.mark.parametrize("N,Ms,uneven", [(1, (5120, 5120, 5120), False), (1, (13824, 13824), False),
+                                         (1, (4096, 1000), True), (3, (1024, 2048), False)])
+def test_split_multi_loopback_ranks(R, N, Ms, uneven):
+    """Sibling form (one multi-matrix GEMV + one grouped all-gather per rank; per-matrix split
+    otherwise), 13B QKV / w1|w3 shard shapes at R=8: every rank's outputs == per-slice products."""
+    K = 5120 if Ms[0] in (5120, 13824) else 4096
+    n = len(Ms)
+    x = O.gaussian(N * K, 0x5EED5000 + R + N, 0.0, 1.0).reshape(N, K)
+    fr = FRACTIONS.get(R) if uneven else None
+    rbs = [split_rows(M, R, fr) for M in Ms]
+    ws = [make_case(K, M, 1, seed=7 * i + R)[0] for i, M in enumerate(Ms)]
+    expect = []
+    for w, rb in zip(ws, rbs):
+        expect.append(np.concatenate([gpu_y(w[rb[r]:rb[r + 1]], K, x) for r in range(R)], axis=1))
+    L = ggml_hip.load()
+    xd = DB.from_array(x)
+    wds = [[DB.from_array(w[rb[r]:rb[r + 1]]) for w, rb in zip(ws, rbs)] for r in range(R)]
+    yds = [[DB(N * M * 4) for M in Ms] for _ in range(R)]
+    ggml_hip.synchronize()
+    mt = (ctypes.c_int64 * n)(*Ms)
+    rp = (ctypes.c_void_p * n)(*[rb.ctypes.data for rb in rbs])
+
+    def rank(r, comm, stream):
+        wp = (ctypes.c_void_p * n)(*[w.ptr for w in wds[r]])
+        yp = (ctypes.c_void_p * n)(*[y.ptr for y in yds[r]])
+        ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split_multi(comm, n, wp, mt, rp, K, xd.ptr, N, yp, stream),
+                       f"split_multi rank {r}")
+
+    run_ranks(R, rank)
+    for r in range(R):
+        for i, M in enumerate(Ms):
+            got = yds[r][i].download((N, M), np.float32)
+            assert np.array_equal(got.view(np.uint32), expect[i].view(np.uint32)), (r, i)
+
+
+def test_split_slab_path_graph_capture():
+    """A split call on the padded-slab path captured in a HIP graph (the bench's form) replays the
+    same gather: the compaction kernel takes row_begin by value, nothing host-side is read at
+    replay.  (Loopback ranks need a host thread each, so the capture runs one rank.)"""
+    K, M, N = 4096, 1000, 3
+    wq, x = make_case(K, M, N, seed=9)
+    expect = gpu_y(wq, K, x)
+    L = ggml_hip.load()
+    xd, wd, y = DB.from_array(x), DB.from_array(wq), DB(N * M * 4)
+    comms = (ctypes.c_void_p * 1)()
+    ggml_hip.check(L.ggml_hip_comm_init_local(comms, 1, None))
+    comm = ctypes.c_void_p(comms[0])
+    s = L.ggml_hip_stream_create()
+    rb = np.array([0, M], np.int64)
+    try:
+        def call():
+            ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split(comm, wd.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
+                                                         xd.ptr, N, y.ptr, s), "split")
+        call()                                   # grows the slab outside capture
+        g = ggml_hip.Graph(s)
+        with g:
+            call()
+        L.ggml_hip_memset(y.ptr, 0, y.nbytes, s)
+        g.launch()
+        got = y.download((N, M), np.float32, stream=s)
+        assert np.array_equal(got.view(np.uint32), expect.view(np.uint32))
+    finally:
+        L.ggml_hip_stream_destroy(s)
+        L.ggml_hip_comm_destroy(comm)
+
+
+# ------------------------------------------------------------------ RCCL, one process per GPU
+def _device_count_subprocess():
+    code = ("import sys; sys.path.insert(0, %r); import ggml_hip; print(ggml_hip.load().ggml_hip_device_count())"
+            % os.path.join(os.path.dirname(HERE), "llama.cpp-q_4_0_amd", "python"))
+    try:
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+        return int(out.stdout.strip().splitlines()[-1])
+    except Exception:
+        return 0
+
+
+@pytest.mark.parametrize("R", [2, 4, 8])
+def test_split_rccl_multiprocess(R):
+    """RCCL transport: R processes (tests/split_worker.py), one GPU each; every rank runs split and
+    split_multi (13B shard shapes, equal and uneven) and checks itself against the unsharded
+    per-slice products it computes locally; unique id via a file."""
+    ndev = _device_count_subprocess()
+    if ndev < R:
+        pytest.skip(f"needs {R} visible devices (have {ndev})")
+    with tempfile.TemporaryDirectory() as td:
+        idfile = os.path.join(td, "uid")
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "split_worker.py"), str(r), str(R), idfile],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                 for r in range(R)]
+        outs = []
+        for p in procs:
+            try:
+                outs.append(p.communicate(timeout=240)[0])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        for r, (p, o) in enumerate(zip(procs, outs)):
+            assert p.returncode == 0, f"rank {r} failed:\n{o[-3000:]}"
+            assert "SPLIT_OK" in o, o[-2000:]

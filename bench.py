@@ -515,65 +515,154 @@ def _cpu_name():
     return cpu
 
 
+def _cpu_flags():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                return set(line.split(":", 1)[1].split())
+    except OSError:
+        pass
+    return set()
+
+
+def _stats(vals):
+    v = np.asarray(vals, np.float64)
+    return {"median": float(np.median(v)), "min": float(v.min()), "max": float(v.max()), "n": int(v.size)}
+
+
 def cpu_baseline(budget_s):
-    """CPU path timed beside the GPU path on this host, decode tokens over a rotating set of whole
-    LLaMA-7B layers (> LLC), tok/s = 1 / (32 x layer time).
+    """CPU path timed beside the GPU path on this host.
 
     kind "reference": the reference's own ggml.c (oracle/_ref, compiled from /root/reference by
-    oracle/Makefile, AVX2/FMA/F16C branches): the mul_mat nodes of the rotating layer copies in one
-    ggml graph per pass, one ggml_graph_compute each (oracle/ref_bench.c), as llama.cpp computes one
-    graph per token.  kind "port" (only when oracle/_ref was not built): the oracle's
-    AVX2 restatement with the same row split and per-call thread spawn."""
-    nthreads = int(os.environ.get("CPU_BASELINE_THREADS", min(16, os.cpu_count() or 1)))
+    oracle/Makefile): the "native" build (AVX-512 + AVX-VNNI: ggml.c's __AVXVNNI__ dpbusd branch,
+    what -march=native selects on the EPYC host) when the host has those extensions, else the AVX2
+    build (-march=x86-64-v3).  Decode = the 7 q4_0 mul_mats of a LLaMA-7B layer over 6 rotating layer
+    copies (> LLC), one ggml graph per pass as llama.cpp computes one graph per token (threads spawned
+    once per graph compute, ggml.c:17540-17571), tok/s = 1 / (32 x layer time), at P threads (P = this
+    process's CPU share) and at 1 thread; plus the spawn-per-mul_mat form (one graph per mul_mat), the
+    persistent-pool form (the oracle's AVX2 restatement of the same path, kind "port"), a 512-token
+    prefill layer, and BASELINE config 1 (test-quantize-perf q4_0 vec_dot over 4096 x 4096 values, one
+    thread).  Median / min / max over the samples.  kind "port" only when oracle/_ref was not built."""
+    P = int(os.environ.get("CPU_BASELINE_THREADS", min(16, os.cpu_count() or 1)))
     n_copies = 6                                   # ~680 MB of weights: beyond any host LLC
-    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_bench.so")
-    if os.path.exists(ref_so) and os.environ.get("CPU_BASELINE_KIND", "reference") == "reference":
-        import ctypes
-        R = ctypes.CDLL(ref_so)
-        R.ref_layers_create.restype = ctypes.c_void_p
-        R.ref_layers_create.argtypes = [ctypes.c_int, ctypes.c_int]
-        R.ref_layer_run.restype = ctypes.c_double
-        R.ref_layer_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-        R.ref_stack_run.restype = ctypes.c_double
-        R.ref_stack_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-        R.ref_layers_destroy.argtypes = [ctypes.c_void_p, ctypes.c_int]
-        h = R.ref_layers_create(n_copies, 1)
-        R.ref_stack_run(h, n_copies, nthreads)     # warm
-        total, n_layers_run = 0.0, 0
-        while total < budget_s:
-            total += R.ref_stack_run(h, n_copies, nthreads)
-            n_layers_run += n_copies
-        R.ref_layers_destroy(h, n_copies)
-        t = total / n_layers_run
-        kind = "reference"
-        what = ("reference ggml.c (oracle/_ref, -march=x86-64-v3): the layers' ggml_mul_mat nodes in one graph, "
-                f"one ggml_graph_compute per pass (as llama.cpp per token), n_threads={nthreads}")
-    else:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as O
-        base = []
-        for mi, (name, K, M) in enumerate(LAYER):
-            wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED0000 + mi, 0.0, 0.02).reshape(M, K))
-            base.append((K, wq))
-        layers = [[(K, wq.copy()) for K, wq in base] for _ in range(n_copies)]
-        x = {K: O.gaussian(K, 0x5EED1000 + K, 0.0, 1.0).reshape(1, K) for K in (4096, 11008)}
-        O.mul_mat(base[0][1], 4096, x[4096], nthreads=nthreads)   # warm
+    flags = _cpu_flags()
+    native_ok = {"avx512f", "avx512bw", "avx512vl", "avx_vnni"} <= flags
+    ref_dir = os.path.join(ROOT, "oracle", "_ref")
+    ref_so = os.path.join(ref_dir, "libref_bench_native.so" if native_ok else "libref_bench.so")
+    if not (os.path.exists(ref_so) and os.environ.get("CPU_BASELINE_KIND", "reference") == "reference"):
+        return cpu_baseline_port(budget_s, P, n_copies)
+    R = ctypes.CDLL(ref_so)
+    R.ref_layers_create.restype = ctypes.c_void_p
+    R.ref_layers_create.argtypes = [ctypes.c_int, ctypes.c_int]
+    for fn in (R.ref_layer_run, R.ref_stack_run):
+        fn.restype = ctypes.c_double
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    R.ref_layers_destroy.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    R.ref_vec_dot_bench.restype = ctypes.c_float
+    R.ref_vec_dot_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    t_start = time.time()
+
+    def samples(run, sample_s, n_min, n_max, budget):
+        """per-layer seconds of >= n_min samples of >= sample_s each, within budget seconds"""
+        out, t0 = [], time.time()
+        while len(out) < n_max and (len(out) < n_min or time.time() - t0 < budget):
+            tot, layers = 0.0, 0
+            while tot < sample_s or layers == 0:
+                dt, nl = run()
+                tot += dt
+                layers += nl
+            out.append(tot / layers)
+        return out
+
+    h = R.ref_layers_create(n_copies, 1)
+    R.ref_stack_run(h, n_copies, P)              # warm: page in every layer copy
+    dec_p = samples(lambda: (R.ref_stack_run(h, n_copies, P), n_copies), 0.8, 5, 12, 0.45 * budget_s)
+    dec_1 = samples(lambda: (R.ref_stack_run(h, n_copies, 1), n_copies), 0.2, 3, 5, 0.08 * budget_s)
+    k = [0]
+
+    def per_call():
+        k[0] += 1
+        return R.ref_layer_run(h, k[0] % n_copies, P), 1
+    dec_spawn = samples(per_call, 0.3, 3, 5, 0.1 * budget_s)
+    R.ref_layers_destroy(h, n_copies)
+    hp = R.ref_layers_create(1, 512)
+    R.ref_stack_run(hp, 1, P)
+    pre = samples(lambda: (R.ref_stack_run(hp, 1, P), 1), 0.0, 3, 3, 0.0)
+    R.ref_layers_destroy(hp, 1)
+    vd = np.zeros(20, np.float64)
+    R.ref_vec_dot_bench(4096 * 4096, vd.size, vd.ctypes.data_as(ctypes.c_void_p))
+    pool = cpu_baseline_port(0.1 * budget_s, P, 2, pool=True, n_min=3)
+
+    def tok(t):
+        return 1.0 / (32 * t)
+    dP, d1, dS = _stats(dec_p), _stats(dec_1), _stats(dec_spawn)
+    pre_s = _stats(pre)
+    pre_ops = 2 * 512 * sum(K * M for _, K, M in LAYER)
+    vd_s = _stats(vd)
+    build = ("-march=x86-64-v4 -mavxvnni (AVX-512 + AVX-VNNI: the __AVXVNNI__ dpbusd branch of ggml.c:647-657; "
+             "the host's -march=native set)" if native_ok else
+             "-march=x86-64-v3 (AVX2/FMA/F16C branches; the host lacks AVX-512/AVX-VNNI)")
+    return {
+        "value": round(tok(dP["median"]), 3), "unit": "tok/s", "cores": P, "kind": "reference",
+        "sample": (f"LLaMA-7B decode layers (7 q4_0 mul_mats, N=1) over {n_copies} rotating layer copies through the "
+                   f"reference ggml.c (oracle/_ref, {build}); one ggml graph per pass, one ggml_graph_compute with "
+                   f"{P} threads (this process's CPU share on the box); {dP['n']} samples of >= 0.8 s, median; "
+                   f"tok/s = 1/(32 x layer time)"),
+        "cpu": _cpu_name(), "host_cpus": os.cpu_count(), "build": build,
+        "decode": {
+            "threads_P": {"threads": P, "tok_s_median": round(tok(dP["median"]), 3),
+                          "tok_s_min": round(tok(dP["max"]), 3), "tok_s_max": round(tok(dP["min"]), 3),
+                          "ms_per_layer": round(dP["median"] * 1e3, 4), "samples": dP["n"]},
+            "threads_1": {"threads": 1, "tok_s_median": round(tok(d1["median"]), 3),
+                          "tok_s_min": round(tok(d1["max"]), 3), "tok_s_max": round(tok(d1["min"]), 3),
+                          "ms_per_layer": round(d1["median"] * 1e3, 4), "samples": d1["n"]},
+            "spawn_per_mul_mat_P": {"threads": P, "tok_s": round(tok(dS["median"]), 3),
+                                    "ms_per_layer": round(dS["median"] * 1e3, 4), "samples": dS["n"],
+                                    "note": "one ggml graph (one thread spawn) per mul_mat, ggml.c:17540-17571"},
+            "persistent_pool_P": pool,
+        },
+        "prefill_512": {"threads": P, "ms_per_layer": round(pre_s["median"] * 1e3, 2),
+                        "TOPs": round(pre_ops / pre_s["median"] / 1e12, 4),
+                        "stack_7B_ms": round(pre_s["median"] * 32 * 1e3, 1), "samples": pre_s["n"]},
+        "config1_vec_dot_4096x4096": {
+            "threads": 1, "us": round(vd_s["median"] * 1e6, 1), "us_min": round(vd_s["min"] * 1e6, 1),
+            "q4_0_GiB_s": round(4096 * 4096 // 32 * 18 / vd_s["min"] / 2**30, 3),
+            "ns_per_32_values": round(vd_s["min"] / (4096 * 4096 / 32) * 1e9, 3),
+            "note": "tests/test-quantize-perf.cpp --type q4_0 --op vec_dot_q --size 16777216; GiB/s of the q4_0 "
+                    "operand at the fastest of 20 calls, as that test reports"},
+        "seconds": round(time.time() - t_start, 1),
+    }
+
+
+def cpu_baseline_port(budget_s, nthreads, n_copies, pool=False, n_min=1):
+    """The oracle's AVX2 restatement of the same path (kind "port"): per mul_mat the q8_0 quantize
+    and the row-split vec_dot, threads spawned per call (ggml.c:17540-17571) or, with pool, a
+    persistent pool."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    base = []
+    for mi, (name, K, M) in enumerate(LAYER):
+        wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED0000 + mi, 0.0, 0.02).reshape(M, K))
+        base.append((K, wq))
+    layers = [[(K, wq.copy()) for K, wq in base] for _ in range(n_copies)]
+    x = {K: O.gaussian(K, 0x5EED1000 + K, 0.0, 1.0).reshape(1, K) for K in (4096, 11008)}
+    O.mul_mat(base[0][1], 4096, x[4096], nthreads=nthreads, mode="avx2", pool=pool)   # warm
+    per = []
+    t_all = time.perf_counter()
+    while len(per) < n_min or time.perf_counter() - t_all < budget_s:
         t0 = time.perf_counter()
-        n_layers_run = 0
-        while True:
-            for K, wq in layers[n_layers_run % n_copies]:
-                O.mul_mat(wq, K, x[K], nthreads=nthreads, mode="avx2", pool=False)
-            n_layers_run += 1
-            if time.perf_counter() - t0 > budget_s:
-                break
-        t = (time.perf_counter() - t0) / n_layers_run
-        kind = "port"
-        what = (f"oracle AVX2 restatement, {nthreads} threads spawned per mul_mat, "
-                f"AVX2={bool(O.lib().oracle_have_avx2())}")
-    return {"value": round(1.0 / (32 * t), 3), "unit": "tok/s", "cores": nthreads, "kind": kind,
-            "sample": f"{n_layers_run} LLaMA-7B decode layers (7 q4_0 mul_mats each, N=1) over {n_copies} "
-                      f"rotating layer copies; {what}; {budget_s:.0f}s budget; tok/s = 1/(32 x mean layer time)",
-            "ms_per_layer": round(t * 1e3, 3), "cpu": _cpu_name()}
+        for K, wq in layers[len(per) % n_copies]:
+            O.mul_mat(wq, K, x[K], nthreads=nthreads, mode="avx2", pool=pool)
+        per.append(time.perf_counter() - t0)
+    st = _stats(per)
+    note = (f"oracle AVX2 restatement of quantize_row_q8_0 + ggml_vec_dot_q4_0_q8_0 + the row split, "
+            f"{nthreads} threads {'in a persistent pool' if pool else 'spawned per mul_mat'}, "
+            f"AVX2={bool(O.lib().oracle_have_avx2())}")
+    if pool:
+        return {"threads": nthreads, "tok_s": round(1.0 / (32 * st["median"]), 3),
+                "ms_per_layer": round(st["median"] * 1e3, 4), "samples": st["n"], "kind": "port", "note": note}
+    return {"value": round(1.0 / (32 * st["median"]), 3), "unit": "tok/s", "cores": nthreads, "kind": "port",
+            "ms_per_layer": round(st["median"] * 1e3, 4), "samples": st["n"], "sample": note, "cpu": _cpu_name()}
 
 
 if __name__ == "__main__":

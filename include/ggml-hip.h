@@ -104,6 +104,17 @@ int    ggml_cpu_has_hipblas(void);
  * GGML_HIP_WEIGHT_CACHE=0.  Counters since the last clear; clear frees every cached copy. */
 int    ggml_hip_weight_cache_stats(int64_t *hits, int64_t *misses, int64_t *resident_bytes);
 int    ggml_hip_weight_cache_clear(void);
+/* Host writes into cached weights.  Writes made by ggml nodes (the reference's LoRA apply rewrites
+ * Q4_0 weights in place through ggml_add_inplace / ggml_cpy graphs, llama.cpp:2950-2967) are seen
+ * by ggml_hip_compute_forward's INIT phase and invalidate the overlapping copies exactly.  A host
+ * that edits weight bytes outside ggml calls ggml_hip_weight_cache_invalidate(ptr, bytes) (drops
+ * every copy overlapping [ptr, ptr+bytes), bytes 0 = the copies containing ptr; returns how many,
+ * or a negative status), or runs with GGML_HIP_WEIGHT_CACHE_VERIFY=full / set_verify(1): every
+ * lookup then fingerprints every byte of the host weight (exact; one host read per call; -1 =
+ * environment, 0 = sampled fingerprint). */
+int64_t ggml_hip_weight_cache_invalidate(const void *host, size_t bytes);
+int    ggml_hip_weight_cache_set_verify(int mode);
+int64_t ggml_hip_weight_cache_invalidations(void);
 
 /* ------------------------------------------------------------------------------------------
  * Tensor-free entry points (device pointers, stream-ordered on `stream` = hipStream_t or NULL

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <memory>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -255,7 +256,8 @@ std::mutex g_host_copy_mu;
 std::unordered_map<const void *, void *> g_host_copies;
 std::unordered_map<WCacheKey, WCacheEntry, WCacheHash> g_wc;
 size_t g_wc_resident = 0;
-uint64_t g_wc_clock = 0, g_wc_hits = 0, g_wc_misses = 0;
+uint64_t g_wc_clock = 0, g_wc_hits = 0, g_wc_misses = 0, g_wc_invalidations = 0;
+std::atomic<uintptr_t> g_wc_lo{UINTPTR_MAX}, g_wc_hi{0};   // hull of the cached host ranges (monotone)
 
 bool wcache_enabled() {
     static const bool on = !getenv("GGML_HIP_WEIGHT_CACHE") || atoi(getenv("GGML_HIP_WEIGHT_CACHE")) != 0;
@@ -266,8 +268,37 @@ size_t wcache_budget() {
     return mb << 20;
 }
 
+// GGML_HIP_WEIGHT_CACHE_VERIFY=full: fingerprint every byte on every lookup (exact, one host read of
+// the weight per call); default "sampled" (below).  In-place host writes that go through ggml nodes
+// are caught exactly either way (wcache_note_host_write), and ggml_hip_weight_cache_invalidate
+// covers writes made outside ggml.
+int wcache_verify_full() {
+    static const int full = [] {
+        const char *e = getenv("GGML_HIP_WEIGHT_CACHE_VERIFY");
+        return e && (strcmp(e, "full") == 0 || strcmp(e, "1") == 0) ? 1 : 0;
+    }();
+    return full;
+}
+std::atomic<int> g_wc_verify_override{-1};
+
+// every byte: 8-byte words through a multiply-xorshift chain (~10 GB/s on one core)
+uint64_t wcache_fingerprint_full(const uint8_t *p, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+        h ^= h >> 32;
+    }
+    for (; i < n; i++) h = (h ^ p[i]) * 1099511628211ull;
+    return h;
+}
+
 // FNV-1a over the first and last 32 bytes and 64 evenly spaced 8-byte samples
 uint64_t wcache_fingerprint(const uint8_t *p, size_t n) {
+    const int ov = g_wc_verify_override.load(std::memory_order_relaxed);
+    if (ov > 0 || (ov < 0 && wcache_verify_full())) return wcache_fingerprint_full(p, n);
     uint64_t h = 1469598103934665603ull ^ n;
     auto mix = [&](const uint8_t *q, size_t len) {
         for (size_t i = 0; i < len; i++) h = (h ^ q[i]) * 1099511628211ull;
@@ -315,7 +346,43 @@ const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, ui
     HIP_FATAL(hipMemcpyAsync(e.dev, host, bytes, hipMemcpyHostToDevice, s));
     g_wc_resident += bytes;
     g_wc[key] = e;
+    const uintptr_t lo = (uintptr_t)host, hi = lo + bytes;
+    if (lo < g_wc_lo.load()) g_wc_lo.store(lo);
+    if (hi > g_wc_hi.load()) g_wc_hi.store(hi);
     return e.dev;
+}
+
+// drop every cached copy whose host range overlaps [host, host + bytes) (bytes == 0: contains host);
+// the next mul_mat re-uploads.  Returns the number of copies dropped.
+int64_t wcache_invalidate(const void *host, size_t bytes) {
+    const uintptr_t lo = (uintptr_t)host, hi = lo + (bytes ? bytes : 1);
+    std::lock_guard<std::mutex> lk(g_wc_mu);
+    int64_t n = 0;
+    for (auto it = g_wc.begin(); it != g_wc.end();) {
+        const uintptr_t a = (uintptr_t)it->first.host, b = a + it->first.bytes;
+        if (a < hi && lo < b) {
+            HIP_FATAL(hipFree(it->second.dev));   // hipFree waits for work that still reads it
+            g_wc_resident -= it->second.bytes;
+            it = g_wc.erase(it);
+            n++;
+            g_wc_invalidations++;
+        } else {
+            ++it;
+        }
+    }
+    return n;
+}
+
+// A ggml node about to write host memory [data, data + bytes) (every node's INIT phase, ggml.c:
+// 17112-17116): cached copies of weights in that range are dropped.  This is the path of the
+// reference's LoRA apply, which rewrites quantized weights in place through ggml_add_inplace /
+// ggml_cpy graphs (llama.cpp:2950-2967).  One range test when nothing cached overlaps.
+void wcache_note_host_write(const void *data, size_t bytes) {
+    const uintptr_t lo = (uintptr_t)data, hi = lo + bytes;
+    if (!data || bytes == 0 || lo >= g_wc_hi.load(std::memory_order_relaxed) ||
+        hi <= g_wc_lo.load(std::memory_order_relaxed))
+        return;
+    wcache_invalidate(data, bytes);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -815,6 +882,87 @@ bool fuse_enabled() {
     return v == 1;
 }
 
+// ---- held-node snapshots (graph lifetime).  A held node (pending chain, group member, node held
+// behind a group) can outlive its ggml_graph_compute: a caller may end a graph on a device-only node
+// and ggml_free the context before the next backend call flushes it.  Every node is therefore copied
+// when it is held, with its operands two levels deep, into a backend-owned arena; the copies carry
+// everything a deferred launch reads (shapes, strides, extras, the host scalar parameters of scale /
+// rope / diag_mask_inf), and flushes run on the copies only.  Identity tests against an arriving
+// node (t->src0 == held) compare the original address AND the original's fields at hold time, so a
+// new graph that reuses a freed address never fuses with a stale node.
+struct SnapTensor {
+    tensor t;                  // working copy: src0 / src1 -> copies, host parameters -> param
+    const tensor *orig = nullptr;
+    tensor pristine;           // the original's bytes when it was copied
+    int depth = -1;
+    alignas(16) uint8_t param[16];
+};
+constexpr size_t SNAP_BLOCK = 1024;
+struct SnapArena {
+    std::vector<std::unique_ptr<SnapTensor[]>> blocks;     // stable addresses
+    size_t used = 0;
+    std::unordered_map<const tensor *, SnapTensor *> memo;  // original -> copy
+};
+SnapArena g_snaps;
+
+bool is_snap(const tensor *t) {
+    for (const auto &b : g_snaps.blocks)
+        if ((const char *)t >= (const char *)b.get() && (const char *)t < (const char *)(b.get() + SNAP_BLOCK)) return true;
+    return false;
+}
+// the fields a graph does not change after building it (n_tasks and the perf counters excluded)
+bool stable_equal(const tensor *a, const tensor *b) {
+    return memcmp(a, b, offsetof(tensor, n_tasks)) == 0 &&
+           memcmp(&a->data, &b->data, offsetof(tensor, padding) - offsetof(tensor, data)) == 0;
+}
+tensor *snap(tensor *t, int depth) {
+    if (!t || is_snap(t)) return t;
+    auto it = g_snaps.memo.find(t);
+    SnapTensor *c = nullptr;
+    if (it != g_snaps.memo.end() && stable_equal(t, &it->second->pristine)) {
+        c = it->second;
+        if (c->depth >= depth) return &c->t;
+    } else {                   // new, or a freed address reused by another tensor: a fresh copy
+        const size_t bi = g_snaps.used / SNAP_BLOCK;
+        if (bi == g_snaps.blocks.size()) g_snaps.blocks.emplace_back(new SnapTensor[SNAP_BLOCK]);
+        c = &g_snaps.blocks[bi][g_snaps.used % SNAP_BLOCK];
+        g_snaps.used++;
+        c->t = *t;
+        c->pristine = *t;
+        c->orig = t;
+        c->t.grad = nullptr;
+        for (int i = 0; i < gabi::MAX_OPT; i++) c->t.opt[i] = nullptr;
+        c->t.src0 = c->t.src1 = nullptr;
+        if (t->backend == gabi::BACKEND_CPU && t->data && (t->type == gabi::TYPE_F32 || t->type == gabi::TYPE_I32) &&
+            gabi::nbytes(t) <= sizeof(c->param)) {
+            memcpy(c->param, t->data, gabi::nbytes(t));
+            c->t.data = c->param;
+        }
+        g_snaps.memo[t] = c;
+    }
+    c->depth = depth;
+    if (depth > 0) {           // t is the live original here: it is being held right now
+        c->t.src0 = snap(t->src0, depth - 1);
+        c->t.src1 = snap(t->src1, depth - 1);
+    }
+    return &c->t;
+}
+tensor *hold(tensor *t) { return snap(t, 2); }
+void snap_reset() {
+    g_snaps.used = 0;
+    g_snaps.memo.clear();
+}
+// is x (arriving, or a copy) the tensor h (a held copy)?
+bool same_tensor(const tensor *x, const tensor *h) {
+    if (x == h) return true;
+    if (!x || !h) return false;
+    const bool sx = is_snap(x), sh = is_snap(h);
+    if (sx == sh) return false;            // two copies (one per tensor) or two live originals
+    const SnapTensor *c = (const SnapTensor *)(sh ? h : x);
+    const tensor *o = sh ? x : h;
+    return o == c->orig && stable_equal(o, &c->pristine);
+}
+
 struct Pending {
     int n = 0;
     tensor *node[4] = {};
@@ -895,18 +1043,18 @@ bool try_fuse(tensor *t) {
     const int id = g_main_device;
     hipStream_t s = g_dev[id].stream;
     // add -> rms_norm(sum): extend
-    if (p.n == 1 && last->op == gabi::OP_ADD && t->op == gabi::OP_RMS_NORM && t->src0 == last && deferrable(t)) {
-        p.node[p.n++] = t;
+    if (p.n == 1 && last->op == gabi::OP_ADD && t->op == gabi::OP_RMS_NORM && same_tensor(t->src0, last) && deferrable(t)) {
+        p.node[p.n++] = hold(t);
         return true;
     }
     // scale -> diag_mask_inf(scaled): extend
-    if (p.n == 1 && last->op == gabi::OP_SCALE && t->op == gabi::OP_DIAG_MASK_INF && t->src0 == last && dev_f32(t) &&
+    if (p.n == 1 && last->op == gabi::OP_SCALE && t->op == gabi::OP_DIAG_MASK_INF && same_tensor(t->src0, last) && dev_f32(t) &&
         same_shape(t, last) && host_scalar_param(t->src1)) {
-        p.node[p.n++] = t;
+        p.node[p.n++] = hold(t);
         return true;
     }
     // [add ->] rms_norm -> mul(norm weight row): complete
-    if (last->op == gabi::OP_RMS_NORM && t->op == gabi::OP_MUL && t->src0 == last && dev_f32(t) && same_shape(t, last) &&
+    if (last->op == gabi::OP_RMS_NORM && t->op == gabi::OP_MUL && same_tensor(t->src0, last) && dev_f32(t) && same_shape(t, last) &&
         dev_f32(t->src1) && t->src1->ne[0] == t->ne[0] && t->src1->ne[1] == 1 && t->src1->ne[2] == 1 && t->src1->ne[3] == 1) {
         const tensor *add = p.n == 2 ? p.node[0] : nullptr;
         const tensor *x = add ? add : last->src0;     // the rms_norm input
@@ -924,22 +1072,22 @@ bool try_fuse(tensor *t) {
     // scale -> diag_mask_inf -> soft_max: held (completed as one launch by flush_pending, or with
     // the KQV that follows at decode)
     if (p.n == 2 && p.node[0]->op == gabi::OP_SCALE && last->op == gabi::OP_DIAG_MASK_INF && t->op == gabi::OP_SOFT_MAX &&
-        t->src0 == last && dev_f32(t) && same_shape(t, last)) {
-        p.node[p.n++] = t;
+        same_tensor(t->src0, last) && dev_f32(t) && same_shape(t, last)) {
+        p.node[p.n++] = hold(t);
         return true;
     }
     // soft_max chain -> KQV (f16 V^T . softmax, one query row per head): extend
-    if (p.n == 3 && softmax_chain(p) && t->op == gabi::OP_MUL_MAT && t->src1 == last && t->src0 &&
+    if (p.n == 3 && softmax_chain(p) && t->op == gabi::OP_MUL_MAT && same_tensor(t->src1, last) && t->src0 &&
         t->src0->type == gabi::TYPE_F16 && t->src0->backend == gabi::BACKEND_GPU && t->src0->extra &&
         t->src0->nb[0] == 2 && t->src0->ne[3] == 1 && last->ne[1] == 1 && last->ne[3] == 1 &&
         t->src0->ne[0] == last->ne[0] && t->src0->ne[2] == last->ne[2] && last->ne[0] <= 16384 && dev_f32(t) &&
         t->ne[1] == 1 && t->ne[0] == t->src0->ne[1] && dev_f32(p.node[0]->src0)) {
-        p.node[p.n++] = t;
+        p.node[p.n++] = hold(t);
         return true;
     }
     // soft_max chain -> KQV -> cpy(permute(KQV)) (the merged heads): complete as one launch
     if (p.n == 4 && softmax_chain(p) && t->op == gabi::OP_CPY && t->src0 && t->src0->op == gabi::OP_PERMUTE &&
-        t->src0->src0 == last) {
+        same_tensor(t->src0->src0, last)) {
         const tensor *m = t->src0, *cb = t->src1;
         if (m->ne[0] == last->ne[0] && m->ne[1] == last->ne[2] && m->ne[2] == last->ne[1] && m->ne[3] == 1 &&
             m->nb[0] == 4 && m->nb[1] == last->nb[2] && m->nb[2] == last->nb[1] && dev_f32(cb) &&
@@ -963,7 +1111,7 @@ bool try_fuse(tensor *t) {
         }
     }
     // silu -> mul(silu, b): complete
-    if (p.n == 1 && last->op == gabi::OP_SILU && t->op == gabi::OP_MUL && t->src0 == last && dev_f32(t) &&
+    if (p.n == 1 && last->op == gabi::OP_SILU && t->op == gabi::OP_MUL && same_tensor(t->src0, last) && dev_f32(t) &&
         same_shape(t, last) && dev_f32(t->src1) && same_shape(t, t->src1)) {
         const OpTables &tb = op_tables(id, s);
         HIP_FATAL(hipSetDevice(id));
@@ -976,7 +1124,7 @@ bool try_fuse(tensor *t) {
         return true;
     }
     // rope -> cpy(rope, strided device view): complete (the K cache store)
-    if (p.n == 1 && last->op == gabi::OP_ROPE && t->op == gabi::OP_CPY && t->src0 == last && t->src1 &&
+    if (p.n == 1 && last->op == gabi::OP_ROPE && t->op == gabi::OP_CPY && same_tensor(t->src0, last) && t->src1 &&
         t->src1->backend == gabi::BACKEND_GPU && t->src1->extra &&
         (t->src1->type == gabi::TYPE_F16 || t->src1->type == gabi::TYPE_F32) && t->src1->ne[3] == 1 &&
         t->src1->ne[0] * t->src1->ne[1] * t->src1->ne[2] == last->ne[0] * last->ne[1] * last->ne[2] &&
@@ -989,7 +1137,7 @@ bool try_fuse(tensor *t) {
     }
     // f16 mul_mat -> cpy(permute(mul_mat, 0, 2, 1, 3), contiguous f32): complete (KQV_merged_contiguous)
     if (p.n == 1 && last->op == gabi::OP_MUL_MAT && t->op == gabi::OP_CPY && t->src0 && t->src0->op == gabi::OP_PERMUTE &&
-        t->src0->src0 == last) {
+        same_tensor(t->src0->src0, last)) {
         const tensor *m = t->src0, *cb = t->src1;
         if (m->ne[0] == last->ne[0] && m->ne[1] == last->ne[2] && m->ne[2] == last->ne[1] && m->ne[3] == 1 &&
             last->ne[3] == 1 && m->nb[0] == 4 && m->nb[1] == last->nb[2] && m->nb[2] == last->nb[1] && dev_f32(cb) &&
@@ -1093,7 +1241,7 @@ bool group_after_ok(const tensor *t) {
 // may q4_0 mul_mat m run before every held node and beside the current members?
 bool group_join_ok(const tensor *m) {
     const Group &g = g_grp;
-    if (g.n >= 4 || m->src1 != g.mm[0]->src1 || m->src0->ne[0] != g.mm[0]->src0->ne[0]) return false;
+    if (g.n >= 4 || !same_tensor(m->src1, g.mm[0]->src1) || m->src0->ne[0] != g.mm[0]->src0->ne[0]) return false;
     for (int i = 0; i < g.n; i++)
         if (dev_overlap(m, g.mm[i]) || dev_overlap(m, g.mm[i]->src1)) return false;
     for (int i = 0; i < g.na; i++) {
@@ -1248,7 +1396,7 @@ void execute_node(tensor *t) {
     }
     if (g_grp.n > 0) {
         if (group_mm_ok(t) && group_join_ok(t)) {
-            g_grp.mm[g_grp.n++] = t;
+            g_grp.mm[g_grp.n++] = hold(t);
             return;
         }
         if (trace_nodes())
@@ -1256,13 +1404,13 @@ void execute_node(tensor *t) {
                     group_mm_ok(t) ? (int)group_join_ok(t) : -1, (int)group_after_ok(t));
         if (!(op == gabi::OP_MUL_MAT && t->src0 && t->src0->type != gabi::TYPE_F16) && group_after_ok(t) &&
             g_grp.na < 16) {
-            g_grp.after[g_grp.na++] = t;
+            g_grp.after[g_grp.na++] = hold(t);
             return;
         }
         flush_group();
     }
     if (g_pend.n == 0 && group_mm_ok(t)) {
-        g_grp.mm[0] = t;
+        g_grp.mm[0] = hold(t);
         g_grp.n = 1;
         return;
     }
@@ -1270,13 +1418,13 @@ void execute_node(tensor *t) {
         if (try_fuse(t)) return;
         flush_pending();
         if (group_mm_ok(t)) {
-            g_grp.mm[0] = t;
+            g_grp.mm[0] = hold(t);
             g_grp.n = 1;
             return;
         }
     }
     if (deferrable(t)) {
-        g_pend.node[g_pend.n++] = t;
+        g_pend.node[g_pend.n++] = hold(t);
         return;
     }
     if (t->op == gabi::OP_MUL_MAT && t->src0 && t->src0->type != gabi::TYPE_F16) {
@@ -1658,6 +1806,11 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
     // KV cache) and the other ops of a LLaMA layer -> ggml_ops.hip; views are free.
     const gabi::compute_params *params = (const gabi::compute_params *)params_;
     tensor *t = (tensor *)tensor_;
+    // a host write into cached weights (LoRA apply) invalidates their device copies; INIT runs once per
+    // node, before any thread writes (ggml.c:17112-17116)
+    if (params->type == gabi::TASK_INIT && t->backend == gabi::BACKEND_CPU && t->data && t->op != gabi::OP_NONE &&
+        t->op != gabi::OP_VIEW && t->op != gabi::OP_RESHAPE && t->op != gabi::OP_PERMUTE && t->op != gabi::OP_TRANSPOSE)
+        wcache_note_host_write(t->data, span_bytes(t));   // (views of a weight write nothing)
     const bool any_on_device = t->backend == gabi::BACKEND_GPU || on_device(t->src0) ||
                                (t->src1 && t->src1->backend == gabi::BACKEND_GPU);
     bool f16_mul_mat = false;
@@ -1702,6 +1855,11 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
                 t->src1 ? t->src1->name : "-");
     const auto t0 = std::chrono::steady_clock::now();
     (void)f16_mul_mat;
+    if (g_grp.n == 0 && g_pend.n == 0) {
+        snap_reset();                      // nothing held: the copies are garbage
+    } else if (g_snaps.memo.count(t)) {
+        flush_deferred();                  // t arrives again: a new graph at the old addresses
+    }
     execute_node(t);
     const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     g_host_ns.fetch_add(ns, std::memory_order_relaxed);
@@ -2158,8 +2316,27 @@ int ggml_hip_weight_cache_clear(void) {
     for (auto &e : g_wc) HIP_RET(hipFree(e.second.dev));
     g_wc.clear();
     g_wc_resident = 0;
-    g_wc_hits = g_wc_misses = 0;
+    g_wc_hits = g_wc_misses = g_wc_invalidations = 0;
+    g_wc_lo.store(UINTPTR_MAX);
+    g_wc_hi.store(0);
     return GGML_HIP_OK;
+}
+
+int64_t ggml_hip_weight_cache_invalidate(const void *host, size_t bytes) {
+    if (!host) return GGML_HIP_ERR_INVALID;
+    flush_deferred();
+    return wcache_invalidate(host, bytes);
+}
+
+int ggml_hip_weight_cache_set_verify(int mode) {
+    if (mode < -1 || mode > 1) return fail(GGML_HIP_ERR_INVALID, "verify mode must be -1, 0 or 1");
+    g_wc_verify_override.store(mode);
+    return GGML_HIP_OK;
+}
+
+int64_t ggml_hip_weight_cache_invalidations(void) {
+    std::lock_guard<std::mutex> lk(g_wc_mu);
+    return (int64_t)g_wc_invalidations;
 }
 
 // ------------------------------------------------------------------------------------------

@@ -25,6 +25,7 @@ namespace ghip {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void_t;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
@@ -330,6 +331,8 @@ struct GemvMats {
 //                     wave's first weight issue, so the x loads are ahead of all of the workgroup's
 //                     weight loads in the CU's memory pipeline (phase stamps: without it the x data
 //                     returned together with the weights, and the prologue barrier gated compute)
+// VAR bit 3 (XHOLD, with XFIRST): the x-waves issue their own weight loads only after x is in LDS
+//                     (the other waves stream weights from the start)
 // PPL > 0 ("row items", decode, K <= 12288): lane l takes pairs l, l+64, ..., l+64*(PPL-1) of the
 //                     row (PPL = ceil(pairs/64)), so one item is a whole row: all of its loads are
 //                     in flight together and it is reduced once (a row of K=4160 no longer costs two
@@ -419,7 +422,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
         }
     };
     auto item_row = [&](int it) __attribute__((always_inline)) { return row0 + (it / nchunk) * rstride; };
-    constexpr bool GLB = (VAR & 1) != 0, XSPLIT = (VAR & 2) != 0, XFIRST = (VAR & 4) != 0;
+    constexpr bool GLB = (VAR & 1) != 0, XSPLIT = (VAR & 2) != 0, XFIRST = (VAR & 4) != 0, XHOLD = (VAR & 8) != 0;
     static_assert(PPL == 0 || GLB, "row items use the global-load form");
     auto issue = [&](int it) __attribute__((always_inline)) {
         const bool valid = it < nitems;                             // past the end: zero-size descriptor
@@ -457,8 +460,10 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
             }
             __builtin_amdgcn_s_barrier();                           // x loads issued before any weight
             asm volatile("" ::: "memory");
+            if (!XHOLD || wave >= XW) {
 #pragma unroll
-            for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+                for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+            }
             GEMV_STAMP(1);
             if (wave < XW) {
 #pragma unroll
@@ -469,6 +474,13 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
                         xw[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * XT), 0, 0);
 #pragma unroll
                     for (int i = 0; i < GEMV_XPRO; i++) quantize_into_lds(xw[i], base + tid + i * XT);
+                }
+                // XHOLD: an x-wave's own weight loads enter the CU's queue only after x is in LDS.
+                // Issue blocks once ~30-40 KB per CU are outstanding (phase stamps), so a wave that
+                // issued its weights first would sit behind them before it could quantize.
+                if constexpr (XHOLD) {
+#pragma unroll
+                    for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
                 }
             }
         } else if (wave < XW) {
@@ -554,7 +566,10 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
             const int r = item_row(it);
             const bool g1 = r >= rb1, g2 = r >= rb2, g3 = r >= rb3;
             const int rb = (g1 ? rb1 : 0) + (g2 ? rb2 - rb1 : 0) + (g3 ? rb3 - rb2 : 0);
-            float *yo = reinterpret_cast<float *>(y0 + (g1 ? yd1 : 0) + (g2 ? yd2 : 0) + (g3 ? yd3 : 0)) + (r - rb);
+            // global (not flat) store: a flat store also counts in lgkmcnt, so the next item's LDS
+            // waits would wait for its memory round trip
+            typedef __attribute__((address_space(1))) float gfloat;
+            gfloat *yo = reinterpret_cast<gfloat *>(y0 + (g1 ? yd1 : 0) + (g2 ? yd2 : 0) + (g3 ? yd3 : 0)) + (r - rb);
             const int64_t ld = l0 + (g1 ? ld1 : 0) + (g2 ? ld2 : 0) + (g3 ? ld3 : 0);
             float out = 0.0f;
 #pragma unroll
@@ -683,15 +698,17 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
     if constexpr (NT == 1) {                        // decode: one item per row (PPL pairs per lane)
         const int rowitems = gemv_policy().rowitems;
         const int ppl = (int)((K / 64 + 63) / 64);
-        if (rowitems && (var == 3 || var == 7) && ppl <= 3) {
+        if (rowitems && (var == 3 || var == 7 || var == 15) && ppl <= 3) {
             // two rows in flight per wave, except the multi-round strided case (M > 2*CUs*16 with
             // the leftover rows a whole round per CU, e.g. the fused LLaMA-7B wq|wk|wv, M = 12288)
             const int64_t M = m.row_begin[m.n], r1 = 2 * (int64_t)dev.num_cus * 16;
             const bool strided_multi = M > r1 && (M % r1) % (r1 / 2) == 0;
             const int rd = depth_env ? depth_env : (strided_multi ? 1 : 2);
-            if (diag == 7) return var == 7 ? launch_gemv_rows<NT, 7, 7>(m, K, x, dev, s, ppl, rd)
-                                           : launch_gemv_rows<NT, 7, 3>(m, K, x, dev, s, ppl, rd);
-            return var == 7 ? launch_gemv_rows<NT, 0, 7>(m, K, x, dev, s, ppl, rd)
+            if (diag == 7) return var == 15 ? launch_gemv_rows<NT, 7, 15>(m, K, x, dev, s, ppl, rd)
+                                  : var == 7 ? launch_gemv_rows<NT, 7, 7>(m, K, x, dev, s, ppl, rd)
+                                             : launch_gemv_rows<NT, 7, 3>(m, K, x, dev, s, ppl, rd);
+            return var == 15 ? launch_gemv_rows<NT, 0, 15>(m, K, x, dev, s, ppl, rd)
+                 : var == 7 ? launch_gemv_rows<NT, 0, 7>(m, K, x, dev, s, ppl, rd)
                             : launch_gemv_rows<NT, 0, 3>(m, K, x, dev, s, ppl, rd);
         }
         // K > 12288: chunked items below (measured equal or faster at 4-5 pairs per lane)
@@ -1245,8 +1262,6 @@ static constexpr int G7_LDS = G7_NX * (G7_X + G7_XD) + 2 * (G7_W + G7_WD);   // 
 static constexpr int G7_OPS = 3 + 2 + 1;                        // per thread per stage: W pair, 2 x glds, d_x glds
 static_assert(G7_X / 1024 == 2 * GM_WAVES, "two 1-KiB activation DMA instructions per wave per stage");
 static_assert(G7_XD / 256 == GM_WAVES, "one 256-B d_x DMA instruction per wave per stage");
-
-typedef __attribute__((address_space(3))) void lds_void_t;
 
 struct G7W {
     u32x4 wa, wb;

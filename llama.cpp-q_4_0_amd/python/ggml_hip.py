@@ -70,6 +70,9 @@ def _bind(L):
         "ggml_hip_mul_mat_q4_0_split_multi": ([vp, i32, vp, vp, vp, i64, vp, i64, vp, vp], i32),
         "ggml_hip_weight_cache_stats": ([vp, vp, vp], i32),
         "ggml_hip_weight_cache_clear": ([], i32),
+        "ggml_hip_weight_cache_invalidate": ([vp, sz], i64),
+        "ggml_hip_weight_cache_set_verify": ([i32], i32),
+        "ggml_hip_weight_cache_invalidations": ([], i64),
         "ggml_hip_set_exact": ([i32], i32),
         "ggml_hip_get_exact": ([], i32),
         "ggml_hip_device_count": ([], i32),

@@ -14,6 +14,7 @@
 #define _POSIX_C_SOURCE 199309L
 #include "ggml.h"
 
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -84,4 +85,39 @@ void ref_layers_destroy(void *h, int n_layers) {
     struct ref_layer *L = (struct ref_layer *)h;
     for (int l = 0; l < n_layers; l++) ggml_free(L[l].ctx);
     free(L);
+}
+
+/* BASELINE config 1: tests/test-quantize-perf.cpp --type q4_0 --op vec_dot_q --size 16777216 (one
+ * 4096 x 4096-value dot on one thread, test-quantize-perf.cpp:339-349; data 0.1 + 2 cos(i + offset),
+ * :64-68).  The second operand is quantized with quantize_row_q_dot (q8_0, what the dot reads;
+ * test-quantize-perf hands it a q4_0 buffer, which times the same loop).  Per-call seconds of `reps`
+ * timed calls after 5 warm-up calls (the test's WARMUP) go to sec[]; returns the dot value. */
+float ref_vec_dot_bench(int size, int reps, double *sec) {
+    float *a = malloc((size_t)size * 4), *b = malloc((size_t)size * 4);
+    void *qa = aligned_alloc(64, ((size_t)size / 32 * 18 + 63) / 64 * 64);
+    void *qb = aligned_alloc(64, ((size_t)size / 32 * 34 + 63) / 64 * 64);
+    for (int i = 0; i < size; i++) {
+        a[i] = 0.1f + 2 * cosf((float)i + 0.0f);
+        b[i] = 0.1f + 2 * cosf((float)i + 1.0f);
+    }
+    struct ggml_init_params ip = {1024, NULL, true};       /* fp16 tables (ggml_init) */
+    struct ggml_context *ctx = ggml_init(ip);
+    const quantize_fns_t f = ggml_internal_get_quantize_fn(GGML_TYPE_Q4_0);
+    f.quantize_row_q(a, qa, size);
+    f.quantize_row_q_dot(b, qb, size);
+    float r = 0.0f;
+    for (int i = 0; i < 5; i++) f.vec_dot_q(size, &r, qa, qb);
+    for (int i = 0; i < reps; i++) {
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        f.vec_dot_q(size, &r, qa, qb);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        sec[i] = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    }
+    ggml_free(ctx);
+    free(a);
+    free(b);
+    free(qa);
+    free(qb);
+    return r;
 }

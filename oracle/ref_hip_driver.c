@@ -11,7 +11,14 @@
 #include "ggml-cuda.h"
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+
+/* from include/ggml-hip.h (libggml_hip.so, loaded as the shim's dependency) */
+int ggml_hip_device_synchronize(void);
+int ggml_hip_memcpy_d2h(void *dst, const void *src, size_t size, void *stream);
+int ggml_hip_weight_cache_stats(int64_t *hits, int64_t *misses, int64_t *resident_bytes);
+int64_t ggml_hip_weight_cache_invalidations(void);
 
 /* y[N][M] = mul_mat(W q4_0 [M][K], x f32 [N][K]) through ggml_graph_compute with n_threads.
  * offload: 0 = weight stays a CPU tensor (ggml decides via can_mul_mat: N >= 32 goes to the GPU
@@ -44,3 +51,81 @@ int refhip_mul_mat(const void *wq, int K, int M, const float *x, int N, float *y
 
 /* 1 when this ggml.c was built with the GPU backend hooks (ggml.c:19465-19470) */
 int refhip_has_gpublas(void) { return ggml_cpu_has_cublas(); }
+
+/* The reference's LoRA apply (llama.cpp:2935-2967) rewrites a Q4_0 weight in place with a ggml graph
+ * (ggml_add_inplace(w, BA) -> ggml_compute_forward_add_q_f32).  Here: y_before = W x (N >= 32: the
+ * backend takes it and caches the CPU weight), then W += delta by ggml_add_inplace on the CPU, then
+ * y_after = W x again through the backend.  wq_after receives the rewritten weight bytes; counts[0..2] =
+ * cache hits, misses, invalidations after the last mul_mat.  Returns 0, or -1 on error. */
+int refhip_lora_add(const void *wq, int K, int M, const float *x, int N, const float *delta, float *y_before,
+                    float *y_after, void *wq_after, int64_t *counts, int n_threads) {
+    const size_t wbytes = (size_t)M * (K / 32) * 18;
+    const size_t need = wbytes + (size_t)K * N * 4 + (size_t)K * M * 4 + 2 * (size_t)M * N * 4 + (4u << 20);
+    struct ggml_init_params ip = {need, NULL, false};
+    struct ggml_context *ctx = ggml_init(ip);
+    if (!ctx) return -1;
+    struct ggml_tensor *w = ggml_new_tensor_2d(ctx, GGML_TYPE_Q4_0, K, M);
+    struct ggml_tensor *xt = ggml_new_tensor_2d(ctx, GGML_TYPE_F32, K, N);
+    struct ggml_tensor *dt = ggml_new_tensor_2d(ctx, GGML_TYPE_F32, K, M);
+    memcpy(w->data, wq, wbytes);
+    memcpy(xt->data, x, (size_t)K * N * 4);
+    memcpy(dt->data, delta, (size_t)K * M * 4);
+    struct ggml_tensor *o1 = ggml_mul_mat(ctx, w, xt);
+    struct ggml_cgraph g1 = ggml_build_forward(o1);
+    g1.n_threads = n_threads;
+    ggml_graph_compute(ctx, &g1);
+    memcpy(y_before, o1->data, (size_t)M * N * 4);
+    struct ggml_tensor *r = ggml_add_inplace(ctx, w, dt);
+    struct ggml_cgraph g2 = ggml_build_forward(r);
+    g2.n_threads = n_threads;
+    ggml_graph_compute(ctx, &g2);
+    struct ggml_tensor *o2 = ggml_mul_mat(ctx, w, xt);
+    struct ggml_cgraph g3 = ggml_build_forward(o2);
+    g3.n_threads = n_threads;
+    ggml_graph_compute(ctx, &g3);
+    memcpy(y_after, o2->data, (size_t)M * N * 4);
+    memcpy(wq_after, w->data, wbytes);
+    int64_t resident;
+    ggml_hip_weight_cache_stats(&counts[0], &counts[1], &resident);
+    counts[2] = ggml_hip_weight_cache_invalidations();
+    ggml_free(ctx);
+    return 0;
+}
+
+/* A graph that ENDS on a device-only node: y = silu(rms_norm(x)) with both nodes offloaded
+ * (ggml_cuda_assign_buffers_no_scratch, as llama.cpp offloads graph tensors).  The backend defers the
+ * final silu (a launch-fusion candidate), so it is still held when ggml_graph_compute returns; the
+ * context is then freed and, with poison, its arena overwritten before the backend is synchronized
+ * (which runs the held node).  y receives the device result; y_cpu the same graph on ggml's CPU ops.
+ * Returns 0, or -1 on error. */
+int refhip_device_tail(const float *x, int n, int rows, float *y, float *y_cpu, int poison, int n_threads) {
+    const size_t need = (size_t)n * rows * 4 * 4 + (1u << 20);
+    void *mem = malloc(need);
+    if (!mem) return -1;
+    for (int dev = 1; dev >= 0; dev--) {
+        struct ggml_init_params ip = {need, mem, false};
+        struct ggml_context *ctx = ggml_init(ip);
+        if (!ctx) return -1;
+        struct ggml_tensor *xt = ggml_new_tensor_2d(ctx, GGML_TYPE_F32, n, rows);
+        memcpy(xt->data, x, (size_t)n * rows * 4);
+        struct ggml_tensor *a = ggml_rms_norm(ctx, xt);
+        if (dev) ggml_cuda_assign_buffers_no_scratch(a);
+        struct ggml_tensor *b = ggml_silu(ctx, a);
+        if (dev) ggml_cuda_assign_buffers_no_scratch(b);
+        struct ggml_cgraph gf = ggml_build_forward(b);
+        gf.n_threads = n_threads;
+        ggml_graph_compute(ctx, &gf);
+        if (dev) {
+            void *d = ((struct ggml_tensor_extra_gpu *)b->extra)->data_device[0];
+            ggml_free(ctx);
+            if (poison) memset(mem, 0xA5, need);
+            if (ggml_hip_device_synchronize() != 0) return -1;
+            if (ggml_hip_memcpy_d2h(y, d, (size_t)n * rows * 4, NULL) != 0) return -1;
+        } else {
+            memcpy(y_cpu, b->data, (size_t)n * rows * 4);
+            ggml_free(ctx);
+        }
+    }
+    free(mem);
+    return 0;
+}

@@ -126,3 +126,53 @@ def test_gpu_split_across_devices(ref, fractions, N):
     finally:
         if fractions is not None:
             ref.ggml_cuda_set_tensor_split((ctypes.c_float * 16)(*([1.0] * ndev + [0.0] * (16 - ndev))))
+
+
+def test_lora_in_place_add_invalidates_cached_weight(ref):
+    """The reference's LoRA apply (llama.cpp:2935-2967): ggml_add_inplace(W_q4_0, delta) runs on
+    ggml's CPU op (add_q_f32 requantizes every block in place).  The backend sees that node's INIT
+    (ggml.c:17112-17116), drops the cached device copy of W, and the next mul_mat through ggml
+    (N >= 32, can_mul_mat) uses the new bytes: y within the bound of the oracle on W_after."""
+    L = __import__("hip_env").ggml_hip.load()
+    __import__("hip_env").ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+    K, M, N = 4096, 128, 40
+    wf = O.gaussian(M * K, 0x5EED5100, 0.0, 0.02).reshape(M, K)
+    wq, _ = O.quantize_q4_0(wf)
+    x = O.gaussian(N * K, 0x5EED5200, 0.0, 1.0).reshape(N, K)
+    delta = O.gaussian(M * K, 0x5EED5300, 0.0, 0.01).reshape(M, K)
+    wq = np.ascontiguousarray(wq, np.uint8)
+    y0 = np.full((N, M), np.nan, np.float32)
+    y1 = np.full((N, M), np.nan, np.float32)
+    w_after = np.zeros_like(wq)
+    counts = np.zeros(3, np.int64)
+    ref.refhip_lora_add.restype = ctypes.c_int
+    ref.refhip_lora_add.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int]
+    rc = ref.refhip_lora_add(wq.ctypes.data, K, M, np.ascontiguousarray(x, np.float32).ctypes.data, N,
+                             np.ascontiguousarray(delta, np.float32).ctypes.data, y0.ctypes.data, y1.ctypes.data,
+                             w_after.ctypes.data, counts.ctypes.data, 4)
+    assert rc == 0
+    assert not np.array_equal(w_after, wq)                 # the CPU op rewrote W in place
+    assert counts[2] >= 1, counts                          # the add node invalidated the cached copy
+    assert counts[1] == 2, counts                          # two uploads: before and after the edit
+    assert_close(wq, x, K, y0, O.mul_mat(wq, K, x))
+    assert_close(w_after, x, K, y1, O.mul_mat(w_after, K, x))
+
+
+@pytest.mark.parametrize("poison", [0, 1])
+def test_graph_ending_on_held_device_node_survives_ggml_free(ref, poison):
+    """A graph whose final node is device-only (silu of an offloaded rms_norm) leaves that node held
+    by the backend's launch fusion when ggml_graph_compute returns.  The caller frees the context
+    (and here overwrites its arena) before synchronizing: the held node runs from the backend's own
+    snapshot, and y is bitwise equal to ggml's CPU ops (rms_norm ggml.c:10389, silu 10188)."""
+    n, rows = 4096, 3
+    x = O.gaussian(n * rows, 0x5EED5400, 0.0, 1.0).astype(np.float32)
+    y = np.full(n * rows, np.nan, np.float32)
+    y_cpu = np.full(n * rows, np.nan, np.float32)
+    ref.refhip_device_tail.restype = ctypes.c_int
+    ref.refhip_device_tail.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int, ctypes.c_int]
+    assert ref.refhip_device_tail(x.ctypes.data, n, rows, y.ctypes.data, y_cpu.ctypes.data, poison, 2) == 0
+    assert np.all(np.isfinite(y_cpu))
+    assert np.array_equal(y.view(np.uint32), y_cpu.view(np.uint32))

@@ -465,3 +465,72 @@ def test_weight_cache_reuses_and_revalidates_host_weights():
     check_y(y3, O.mul_mat(wq2, K, x), s_abs2, RTOL, ATOL_BLOCKS)
     ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
     assert stats() == (0, 0, 0)
+
+
+def test_weight_cache_invalidate_and_full_verify():
+    """In-place edits the sampled fingerprint cannot see (one block between its sample points):
+    ggml_hip_weight_cache_invalidate(ptr, bytes) drops the copy exactly (the next call re-uploads
+    and y follows the new bytes), and GGML_HIP_WEIGHT_CACHE_VERIFY=full (set_verify(1)) detects the
+    edit without any call.  Reference: the LoRA apply rewrites weights in place, llama.cpp:2950-2967."""
+    L = ggml_hip.load()
+    ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+    K, M, N = 4096, 192, 40
+    wq, x = make_case(K, M, N, seed=23)
+    w_np, x_np = np.ascontiguousarray(wq).copy(), np.ascontiguousarray(x)
+    n = w_np.nbytes
+    flat = w_np.reshape(-1)
+
+    def sampled(lo, hi):            # wcache_fingerprint's sampled byte windows
+        win = [(0, 32), (n - 32, n)] + [((n // 64) * i + n // 128, (n // 64) * i + n // 128 + 8) for i in range(64)]
+        return any(a < hi and lo < b for a, b in win)
+
+    def stats():
+        h, m, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        ggml_hip.check(L.ggml_hip_weight_cache_stats(ctypes.byref(h), ctypes.byref(m), ctypes.byref(r)))
+        return h.value, m.value
+
+    def run():
+        y_np = np.zeros((N, M), np.float32)
+        w = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_Q4_0, (K, M), w_np)
+        xt = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (K, N), x_np)
+        y = ggml_hip.make_tensor(ggml_hip.GGML_TYPE_F32, (M, N), y_np)
+        L.ggml_hip_mul_mat(ctypes.byref(w), ctypes.byref(xt), ctypes.byref(y))
+        return y_np
+
+    def expect(y):
+        w2 = w_np.reshape(M, -1)
+        _, s_abs = block_terms(w2, O.quantize_q8_0(x, "avx2"), K)
+        check_y(y, O.mul_mat(w2, K, x), s_abs, RTOL, ATOL_BLOCKS)
+
+    def edit_block(off):            # double the block's fp16 scale (exponent + 1): y of its row moves
+        assert off % 18 == 0 and not sampled(off, off + 18)
+        d = flat[off:off + 2].view(np.uint16)
+        d[0] = np.uint16(d[0] + 0x0400) if (d[0] & 0x7C00) < 0x7800 else d[0]
+        return off // (18 * K // 32)
+
+    try:
+        y0 = run()
+        assert stats() == (0, 1)
+        row = edit_block(18 * 4000)
+        y_stale = run()                                   # sampled fingerprint: same bytes seen
+        assert stats() == (1, 1)
+        assert np.array_equal(y_stale.view(np.uint32), y0.view(np.uint32))
+        dropped = L.ggml_hip_weight_cache_invalidate(ctypes.c_void_p(w_np.ctypes.data + 18 * 4000), 18)
+        assert dropped == 1
+        y1 = run()
+        assert stats() == (1, 2)
+        assert not np.array_equal(y1[:, row], y0[:, row])
+        expect(y1)
+        assert L.ggml_hip_weight_cache_invalidate(ctypes.c_void_p(w_np.ctypes.data + n + 4096), 16) == 0
+        ggml_hip.check(L.ggml_hip_weight_cache_set_verify(1), "verify full")
+        row2 = edit_block(18 * 9000)
+        y2 = run()                                        # full fingerprint: the edit is a miss
+        assert stats() == (1, 3)
+        assert not np.array_equal(y2[:, row2], y1[:, row2])
+        expect(y2)
+        y3 = run()
+        assert stats() == (2, 3)
+        assert np.array_equal(y3.view(np.uint32), y2.view(np.uint32))
+    finally:
+        ggml_hip.check(L.ggml_hip_weight_cache_set_verify(-1), "verify reset")
+        ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")

@@ -263,6 +263,16 @@ bool wcache_enabled() {
     static const bool on = !getenv("GGML_HIP_WEIGHT_CACHE") || atoi(getenv("GGML_HIP_WEIGHT_CACHE")) != 0;
     return on;
 }
+std::atomic<int64_t> g_decode_min_weights{-1};
+int64_t decode_min_weights() {
+    int64_t v = g_decode_min_weights.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = getenv("GGML_HIP_DECODE_MIN_WEIGHTS");
+        v = e ? atoll(e) : (int64_t)1 << 19;
+        g_decode_min_weights.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
 size_t wcache_budget() {
     static const size_t mb = getenv("GGML_HIP_WEIGHT_CACHE_MB") ? (size_t)atoll(getenv("GGML_HIP_WEIGHT_CACHE_MB")) : 65536;
     return mb << 20;
@@ -1474,7 +1484,14 @@ bool ggml_hip_can_mul_mat(const struct ggml_tensor *src0_, const struct ggml_ten
     // the op here regardless and fail inside ggml_cuda_mul_mat)
     ensure_init();
     if (g_device_count == 0) return false;
-    return dst->ne[0] >= 32 && dst->ne[1] >= 32 && src1->ne[0] >= 32;
+    if (dst->ne[0] >= 32 && dst->ne[1] >= 32 && src1->ne[0] >= 32) return true;
+    // Decode (N < 32) of a host-resident Q4_0 weight: the reference declines it (each call would
+    // re-upload the weight, ggml-cuda.cu:2496-2502), so the arch/ frontends, which never offload,
+    // decode on the CPU.  Here the weight-residency cache keeps the weight on the device after its
+    // first use, so a weight of at least GGML_HIP_DECODE_MIN_WEIGHTS elements (default 2^19: one
+    // LLaMA/Falcon projection is 2^24) is taken at any N; smaller ones stay on ggml's CPU op.
+    return src0->type == gabi::TYPE_Q4_0 && wcache_enabled() &&
+           (uint64_t)src0->ne[0] * (uint64_t)src0->ne[1] >= (uint64_t)decode_min_weights();
 }
 
 size_t ggml_hip_mul_mat_get_wsize(const struct ggml_tensor *, const struct ggml_tensor *, struct ggml_tensor *) {
@@ -2518,6 +2535,14 @@ int ggml_hip_debug_set_gemv_policy(int map, int depth, int rowitems, int wg_per_
         return fail(GGML_HIP_ERR_INVALID, "bad GEMV policy");
     ghip::gemv_set_policy(map, depth, rowitems, wg_per_cu);
     return GGML_HIP_OK;
+}
+
+// not in the public header: the smallest host Q4_0 weight (elements) taken at N < 32 through the
+// residency cache (-1 = GGML_HIP_DECODE_MIN_WEIGHTS or 2^19); returns the previous value
+int64_t ggml_hip_debug_set_decode_min_weights(int64_t n) {
+    const int64_t prev = decode_min_weights();
+    g_decode_min_weights.store(n < 0 ? -1 : n);
+    return prev;
 }
 
 // not in the public header: nodes taken by ggml_hip_compute_forward per ggml op (counts[op], op < n);

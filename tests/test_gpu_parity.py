@@ -230,6 +230,24 @@ def test_llama7b_decode_full_shape(K, M):
     check_y(y, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
 
 
+@pytest.mark.parametrize("K,M", [(4544, 4672), (4544, 4544), (4544, 18176), (18176, 4544),
+                                 (6144, 18432), (6144, 24576), (24576, 6144)],
+                         ids=["falcon-qkv", "falcon-dense", "falcon-h_to_4h", "falcon-4h_to_h",
+                              "neox-qkv", "neox-h_to_4h", "neox-4h_to_h"])
+@pytest.mark.parametrize("N", [1, 4])
+def test_arch_decode_full_shapes(K, M, N):
+    """BASELINE config 5 at full size: Falcon-7B (arch/falcon/falcon.cpp:995-1025; K = 4544 rows are
+    only 4-byte aligned, K = 18176 takes the 64-pair-chunk items) and GPT-NeoX / StableLM-7B
+    (n_embd 6144: QKV {n_embd, 3 n_embd}, MLP {n_embd, 4 n_embd}, arch/gptneox/gptneox.cpp:1014-1024).
+    q8_0 bytes bit-exact, y within the parity bound."""
+    wq, x = make_case(K, M, N, seed=5 * K + M + N)
+    y, _ = gpu_mul_mat(wq, K, x)
+    y_ref = O.mul_mat(wq, K, x, nthreads=8, mode="avx2", pool=False)
+    xq = O.quantize_q8_0(x, "avx2")
+    assert np.array_equal(gpu_q8(x), xq)
+    check_y(y, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
+
+
 @pytest.mark.parametrize("K,M", [(4096, 4096), (4096, 11008)])
 def test_llama7b_prefill_512_full_shape(K, M):
     wq, x = make_case(K, M, 512, seed=3 * K + M)

@@ -162,6 +162,35 @@ int ggml_hip_get_exact(void);
 int ggml_hip_reserve_workspace(int64_t K, int64_t N);
 
 /* ------------------------------------------------------------------------------------------
+ * Decode chains: a sequence of dependent N = 1 q4_0 mul_mats as ONE persistent launch.
+ * A decode eval issues its q4_0 mul_mats one after another on one stream (llama.cpp:1217-1600 ->
+ * ggml_compute_forward_mul_mat_q_f32, ggml.c:11226-11411); each pays a kernel boundary and a ramp.
+ * A chain runs tasks 0..n-1 in order inside one launch: task t reads x only after every task < t
+ * has written its y (so x of a task may be, or overlap, the y of an earlier task), while the
+ * weight loads of later tasks stream ahead.  Results are bitwise equal to n separate
+ * ggml_hip_mul_mat_q4_0_multi(N = 1) calls.  Weights must not change while a launch runs; a
+ * task's y must not overlap its own x.  Exact mode (ggml_hip_set_exact) runs the tasks as
+ * separate exact-mode calls.  No ggml-cuda.h counterpart.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct ggml_hip_chain_task {
+    int nmat;                 /* 1..4 sibling matrices sharing x (e.g. wq|wk|wv) */
+    int64_t K;                /* K % 64 == 0 */
+    const float *x;           /* f32 [K], 16-byte aligned */
+    const void *W[4];         /* block_q4_0 rows, M[i] x K, 16-byte aligned */
+    int64_t M[4];
+    float *y[4];              /* f32 [M[i]] */
+} ggml_hip_chain_task;
+typedef struct ggml_hip_chain ggml_hip_chain;
+/* Validates the tasks and uploads the task table to the current device (synchronous). */
+int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **chain);
+/* Stream-ordered (graph-capturable): one memset node + one kernel per segment of <= 256 tasks. */
+int ggml_hip_chain_launch(ggml_hip_chain *chain, void *stream);
+/* Synchronizes the device; 0 when every dependency wait of the last launch completed, else the
+ * index + 1 of the first task whose wait gave up (bounded spin; its results are invalid). */
+int ggml_hip_chain_status(ggml_hip_chain *chain);
+int ggml_hip_chain_destroy(ggml_hip_chain *chain);
+
+/* ------------------------------------------------------------------------------------------
  * Multi-GPU, one process per GPU (torch.distributed-style ranks), RCCL over xGMI.
  * The reference row-splits weights across devices (GGML_BACKEND_GPU_SPLIT, ggml-cuda.cu:
  * 2361-2368, 2773-2806) and gathers each device's dst rows with cudaMemcpyAsync

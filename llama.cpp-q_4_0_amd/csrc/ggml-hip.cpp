@@ -1971,6 +1971,169 @@ int ggml_hip_reserve_workspace(int64_t K, int64_t N) {
 }
 
 // ------------------------------------------------------------------------------------------
+// decode chains (q4_0_chain.hip): tasks packed into the kernel's 32-word records, in segments
+// whose LDS image (task table + x image + staging) fits a workgroup's 64 KB.
+
+}  // extern "C"
+
+struct ggml_hip_chain {
+    int device = 0;
+    int grid = 0;
+    int depth = 8;
+    std::vector<ggml_hip_chain_task> tasks;       // host copy (exact-mode path)
+    struct Seg {
+        int first, count, kmax;
+    };
+    std::vector<Seg> segs;
+    ghip::ChainTaskDev *d_tasks = nullptr;
+    uint32_t *d_sync = nullptr;                    // CHAIN_SYNC_WORDS per segment
+    unsigned long long *d_stamps = nullptr;        // diagnostics: [grid][ntasks][8] (GGML_HIP_CHAIN_STAMPS=1)
+};
+
+extern "C" {
+
+int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **out) {
+    ensure_init();
+    if (!out) return fail(GGML_HIP_ERR_INVALID, "null out");
+    *out = nullptr;
+    if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
+    if (ntasks < 1 || !tasks) return fail(GGML_HIP_ERR_INVALID, "ntasks must be >= 1");
+    const int dev = current_device();
+    const int cus = g_dev[dev].info.num_cus;
+    static const int depth_env = [] {
+        const char *e = getenv("GGML_HIP_CHAIN_DEPTH");
+        return e ? atoi(e) : 8;
+    }();
+    const int depth = (depth_env == 2 || depth_env == 4 || depth_env == 6) ? depth_env : 8;
+    std::vector<ghip::ChainTaskDev> rec(ntasks);
+    for (int t = 0; t < ntasks; t++) {
+        const ggml_hip_chain_task &k = tasks[t];
+        if (k.nmat < 1 || k.nmat > ghip::GEMV_MULTI_MAX) return fail(GGML_HIP_ERR_INVALID, "nmat must be 1..4");
+        if (k.K <= 0 || k.K % 64 != 0 || !k.x || !aligned(k.x, 16))
+            return fail(GGML_HIP_ERR_INVALID, "bad x or K (K % 64 == 0, 16-byte aligned x)");
+        if ((double)k.K * 1.25 > 32768.0) return fail(GGML_HIP_ERR_UNSUPPORTED, "K too large for a chain");
+        int64_t total = 0;
+        uint32_t *w = rec[t].w;
+        memset(w, 0, sizeof(rec[t].w));
+        int rb[ghip::GEMV_MULTI_MAX + 1] = {0};
+        for (int i = 0; i < ghip::GEMV_MULTI_MAX; i++) {
+            const bool used = i < k.nmat;
+            if (used && (!k.W[i] || !k.y[i] || k.M[i] <= 0 || !aligned(k.W[i], 16) || !aligned(k.y[i], 4)))
+                return fail(GGML_HIP_ERR_INVALID, "null / misaligned W or y, or M <= 0");
+            const uint64_t wp = (uint64_t)(uintptr_t)(used ? k.W[i] : k.W[0]);
+            const uint64_t yp = (uint64_t)(uintptr_t)(used ? k.y[i] : k.y[0]);
+            w[2 * i] = (uint32_t)wp;
+            w[2 * i + 1] = (uint32_t)(wp >> 32);
+            w[8 + 2 * i] = (uint32_t)yp;
+            w[8 + 2 * i + 1] = (uint32_t)(yp >> 32);
+            total += used ? k.M[i] : 0;
+            rb[i + 1] = (int)std::min<int64_t>(total, 1 << 30);
+        }
+        if (total > (int64_t)ghip::CHAIN_STAGE_MAX * cus)
+            return fail(GGML_HIP_ERR_UNSUPPORTED, "too many rows for one chain task");
+        const uint64_t xp = (uint64_t)(uintptr_t)k.x;
+        w[16] = (uint32_t)xp;
+        w[17] = (uint32_t)(xp >> 32);
+        w[18] = (uint32_t)rb[1];
+        w[19] = (uint32_t)rb[2];
+        w[20] = (uint32_t)rb[3];
+        w[21] = (uint32_t)total;
+        w[22] = (uint32_t)k.K;
+    }
+    auto *c = new ggml_hip_chain();
+    c->device = dev;
+    c->depth = depth;
+    c->grid = cus;
+    c->tasks.assign(tasks, tasks + ntasks);
+    // segments: as many tasks as fit the 64 KB LDS image with their largest K
+    for (int t = 0; t < ntasks;) {
+        int kmax = 0, n = 0;
+        while (t + n < ntasks) {
+            const int k2 = std::max(kmax, (int)tasks[t + n].K);
+            if (ghip::chain_lds_bytes(n + 1, k2) + 64 > 65536) break;
+            kmax = k2;
+            n++;
+        }
+        c->segs.push_back({t, n, kmax});
+        t += n;
+    }
+    for (const auto &sg : c->segs) {
+        if (ghip::chain_max_workgroups(sg.kmax, sg.count, depth) < 1) {
+            delete c;
+            return fail(GGML_HIP_ERR_UNSUPPORTED, "chain kernel cannot be resident (occupancy 0)");
+        }
+    }
+    if (hipMalloc(&c->d_tasks, sizeof(ghip::ChainTaskDev) * ntasks) != hipSuccess ||
+        hipMalloc(&c->d_sync, sizeof(uint32_t) * ghip::CHAIN_SYNC_WORDS * c->segs.size()) != hipSuccess) {
+        if (c->d_tasks) (void)hipFree(c->d_tasks);
+        delete c;
+        return fail(GGML_HIP_ERR_NOMEM, "chain: hipMalloc failed");
+    }
+    HIP_RET(hipMemcpy(c->d_tasks, rec.data(), sizeof(ghip::ChainTaskDev) * ntasks, hipMemcpyHostToDevice));
+    if (getenv("GGML_HIP_CHAIN_STAMPS") && c->segs.size() == 1) {
+        HIP_RET(hipMalloc(&c->d_stamps, sizeof(unsigned long long) * 8 * (size_t)c->grid * ntasks));
+        HIP_RET(hipMemset(c->d_stamps, 0, sizeof(unsigned long long) * 8 * (size_t)c->grid * ntasks));
+    }
+    HIP_RET(hipMemset(c->d_sync, 0, sizeof(uint32_t) * ghip::CHAIN_SYNC_WORDS * c->segs.size()));
+    *out = c;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_chain_launch(ggml_hip_chain *c, void *stream) {
+    ensure_init();
+    if (!c) return fail(GGML_HIP_ERR_INVALID, "null chain");
+    if (current_device() != c->device) return fail(GGML_HIP_ERR_INVALID, "chain belongs to another device");
+    hipStream_t s = resolve_stream(stream);
+    if (exact_mode()) {                          // the exact kernels, one call per task
+        for (const auto &k : c->tasks) {
+            int rc = ggml_hip_mul_mat_q4_0_multi(k.nmat, k.W, k.M, k.K, k.x, 1, (float *const *)k.y, s);
+            if (rc != GGML_HIP_OK) return rc;
+        }
+        return GGML_HIP_OK;
+    }
+    for (size_t i = 0; i < c->segs.size(); i++) {
+        const auto &sg = c->segs[i];
+        uint32_t *sync = c->d_sync + i * ghip::CHAIN_SYNC_WORDS;
+        // polled words are zeroed by a stream-ordered memset before every launch (a memset node
+        // under graph capture): a launch never depends on the state a previous one left
+        HIP_RET(hipMemsetAsync(sync, 0, sizeof(uint32_t) * ghip::CHAIN_SYNC_WORDS, s));
+        HIP_RET(ghip::gemv_chain_q4_0(c->d_tasks + sg.first, sg.count, sync, sg.kmax, c->grid, c->depth, c->d_stamps, s));
+    }
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_chain_status(ggml_hip_chain *c) {
+    if (!c) return fail(GGML_HIP_ERR_INVALID, "null chain");
+    HIP_RET(hipDeviceSynchronize());
+    for (size_t i = 0; i < c->segs.size(); i++) {
+        uint32_t code = 0;
+        HIP_RET(hipMemcpy(&code, c->d_sync + i * ghip::CHAIN_SYNC_WORDS + 9 * ghip::CHAIN_SHARD_STRIDE, 4,
+                          hipMemcpyDeviceToHost));
+        if (code) return c->segs[i].first + (int)code;
+    }
+    return 0;
+}
+
+// diagnostics (not in the public header): copy [grid][ntasks][8] stamps of the last launch
+int ggml_hip_debug_chain_stamps(ggml_hip_chain *c, unsigned long long *host, int64_t n, int *grid) {
+    if (!c || !c->d_stamps) return fail(GGML_HIP_ERR_INVALID, "no stamps (set GGML_HIP_CHAIN_STAMPS=1)");
+    if (grid) *grid = c->grid;
+    HIP_RET(hipDeviceSynchronize());
+    HIP_RET(hipMemcpy(host, c->d_stamps, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_chain_destroy(ggml_hip_chain *c) {
+    if (!c) return GGML_HIP_OK;
+    (void)hipDeviceSynchronize();
+    if (c->d_tasks) (void)hipFree(c->d_tasks);
+    if (c->d_sync) (void)hipFree(c->d_sync);
+    if (c->d_stamps) (void)hipFree(c->d_stamps);
+    delete c;
+    return GGML_HIP_OK;
+}
+
+// ------------------------------------------------------------------------------------------
 // multi-GPU (one process per GPU) over RCCL.
 //
 // Transport: a communicator is either an RCCL communicator (ggml_hip_comm_init: one rank per

@@ -72,6 +72,20 @@ struct RowBegins {
 hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const RowBegins &row_begin,
                          int64_t N, float *y, int64_t ldy, hipStream_t s);
 
+// Chain of dependent decode (N = 1) mul_mats as one persistent launch (q4_0_chain.hip).
+// Device task record: 32 words = W[4] (u64), y[4] (u64), x (u64), row_begin[1..3], M total, K.
+struct ChainTaskDev {
+    uint32_t w[32];
+};
+constexpr int CHAIN_STAGE_MAX = 256;          // rows per workgroup per task (M <= 256 * grid)
+constexpr int CHAIN_SHARD_STRIDE = 64;        // words between sync words (one 256-B line each)
+constexpr int CHAIN_SYNC_WORDS = 10 * CHAIN_SHARD_STRIDE;   // [0] top counter, [1..8] per-XCD arrival
+                                                            // counters, [9] timeout code
+size_t chain_lds_bytes(int ntasks, int kmax);
+int chain_max_workgroups(int kmax, int ntasks, int depth);   // resident workgroups per CU
+hipError_t gemv_chain_q4_0(const ChainTaskDev *tasks, int ntasks, uint32_t *sync, int kmax, int grid, int depth,
+                           unsigned long long *stamps, hipStream_t s);
+
 // Synthetic inputs for the bench (splitmix64 + Box-Muller on device).
 hipError_t fill_gaussian(float *dst, int64_t n, uint64_t seed, float mean, float std, hipStream_t s);
 

@@ -96,6 +96,10 @@ def _bind(L):
         "ggml_hip_graph_end": ([vp, vp], i32),
         "ggml_hip_graph_launch": ([vp, vp], i32),
         "ggml_hip_graph_destroy": ([vp], i32),
+        "ggml_hip_chain_create": ([i32, vp, vp], i32),
+        "ggml_hip_chain_launch": ([vp, vp], i32),
+        "ggml_hip_chain_status": ([vp], i32),
+        "ggml_hip_chain_destroy": ([vp], i32),
         "ggml_hip_last_error": ([], cp),
         "ggml_hip_version": ([], cp),
     }
@@ -224,6 +228,46 @@ def mul_mat_multi(ws, Ms, K, x_dev, N, ys, stream=None):
     mp = (ctypes.c_int64 * n)(*Ms)
     xp = x_dev if isinstance(x_dev, int) else x_dev.ptr
     check(load().ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xp, N, yp, stream), "mul_mat_q4_0_multi")
+
+
+class ChainTask(ctypes.Structure):
+    """struct ggml_hip_chain_task (include/ggml-hip.h)"""
+    _fields_ = [("nmat", ctypes.c_int), ("K", ctypes.c_int64), ("x", ctypes.c_void_p),
+                ("W", ctypes.c_void_p * 4), ("M", ctypes.c_int64 * 4), ("y", ctypes.c_void_p * 4)]
+
+
+def _ptr(b):
+    return b if isinstance(b, int) else b.ptr
+
+
+class Chain:
+    """A decode chain (ggml_hip_chain_*): tasks = [(ws, Ms, K, x, ys), ...] run in order as one
+    persistent launch; task t reads x after every earlier task wrote its y."""
+
+    def __init__(self, tasks):
+        L = load()
+        arr = (ChainTask * len(tasks))()
+        for t, (ws, Ms, K, x, ys) in enumerate(tasks):
+            arr[t].nmat = len(ws)
+            arr[t].K = K
+            arr[t].x = _ptr(x)
+            for i in range(len(ws)):
+                arr[t].W[i] = _ptr(ws[i])
+                arr[t].M[i] = Ms[i]
+                arr[t].y[i] = _ptr(ys[i])
+        self.h = ctypes.c_void_p()
+        check(L.ggml_hip_chain_create(len(tasks), arr, ctypes.byref(self.h)), "chain_create")
+
+    def launch(self, stream=None):
+        check(load().ggml_hip_chain_launch(self.h, stream), "chain_launch")
+
+    def status(self):
+        return load().ggml_hip_chain_status(self.h)
+
+    def __del__(self):
+        if _lib is not None and getattr(self, "h", None):
+            _lib.ggml_hip_chain_destroy(self.h)
+            self.h = None
 
 
 def synchronize():

@@ -324,6 +324,19 @@ struct GemvMats {
 // Every field is read with a constant index: the kernel's kernargs arrive in one batch of scalar
 // loads and the per-row matrix lookup is a chain of s_cselect, not a dependent kernarg load.
 
+// Kernel arguments.  Everything a wave needs before its first weight issue (and x for the x-waves)
+// comes first as 14 dwords of scalar arguments, which the library build preloads into SGPRs at wave
+// start (-mllvm -amdgpu-kernarg-preload-count, Makefile): no kernarg round trip, no branch on a
+// kernarg load, no hidden-argument load for the grid size.  Before this the prologue waited on four
+// dependent kernarg loads and a 64-bit division (~0.7 us from wave start to the first weight issue in
+// the phase stamps).  The rest (a fourth sibling's matrix, y, ldy) is only needed at a row's end.
+struct GemvTail {
+    const uint8_t *W3;
+    float *y[GEMV_MAXMAT];
+    int64_t ldy[GEMV_MAXMAT];
+};
+// geom = nb | map << 16 | grid << 18  (nb < 2^16, grid < 2^14; checked by the launcher)
+
 // VAR bit 0 (GLB): weight loads are plain global loads with clamped lane addresses
 // VAR bit 1 (XSPLIT): only the first XW waves load and quantize x; the other waves issue their
 //                     weight loads at once (the x loads enter the CU's queue first)
@@ -338,9 +351,15 @@ struct GemvMats {
 //                     in flight together and it is reduced once (a row of K=4160 no longer costs two
 //                     items for one extra pair).  PPL == 0: 64-pair chunks, one item per chunk.
 template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0>
-__global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, int64_t rowbytes, int nb,
-                                                          const float *__restrict__ x, int K) {
+__global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restrict__ x_, const uint8_t *W0,
+                                                          const uint8_t *W1, const uint8_t *W2, int rb1_, int rb2_,
+                                                          int rb3_, int rowbytes_, int geom, int M_,
+                                                          const GemvTail tail) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int nb = geom & 0xFFFF;
+    const int map = (geom >> 16) & 3;
+    const int grid = (int)((uint32_t)geom >> 18);
+    const int64_t rowbytes = rowbytes_;
     // xq: per token, chunk-major [4][npairs] x 16 B: chunk j = (block & 1) * 2 + word / 4 of pair
     // p = block / 2, so lane p's four ds_read_b128 are lane-contiguous (no bank conflicts)
     uint32_t *xq = lds;                                             // [NT][4][npairs][4] int8x4
@@ -350,17 +369,19 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // kernargs into scalar locals; the per-row matrix choice is written as sums of deltas
-    // selected by (row >= row_begin[i]) so that it compiles to s_cselect (a ternary chain over
-    // four values is turned into a lookup table in scratch by the optimizer)
-    const int M = mats.M;
-    const int rb1 = mats.row_begin[1], rb2 = mats.row_begin[2], rb3 = mats.row_begin[3];
-    const uint64_t w0 = (uint64_t)mats.W[0], wd1 = (uint64_t)mats.W[1] - (uint64_t)mats.W[0],
-                   wd2 = (uint64_t)mats.W[2] - (uint64_t)mats.W[1], wd3 = (uint64_t)mats.W[3] - (uint64_t)mats.W[2];
-    const uint64_t y0 = (uint64_t)mats.y[0], yd1 = (uint64_t)mats.y[1] - (uint64_t)mats.y[0],
-                   yd2 = (uint64_t)mats.y[2] - (uint64_t)mats.y[1], yd3 = (uint64_t)mats.y[3] - (uint64_t)mats.y[2];
-    const int64_t l0 = mats.ldy[0], ld1 = mats.ldy[1] - mats.ldy[0], ld2 = mats.ldy[2] - mats.ldy[1],
-                  ld3 = mats.ldy[3] - mats.ldy[2];
+    // the y / ldy choice at a row's end is written as sums of deltas selected by (row >=
+    // row_begin[i]) so that it compiles to s_cselect (a ternary chain over four struct fields is
+    // turned into a lookup table in scratch by the optimizer)
+    // (every argument is copied into a local first: a lambda capturing an SGPR-preloaded argument or
+    // the by-value struct by reference materialises the whole argument block in scratch)
+    const float *const x = x_;
+    const uint8_t *const w0 = W0, *const w3 = tail.W3;
+    const uint64_t wd1 = (uint64_t)W1 - (uint64_t)W0, wd2 = (uint64_t)W2 - (uint64_t)W1;
+    const int rb1 = rb1_, rb2 = rb2_, rb3 = rb3_, M = M_;
+    const uint64_t y0 = (uint64_t)tail.y[0], yd1 = (uint64_t)tail.y[1] - (uint64_t)tail.y[0],
+                   yd2 = (uint64_t)tail.y[2] - (uint64_t)tail.y[1], yd3 = (uint64_t)tail.y[3] - (uint64_t)tail.y[2];
+    const int64_t l0 = tail.ldy[0], ld1 = tail.ldy[1] - tail.ldy[0], ld2 = tail.ldy[2] - tail.ldy[1],
+                  ld3 = tail.ldy[3] - tail.ldy[2];
     const int npairs = nb >> 1;
     const int nchunk = PPL > 0 ? 1 : (npairs + 63) >> 6;
     constexpr int NPR = PPL > 0 ? PPL : 1;                          // pairs per lane per item
@@ -374,26 +395,31 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const GemvMats mats, i
     // With grid a multiple of the CU count, 1 and 2 give every CU floor or ceil of M/grid rows per
     // workgroup (no CU streams twice the bytes of another at the tail); 0 does when M is a
     // multiple of grid*WAVES.
-    const int map = mats.map;
     int row0, rstride, rend;
-    if (map == 2) {
-        row0 = (int)(((int64_t)blockIdx.x * M) / (int)gridDim.x) + wave;
-        rend = (int)(((int64_t)(blockIdx.x + 1) * M) / (int)gridDim.x);
+    if (map == 2) {                                                 // grid * M < 2^32 (launcher)
+        row0 = (int)(((uint32_t)blockIdx.x * (uint32_t)M) / (uint32_t)grid) + wave;
+        rend = (int)(((uint32_t)(blockIdx.x + 1) * (uint32_t)M) / (uint32_t)grid);
         rstride = WAVES;
     } else {
-        row0 = map == 1 ? wave * (int)gridDim.x + blockIdx.x : blockIdx.x * WAVES + wave;
+        row0 = map == 1 ? wave * grid + blockIdx.x : blockIdx.x * WAVES + wave;
         rend = M;
-        rstride = mats.rstride;
+        rstride = grid * WAVES;
     }
-    const int nrows_w = row0 < rend ? (rend - 1 - row0) / rstride + 1 : 0;
+    const int nrows_w = row0 < rend ? (int)((uint32_t)(rend - 1 - row0) / (uint32_t)rstride) + 1 : 0;
     const int nitems = nrows_w * nchunk;                            // (row, chunk) items of this wave
     GEMV_STAMP(0);
 
     static_assert(GEMV_MAXMAT == 4, "matrix selection below is written for 4 siblings");
     auto row_ptr = [&](int r) __attribute__((always_inline)) {     // wave-uniform
-        const bool g1 = r >= rb1, g2 = r >= rb2, g3 = r >= rb3;
-        const uint64_t w = w0 + (g1 ? wd1 : 0) + (g2 ? wd2 : 0) + (g3 ? wd3 : 0);
-        const int rb = (g1 ? rb1 : 0) + (g2 ? rb2 - rb1 : 0) + (g3 ? rb3 - rb2 : 0);
+        // sums of selected deltas (a ternary chain over the pointers becomes a scratch lookup table)
+        const bool g1 = r >= rb1, g2 = r >= rb2;
+        uint64_t w = (uint64_t)w0 + (g1 ? wd1 : 0) + (g2 ? wd2 : 0);
+        int rb = (g1 ? rb1 : 0) + (g2 ? rb2 - rb1 : 0);
+        if (r >= rb3) {                       // a fourth sibling: its pointer is not preloaded, and
+            asm volatile("");                 // the branch must stay one (a select would wait for it)
+            w = (uint64_t)w3;
+            rb = rb3;
+        }
         return reinterpret_cast<const uint8_t *>(w) + (int64_t)(r - rb) * rowbytes;
     };
 
@@ -652,17 +678,23 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     const int64_t bal = need <= cus ? need : cus * ((need + cus - 1) / cus);
     const unsigned grid = (unsigned)(bal < cap ? bal : cap);
     const int map_env = gemv_policy().map;
-    GemvMats ma = m;
-    ma.M = (int)M;
-    ma.rstride = (int)grid * WAVES;
     // strided (contiguous 16-row spans) when its leftover rows form whole rounds of one workgroup per
     // CU (every CU then gets the same rows); otherwise interleaved at two workgroups per CU and
     // blocked at one (measured per shape, tools/shape_sweep.py)
-    ma.map = map_env >= 0 ? map_env
-           : ((M % ((int64_t)grid * WAVES)) % (cus * WAVES) == 0 ? 0 : ((int64_t)grid > cus ? 1 : 2));
+    int map = map_env >= 0 ? map_env
+            : ((M % ((int64_t)grid * WAVES)) % (cus * WAVES) == 0 ? 0 : ((int64_t)grid > cus ? 1 : 2));
+    if (map == 2 && (int64_t)grid * M >= (int64_t)1 << 32) map = 1;   // the kernel's 32-bit row split
+    if (nb >= (1 << 16) || grid >= (1u << 14) || rowbytes > INT_MAX || M > INT_MAX) return hipErrorInvalidValue;
+    GemvTail tail;
+    tail.W3 = m.W[3];
+    for (int i = 0; i < GEMV_MAXMAT; i++) {
+        tail.y[i] = m.y[i];
+        tail.ldy[i] = m.ldy[i];
+    }
+    const int geom = nb | map << 16 | (int)(grid << 18);
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>), dim3(grid), dim3(WAVES * 64), lds, s, ma, rowbytes, nb,
-                       x, (int)K);
+    hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
+                       m.W[1], m.W[2], m.row_begin[1], m.row_begin[2], m.row_begin[3], (int)rowbytes, geom, (int)M, tail);
     return hipGetLastError();
 }
 
@@ -681,14 +713,21 @@ static hipError_t launch_gemv_rows(const GemvMats &m, int64_t K, const float *x,
 
 template <int NT>
 static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
-    // Production: VAR 3 (global weight loads + x-wave prologue), ring depth 1 for single-chunk
-    // rows (K <= 4096) and 2 when a row spans several 64-pair chunks (measured per shape,
-    // tools/gemv_ab.sh).  GGML_HIP_GEMV_VAR=0 / 7 / GGML_HIP_GEMV_DEPTH=1|2 select the A/B variants;
+    // Production: VAR 3 or 15 (global weight loads + x-wave prologue; policy below), decode row items
+    // at ring depth 1; chunked items (N > 1 or K > 12288) at depth 1 for single-chunk rows and 2
+    // otherwise (measured per shape, tools/gemv_ab.sh).  GGML_HIP_GEMV_VAR=0 / 3 / 7 / 15 and
+    // GGML_HIP_GEMV_DEPTH=1|2 select the A/B variants;
     // GGML_HIP_GEMV_DIAG=7 the phase-stamp build (row items as in production), 8/9/10 the timing
     // knockouts (invalid results).
     static const int diag = env_int("GGML_HIP_GEMV_DIAG", 0);
-    static const int var = env_int("GGML_HIP_GEMV_VAR", 3);
+    static const int var_env = env_int("GGML_HIP_GEMV_VAR", -1);
     const int depth_env = gemv_policy().depth;
+    // Decode row items (round 2, with preloaded kernargs; tools/gemv_ab.sh, LLaMA-7B shapes): one row
+    // in flight per wave, and XHOLD (VAR 15: the x-waves issue their own weights once x is in LDS)
+    // when a wave has at most two rows and x is short (wq|wk|wv 7.33 -> 7.19 us, wo 4.82 -> 4.24);
+    // VAR 3 otherwise (w1|w3 at 2.7 rows per wave 10.56 vs 10.73, w2 at K = 11008 7.33 vs 8.06)
+    const int64_t Mrows = m.row_begin[m.n];
+    const int var = var_env >= 0 ? var_env : (NT == 1 && K <= 8192 && Mrows <= 2 * 512 * 16 ? 15 : 3);
     const int depth = depth_env ? depth_env : (K / 64 > 64 ? 2 : 1);
     if constexpr (NT == 1) {
         if (diag == 8) return launch_gemv_w<NT, 8, 16, 1>(m, K, x, dev, s);
@@ -701,9 +740,7 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
         if (rowitems && (var == 3 || var == 7 || var == 15) && ppl <= 3) {
             // two rows in flight per wave, except the multi-round strided case (M > 2*CUs*16 with
             // the leftover rows a whole round per CU, e.g. the fused LLaMA-7B wq|wk|wv, M = 12288)
-            const int64_t M = m.row_begin[m.n], r1 = 2 * (int64_t)dev.num_cus * 16;
-            const bool strided_multi = M > r1 && (M % r1) % (r1 / 2) == 0;
-            const int rd = depth_env ? depth_env : (strided_multi ? 1 : 2);
+            const int rd = depth_env ? depth_env : 1;
             if (diag == 7) return var == 15 ? launch_gemv_rows<NT, 7, 15>(m, K, x, dev, s, ppl, rd)
                                   : var == 7 ? launch_gemv_rows<NT, 7, 7>(m, K, x, dev, s, ppl, rd)
                                              : launch_gemv_rows<NT, 7, 3>(m, K, x, dev, s, ppl, rd);

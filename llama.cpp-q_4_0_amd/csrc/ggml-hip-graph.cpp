@@ -1,0 +1,299 @@
+// ggml-hip-graph.cpp — the launch recorder behind ghip::launch_k (launch.h).
+//
+// Full offload hands the backend one ggml node at a time (ggml.c:15645-15652), ~1,187 nodes and ~375
+// kernel launches per decode eval of LLaMA-7B; issued one by one each launch costs ~2.6 us of host
+// time (tools/host_costs2.hip), which made the end-to-end decode host bound.  While recording is on,
+// launch_k appends the launch to a run; the run is submitted at the next sync point as one HIP graph:
+//   * runs are keyed by their kernel sequence (function, block, LDS bytes, argument layout); a run
+//     whose sequence matches a cached executable graph updates only the nodes whose grid or argument
+//     bytes changed (the n_past-dependent rope / cache-copy / attention nodes of a decode eval) and
+//     replays it; a new sequence is instantiated once (~1.3 ms per 48 nodes) and cached (LRU of 64);
+//   * a run is submitted every GGML_HIP_GRAPH_CHUNK (48) launches, so the device overlaps the host;
+//   * the nodes of a run form one dependency chain: the same order as the stream would execute them.
+// The results are the kernels' own, so every bitwise test of the eager path holds for the recorded one.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "launch.h"
+
+namespace ghip {
+namespace {
+
+constexpr int MAX_ARGS = 32;
+constexpr size_t MAX_CACHED = 64;
+
+struct Item {
+    const void *fn;
+    dim3 grid, block;
+    size_t lds;
+    int nargs;
+    size_t off[MAX_ARGS];     // argument offsets in the run's blob
+    size_t size[MAX_ARGS];
+};
+
+struct Run {
+    std::vector<Item> items;
+    std::vector<unsigned char> blob;
+};
+
+struct Cached {
+    Run run;
+    uint64_t sig = 0;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ex = nullptr;
+    std::vector<hipGraphNode_t> nodes;
+    hipEvent_t done = nullptr;
+    uint64_t used = 0;
+};
+
+struct Recorder {
+    hipStream_t stream = nullptr;
+    bool on = false;
+    Run cur;
+    std::vector<Cached *> cache;
+    uint64_t clock = 0;
+    int ordinal = 0;          // runs submitted since the last sync point (chunk position in the eval)
+    long long runs = 0, kernels = 0, updated = 0, built = 0, submit_ns = 0;
+};
+Recorder &rec() {
+    static Recorder r;
+    return r;
+}
+
+void fatal(hipError_t e, const char *what) {
+    fprintf(stderr, "ggml-hip: launch recorder: %s failed: %s\n", what, hipGetErrorString(e));
+    exit(1);
+}
+#define REC_CK(x)                                   \
+    do {                                            \
+        hipError_t e_ = (x);                        \
+        if (e_ != hipSuccess) fatal(e_, #x);        \
+    } while (0)
+
+bool same_shape(const Item &a, const Item &b) {
+    if (a.fn != b.fn || a.nargs != b.nargs || a.block.x != b.block.x || a.block.y != b.block.y ||
+        a.block.z != b.block.z)
+        return false;
+    for (int i = 0; i < a.nargs; i++)
+        if (a.size[i] != b.size[i]) return false;
+    return true;
+}
+
+uint64_t signature(const Run &r, int ordinal) {
+    uint64_t h = (1469598103934665603ull ^ r.items.size()) * 1099511628211ull ^ (uint64_t)ordinal;
+    for (const Item &it : r.items) {
+        h = (h ^ (uint64_t)(uintptr_t)it.fn) * 1099511628211ull;
+        h = (h ^ (31 * it.block.x + 7 * it.nargs)) * 1099511628211ull;
+    }
+    return h;
+}
+
+hipKernelNodeParams params_of(Run &r, size_t i, void **argv) {
+    Item &it = r.items[i];
+    for (int a = 0; a < it.nargs; a++) argv[a] = r.blob.data() + it.off[a];
+    hipKernelNodeParams p{};
+    p.blockDim = it.block;
+    p.extra = nullptr;
+    p.func = const_cast<void *>(it.fn);
+    p.gridDim = it.grid;
+    p.kernelParams = argv;
+    p.sharedMemBytes = (unsigned int)it.lds;
+    return p;
+}
+
+void destroy(Cached *c) {
+    if (c->done) {
+        REC_CK(hipEventSynchronize(c->done));
+        REC_CK(hipEventDestroy(c->done));
+    }
+    if (c->ex) REC_CK(hipGraphExecDestroy(c->ex));
+    if (c->g) REC_CK(hipGraphDestroy(c->g));
+    delete c;
+}
+
+Cached *build(Run &run, uint64_t sig) {
+    Cached *c = new Cached;
+    c->sig = sig;
+    REC_CK(hipGraphCreate(&c->g, 0));
+    c->nodes.resize(run.items.size());
+    void *argv[MAX_ARGS];
+    for (size_t i = 0; i < run.items.size(); i++) {
+        hipKernelNodeParams p = params_of(run, i, argv);
+        REC_CK(hipGraphAddKernelNode(&c->nodes[i], c->g, i ? &c->nodes[i - 1] : nullptr, i ? 1 : 0, &p));
+    }
+    REC_CK(hipGraphInstantiate(&c->ex, c->g, nullptr, nullptr, 0));
+    REC_CK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
+    c->run.items.swap(run.items);
+    c->run.blob.swap(run.blob);
+    rec().built++;
+    return c;
+}
+
+// the nodes of c whose grid or argument bytes differ from run's take run's values
+// submit the pending run; chunk = the run was cut by its length (the next run continues the same
+// stretch of the eval), else a sync point ends the stretch
+void submit(bool chunk);
+
+bool update(Cached *c, Run &run) {
+    if (hipEventQuery(c->done) == hipErrorNotReady) REC_CK(hipEventSynchronize(c->done));
+    void *argv[MAX_ARGS];
+    for (size_t i = 0; i < run.items.size(); i++) {
+        const Item &a = run.items[i], &b = c->run.items[i];
+        bool diff = a.grid.x != b.grid.x || a.grid.y != b.grid.y || a.grid.z != b.grid.z || a.lds != b.lds;
+        for (int k = 0; !diff && k < a.nargs; k++)
+            diff = memcmp(run.blob.data() + a.off[k], c->run.blob.data() + b.off[k], a.size[k]) != 0;
+        if (!diff) continue;
+        static const bool trace = getenv("GGML_HIP_TRACE_GRAPH") && atoi(getenv("GGML_HIP_TRACE_GRAPH")) >= 2;
+        if (trace) {
+            int k = 0;
+            while (k < a.nargs && memcmp(run.blob.data() + a.off[k], c->run.blob.data() + b.off[k], a.size[k]) == 0) k++;
+            uint64_t vo = 0, vn = 0;
+            if (k < a.nargs) {
+                memcpy(&vo, c->run.blob.data() + b.off[k], a.size[k] < 8 ? a.size[k] : 8);
+                memcpy(&vn, run.blob.data() + a.off[k], a.size[k] < 8 ? a.size[k] : 8);
+            }
+            fprintf(stderr, "rec_update: node %zu %s grid %u->%u lds %zu->%zu arg %d (%zu B) %llx -> %llx\n", i,
+                    hipKernelNameRefByPtr(a.fn, nullptr), b.grid.x, a.grid.x, b.lds, a.lds, k, k < a.nargs ? a.size[k] : 0,
+                    (unsigned long long)vo, (unsigned long long)vn);
+        }
+        hipKernelNodeParams p = params_of(run, i, argv);
+        if (hipGraphExecKernelNodeSetParams(c->ex, c->nodes[i], &p) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        rec().updated++;
+    }
+    c->run.items.swap(run.items);
+    c->run.blob.swap(run.blob);
+    return true;
+}
+
+}  // namespace
+
+bool rec_active(hipStream_t s) {
+    const Recorder &r = rec();
+    return r.on && s == r.stream;
+}
+
+bool rec_pending() { return !rec().cur.items.empty(); }
+
+void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, int nargs, void *const *args,
+                const size_t *sizes, const size_t *aligns) {
+    Recorder &r = rec();
+    if (nargs > MAX_ARGS) {
+        fprintf(stderr, "ggml-hip: launch recorder: %d kernel arguments (max %d)\n", nargs, MAX_ARGS);
+        exit(1);
+    }
+    (void)s;
+    Item it;
+    it.fn = fn;
+    it.grid = grid;
+    it.block = block;
+    it.lds = lds;
+    it.nargs = nargs;
+    for (int i = 0; i < nargs; i++) {
+        size_t off = (r.cur.blob.size() + aligns[i] - 1) & ~(aligns[i] - 1);
+        r.cur.blob.resize(off + sizes[i]);
+        memcpy(r.cur.blob.data() + off, args[i], sizes[i]);
+        it.off[i] = off;
+        it.size[i] = sizes[i];
+    }
+    r.cur.items.push_back(it);
+    // submit every `chunk` launches, so the device starts on an eval while the host still walks its
+    // nodes (a whole eval as one graph would run only after the host finished: no overlap)
+    static const size_t chunk = [] {
+        const char *e = getenv("GGML_HIP_GRAPH_CHUNK");
+        const int v = e ? atoi(e) : 0;
+        return (size_t)(v > 0 ? v : 48);
+    }();
+    if (r.cur.items.size() >= chunk) submit(true);
+}
+
+void rec_flush_at(const char *why) {
+    static const bool trace = getenv("GGML_HIP_TRACE_GRAPH") != nullptr;
+    if (trace && !rec().cur.items.empty())
+        fprintf(stderr, "rec_flush: %zu launches, by %s\n", rec().cur.items.size(), why);
+    rec_flush();
+}
+
+void rec_flush() { submit(false); }
+
+namespace {
+void submit(bool chunk) {
+    Recorder &r = rec();
+    if (r.cur.items.empty()) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    // runs are matched by kernel sequence AND position since the last sync point: the 32 layers of a
+    // decode eval repeat one kernel sequence, and a chunk must replay its own graph (same buffers),
+    // not another layer's (every node would need an update, and that graph may still be running)
+    const uint64_t sig = signature(r.cur, r.ordinal);
+    r.ordinal = chunk ? r.ordinal + 1 : 0;
+    Cached *hit = nullptr;
+    for (Cached *c : r.cache) {
+        if (c->sig != sig || c->run.items.size() != r.cur.items.size()) continue;
+        bool same = true;
+        for (size_t i = 0; same && i < r.cur.items.size(); i++) same = same_shape(r.cur.items[i], c->run.items[i]);
+        if (same) {
+            hit = c;
+            break;
+        }
+    }
+    if (hit && !update(hit, r.cur)) {          // a change the executable graph cannot take: rebuild it
+        for (size_t i = 0; i < r.cache.size(); i++)
+            if (r.cache[i] == hit) r.cache.erase(r.cache.begin() + i);
+        destroy(hit);
+        hit = nullptr;
+    }
+    if (!hit) {
+        if (r.cache.size() >= MAX_CACHED) {    // evict the least recently used
+            size_t lru = 0;
+            for (size_t i = 1; i < r.cache.size(); i++)
+                if (r.cache[i]->used < r.cache[lru]->used) lru = i;
+            destroy(r.cache[lru]);
+            r.cache.erase(r.cache.begin() + lru);
+        }
+        hit = build(r.cur, sig);
+        r.cache.push_back(hit);
+    }
+    hit->used = ++r.clock;
+    r.runs++;
+    r.kernels += (long long)hit->run.items.size();
+    REC_CK(hipGraphLaunch(hit->ex, r.stream));
+    REC_CK(hipEventRecord(hit->done, r.stream));
+    r.cur.items.clear();
+    r.cur.blob.clear();
+    r.submit_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
+
+// recording on / off for stream s; switching streams submits what is pending (turning recording off
+// does not: the next eager launch or sync point does)
+void rec_enable(hipStream_t s, bool on) {
+    Recorder &r = rec();
+    if (s != r.stream) rec_flush();
+    r.stream = s;
+    r.on = on;
+}
+
+void rec_stats(long long *runs, long long *kernels, long long *updated, long long *built, long long *submit_ns) {
+    const Recorder &r = rec();
+    *submit_ns = r.submit_ns;
+    *runs = r.runs;
+    *kernels = r.kernels;
+    *updated = r.updated;
+    *built = r.built;
+}
+
+void rec_clear_cache() {
+    Recorder &r = rec();
+    rec_flush();
+    for (Cached *c : r.cache) destroy(c);
+    r.cache.clear();
+}
+
+}  // namespace ghip

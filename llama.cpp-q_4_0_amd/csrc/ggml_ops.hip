@@ -22,6 +22,7 @@
 // These are small, latency-bound launches (a decode layer moves a few KB through them); one wave
 // per row where the CPU reduces over a row, one lane per element otherwise.
 #include "ggml_ops.h"
+#include "launch.h"
 
 #include <cmath>
 
@@ -688,9 +689,9 @@ hipError_t op_add_rms_norm_mul_f32(const float *a, const float *b, float *sum, f
                                    int64_t ncols, int64_t nrows, hipStream_t s) {
     if (nrows <= 0) return hipSuccess;
     if (row_norm4_ok(ncols, a, b, sum, norm, w, out))
-        hipLaunchKernelGGL(k_row_norm4, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, a, b, sum, norm, w, out, ncols);
+        launch_k(k_row_norm4, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, a, b, sum, norm, w, out, ncols);
     else
-        hipLaunchKernelGGL(k_add_rms_norm_mul, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, a, b, sum, norm, w, out,
+        launch_k(k_add_rms_norm_mul, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, a, b, sum, norm, w, out,
                            ncols, nrows);
     return hipGetLastError();
 }
@@ -699,7 +700,7 @@ hipError_t op_scale_mask_soft_max_f32(const float *x, float *scaled, float *mask
                                       int64_t nrows, int64_t rows_per_channel, int n_past, const uint16_t *table,
                                       hipStream_t s) {
     if (nrows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_scale_mask_soft_max, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, scaled, masked, d, v,
+    launch_k(k_scale_mask_soft_max, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, scaled, masked, d, v,
                        ncols, nrows, rows_per_channel, n_past, table);
     return hipGetLastError();
 }
@@ -709,7 +710,7 @@ hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *
                           int64_t nout, float *kqv, float *merged, hipStream_t s) {
     if (nhead <= 0 || nkv <= 0 || nout <= 0) return hipSuccess;
     const int splits = (int)((nout + SM_OUT - 1) / SM_OUT);
-    hipLaunchKernelGGL(k_softmax_kqv, dim3((unsigned)(nhead * splits)), dim3(SM_THREADS), (size_t)nkv * 4, s, kq, scaled,
+    launch_k(k_softmax_kqv, dim3((unsigned)(nhead * splits)), dim3(SM_THREADS), (size_t)nkv * 4, s, kq, scaled,
                        masked, sm, v, n_past, table, nkv, (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged);
     return hipGetLastError();
 }
@@ -717,13 +718,13 @@ hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *
 hipError_t op_silu_mul_f32(const float *a, const float *b, float *u, float *out, int64_t n, const uint16_t *table,
                            hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_silu_mul, dim3(blocks(n)), dim3(TPB), 0, s, a, b, u, out, n, table);
+    launch_k(k_silu_mul, dim3(blocks(n)), dim3(TPB), 0, s, a, b, u, out, n, table);
     return hipGetLastError();
 }
 
 hipError_t op_add_f32(const float *a, const float *b, float *d, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_add_f32, dim3(blocks(n)), dim3(TPB), 0, s, a, b, d, n);
+    launch_k(k_add_f32, dim3(blocks(n)), dim3(TPB), 0, s, a, b, d, n);
     return hipGetLastError();
 }
 
@@ -731,20 +732,20 @@ hipError_t op_mul_f32(const float *a, const float *b, float *d, int64_t ne00, in
                       int64_t ne11, int64_t ne12, int64_t ne13, hipStream_t s) {
     const int64_t nrows = ne01 * ne02 * ne03;
     if (nrows * ne00 <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mul_f32, dim3(blocks(nrows * ne00)), dim3(TPB), 0, s, a, b, d, ne00, ne01, ne02, nrows, ne11,
+    launch_k(k_mul_f32, dim3(blocks(nrows * ne00)), dim3(TPB), 0, s, a, b, d, ne00, ne01, ne02, nrows, ne11,
                        ne12, ne13);
     return hipGetLastError();
 }
 
 hipError_t op_silu_f32(const float *x, float *d, int64_t n, const uint16_t *table, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_silu_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, n, table);
+    launch_k(k_silu_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, n, table);
     return hipGetLastError();
 }
 
 hipError_t op_scale_f32(const float *x, float *d, float v, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_scale_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, v, n);
+    launch_k(k_scale_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, v, n);
     return hipGetLastError();
 }
 
@@ -752,7 +753,7 @@ hipError_t op_diag_mask_inf_f32(const float *x, float *d, int64_t ncols, int64_t
                                 int n_past, hipStream_t s) {
     const int64_t n = ncols * nrows;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_diag_mask_inf_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, ncols, n, rows_per_channel, n_past);
+    launch_k(k_diag_mask_inf_f32, dim3(blocks(n)), dim3(TPB), 0, s, x, d, ncols, n, rows_per_channel, n_past);
     return hipGetLastError();
 }
 
@@ -760,16 +761,16 @@ hipError_t op_rms_norm_f32(const float *x, float *d, int64_t ncols, int64_t nrow
                            hipStream_t s) {
     if (nrows <= 0) return hipSuccess;
     if (ldx == ncols && ldd == ncols && row_norm4_ok(ncols, nullptr, x, nullptr, d, nullptr, nullptr))
-        hipLaunchKernelGGL(k_row_norm4, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, nullptr, x, nullptr, d, nullptr,
+        launch_k(k_row_norm4, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, nullptr, x, nullptr, d, nullptr,
                            nullptr, ncols);
     else
-        hipLaunchKernelGGL(k_rms_norm_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, ldx, ldd);
+        launch_k(k_rms_norm_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, ldx, ldd);
     return hipGetLastError();
 }
 
 hipError_t op_soft_max_f32(const float *x, float *d, int64_t ncols, int64_t nrows, const uint16_t *table, hipStream_t s) {
     if (nrows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_soft_max_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, table);
+    launch_k(k_soft_max_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, table);
     return hipGetLastError();
 }
 
@@ -777,7 +778,7 @@ hipError_t op_rope_f32(const void *x, void *d, const int64_t ne[4], const int64_
                        const void *cs, int npairs, hipStream_t s) {
     const int64_t n = ne[0] / 2 * ne[1] * ne[2] * ne[3];
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rope_f32, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1], ne[2],
+    launch_k(k_rope_f32, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1], ne[2],
                        nbx[1], nbx[2], nbx[3], nbd[1], nbd[2], nbd[3], n, (const float2 *)cs, npairs);
     return hipGetLastError();
 }
@@ -788,11 +789,11 @@ hipError_t op_rope_cpy_f32(const void *x, void *d, const int64_t ne[4], const in
     const int64_t n = ne[0] / 2 * ne[1] * ne[2] * ne[3];
     if (n <= 0) return hipSuccess;
     if (to_f16)
-        hipLaunchKernelGGL(k_rope_cpy<true>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1],
+        launch_k(k_rope_cpy<true>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1],
                            ne[2], nbx[1], nbx[2], nbx[3], nbd[1], nbd[2], nbd[3], n, (const float2 *)cs, npairs, (char *)c,
                            ne10, ne11, nb10, nb11, nb12);
     else
-        hipLaunchKernelGGL(k_rope_cpy<false>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1],
+        launch_k(k_rope_cpy<false>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, ne[0], ne[1],
                            ne[2], nbx[1], nbx[2], nbx[3], nbd[1], nbd[2], nbd[3], n, (const float2 *)cs, npairs, (char *)c,
                            ne10, ne11, nb10, nb11, nb12);
     return hipGetLastError();
@@ -803,10 +804,10 @@ hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne
                       hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (to_f16)
-        hipLaunchKernelGGL(k_cpy_f32<true>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, n, ne00, ne01,
+        launch_k(k_cpy_f32<true>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, n, ne00, ne01,
                            nb00, nb01, nb02, ne10, ne11, nb10, nb11, nb12);
     else
-        hipLaunchKernelGGL(k_cpy_f32<false>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, n, ne00, ne01,
+        launch_k(k_cpy_f32<false>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, n, ne00, ne01,
                            nb00, nb01, nb02, ne10, ne11, nb10, nb11, nb12);
     return hipGetLastError();
 }
@@ -821,7 +822,7 @@ hipError_t op_elem_batch(const ElemBatch &b, hipStream_t s) {
     }
     for (int q = bb.nops; q < ELEM_MAX; q++) bb.block_begin[q] = total;
     if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_elem_batch, dim3(total), dim3(TPB), 0, s, bb);
+    launch_k(k_elem_batch, dim3(total), dim3(TPB), 0, s, bb);
     return hipGetLastError();
 }
 
@@ -834,13 +835,13 @@ hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, i
     const bool fits = ne02 <= 65535 && (ne11 + FT - 1) / FT <= 65535;
     if (fits && (tiled > 0 || (tiled < 0 && tiled_min > 0 && ne11 >= tiled_min))) {
         // many src1 rows (prefill): tiled through LDS, same bits
-        hipLaunchKernelGGL(k_mul_mat_f16_f32_tiled, dim3((unsigned)((ne01 + FT - 1) / FT), (unsigned)((ne11 + FT - 1) / FT),
+        launch_k(k_mul_mat_f16_f32_tiled, dim3((unsigned)((ne01 + FT - 1) / FT), (unsigned)((ne11 + FT - 1) / FT),
                                                          (unsigned)ne02),
                            dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d, K, ne01, ne11, ne02, nb01, nb02, nb11,
                            nb12, merged);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_mul_mat_f16_f32, dim3(blocks(nout * 32)), dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d,
+    launch_k(k_mul_mat_f16_f32, dim3(blocks(nout * 32)), dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d,
                        K, ne01, ne11, ne02, nb01, nb02, nb11, nb12, merged);
     return hipGetLastError();
 }

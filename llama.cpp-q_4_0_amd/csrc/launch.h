@@ -1,0 +1,75 @@
+// launch.h — every kernel launch of libggml_hip.so goes through ghip::launch_k.
+//
+// Eager by default (hipLaunchKernel).  While the launch recorder is active on the stream (full
+// offload through ggml_hip_compute_forward, one device: a decode eval issues ~375 small launches
+// at ~2.6 us of host time each, measured by tools/host_costs2.hip), a launch is only recorded
+// (function, grid, block, LDS bytes, a copy of the argument values); the recorded run is submitted
+// as one HIP graph at the next sync point (any memcpy / event / synchronize / free of the backend,
+// ggml-hip-graph.cpp).  A run with the same kernels as a cached graph is submitted by updating the
+// nodes whose grid or arguments changed (hipGraphExecKernelNodeSetParams, ~0.6 us per changed node)
+// and one hipGraphLaunch (~0.03 us per kernel of host time).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <type_traits>
+#include <utility>
+
+namespace ghip {
+
+template <class T> struct type_tag { using type = T; };
+
+// true while launches on s are recorded instead of issued
+bool rec_active(hipStream_t s);
+// launches recorded but not yet submitted
+bool rec_pending();
+// records one launch; args[i] points at the value of parameter i (copied before returning)
+void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, int nargs, void *const *args,
+                const size_t *sizes, const size_t *aligns);
+// submits the recorded launches (no-op when none are pending); every backend HIP call that is not
+// a kernel launch calls it first (GHIP_SYNC in ggml-hip.cpp)
+void rec_flush();
+void rec_flush_at(const char *why);      // the same, naming the caller (GGML_HIP_TRACE_GRAPH=1 prints it)
+// recording on / off for stream s (switching stream or turning it off submits what is pending)
+void rec_enable(hipStream_t s, bool on);
+// counters: submitted runs, kernels in them, nodes updated in place, graphs instantiated, host ns
+// spent submitting
+void rec_stats(long long *runs, long long *kernels, long long *updated, long long *built, long long *submit_ns);
+// submits what is pending and destroys every cached graph
+void rec_clear_cache();
+
+template <typename... P, typename... A>
+inline void launch_k(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t s, A &&...a) {
+    static_assert(sizeof...(P) == sizeof...(A), "launch_k: argument count");
+    if (!rec_active(s)) {
+        if (rec_pending()) rec_flush_at("eager launch");   // never overtakes recorded launches
+        hipLaunchKernelGGL(k, grid, block, lds, s, std::forward<A>(a)...);
+        return;
+    }
+    // convert every argument to the parameter's exact type, then hand the recorder their addresses
+    struct Holder {
+        alignas(16) unsigned char raw[(sizeof(std::decay_t<P>) + ... + 0) + 16 * sizeof...(P) + 1];
+    } h;
+    void *ptrs[sizeof...(P) + 1];
+    size_t sizes[sizeof...(P) + 1], aligns[sizeof...(P) + 1];
+    size_t off = 0;
+    int i = 0;
+    auto put = [&](auto &&v, auto tag) {
+        using T = typename decltype(tag)::type;
+        static_assert(std::is_trivially_copyable<T>::value, "kernel arguments are copied bytewise");
+        off = (off + alignof(T) - 1) & ~(alignof(T) - 1);
+        new (h.raw + off) T(static_cast<T>(v));
+        ptrs[i] = h.raw + off;
+        sizes[i] = sizeof(T);
+        aligns[i] = alignof(T);
+        off += sizeof(T);
+        i++;
+    };
+    (put(std::forward<A>(a), type_tag<std::decay_t<P>>{}), ...);
+    rec_kernel((const void *)k, grid, block, lds, s, (int)sizeof...(P), ptrs, sizes, aligns);
+}
+
+}  // namespace ghip

@@ -17,6 +17,7 @@
 // d_w*d_x*sumi runs in a different order than AVX2's 8-lane fma chain, so y agrees with the
 // reference within the fp32-accumulation bound (tests/parity.py), not bitwise.
 #include "q4_0_kernels.h"
+#include "launch.h"
 
 #include <climits>
 #include <cstdlib>
@@ -148,7 +149,7 @@ hipError_t quantize_q8_0_aos(const float *x, int64_t K, int64_t N, void *xq8, hi
     if (total8 == 0) return hipSuccess;
     const int64_t grid = (total8 + 255) / 256;
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL(k_quantize_q8_0<true>, dim3((unsigned)grid), dim3(256), 0, s, x, K, total8,
+    launch_k(k_quantize_q8_0<true>, dim3((unsigned)grid), dim3(256), 0, s, x, K, total8,
                        (uint8_t *)xq8, (int8_t *)nullptr, (float *)nullptr);
     return hipGetLastError();
 }
@@ -158,7 +159,7 @@ hipError_t quantize_q8_0_soa(const float *x, int64_t K, int64_t N, int8_t *qs, f
     if (total8 == 0) return hipSuccess;
     const int64_t grid = (total8 + 255) / 256;
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL(k_quantize_q8_0<false>, dim3((unsigned)grid), dim3(256), 0, s, x, K, total8,
+    launch_k(k_quantize_q8_0<false>, dim3((unsigned)grid), dim3(256), 0, s, x, K, total8,
                        (uint8_t *)nullptr, qs, d);
     return hipGetLastError();
 }
@@ -206,7 +207,7 @@ hipError_t quantize_q4_0(const float *w, int64_t K, int64_t M, void *wq, hipStre
     const int64_t nblocks = M * (K / QK);
     if (nblocks == 0) return hipSuccess;
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL(k_quantize_q4_0, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, s, w, nblocks,
+    launch_k(k_quantize_q4_0, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, s, w, nblocks,
                        (uint8_t *)wq);
     return hipGetLastError();
 }
@@ -229,7 +230,7 @@ hipError_t dequantize_q4_0(const void *wq, int64_t K, int64_t M, float *w, hipSt
     const int64_t nblocks = M * (K / QK);
     if (nblocks == 0) return hipSuccess;
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL(k_dequantize_q4_0, dim3((unsigned)((nblocks * 16 + 255) / 256)), dim3(256), 0, s,
+    launch_k(k_dequantize_q4_0, dim3((unsigned)((nblocks * 16 + 255) / 256)), dim3(256), 0, s,
                        (const uint8_t *)wq, nblocks, w);
     return hipGetLastError();
 }
@@ -693,7 +694,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     }
     const int geom = nb | map << 16 | (int)(grid << 18);
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
+    launch_k((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
                        m.W[1], m.W[2], m.row_begin[1], m.row_begin[2], m.row_begin[3], (int)rowbytes, geom, (int)M, tail);
     return hipGetLastError();
 }
@@ -1595,16 +1596,16 @@ hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, 
     const int sk = sk_env ? sk_env : (tiles < 2 * (int64_t)num_cus ? 16 : 8);
     (void)hipGetLastError();  // report only this launch's error
     if (sk == 16 && dp == 4)
-        hipLaunchKernelGGL((k_gemm_sk_q4_0<16, 4>), grid, dim3(1024), 16 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
+        launch_k((k_gemm_sk_q4_0<16, 4>), grid, dim3(1024), 16 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
                            nb, (int)M, xqs, xd, (int)N, (int)K, y, ldy);
     else if (sk == 8 && dp == 4)
-        hipLaunchKernelGGL((k_gemm_sk_q4_0<8, 4>), grid, dim3(512), 8 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
+        launch_k((k_gemm_sk_q4_0<8, 4>), grid, dim3(512), 8 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
                            nb, (int)M, xqs, xd, (int)N, (int)K, y, ldy);
     else if (sk == 16)
-        hipLaunchKernelGGL((k_gemm_sk_q4_0<16, 2>), grid, dim3(1024), 16 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
+        launch_k((k_gemm_sk_q4_0<16, 2>), grid, dim3(1024), 16 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
                            nb, (int)M, xqs, xd, (int)N, (int)K, y, ldy);
     else
-        hipLaunchKernelGGL((k_gemm_sk_q4_0<8, 2>), grid, dim3(512), 8 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
+        launch_k((k_gemm_sk_q4_0<8, 2>), grid, dim3(512), 8 * 16 * 64 * 4, s, (const uint8_t *)W, rowbytes,
                            nb, (int)M, xqs, xd, (int)N, (int)K, y, ldy);
     return hipGetLastError();
 }
@@ -1627,7 +1628,7 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
             attr7 = true;
         }
         (void)hipGetLastError();  // report only this launch's error
-        hipLaunchKernelGGL(k_gemm7_q4_0, grid, dim3(GM_THREADS), G7_LDS, s, (const uint8_t *)W, rowbytes, nb, (int)M,
+        launch_k(k_gemm7_q4_0, grid, dim3(GM_THREADS), G7_LDS, s, (const uint8_t *)W, rowbytes, nb, (int)M,
                            xqs, xd, (int)N, (int)K, y, ldy);
         return hipGetLastError();
     }
@@ -1647,7 +1648,7 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
             attr6 = true;
         }
         (void)hipGetLastError();  // report only this launch's error
-        hipLaunchKernelGGL(k6, grid, dim3(GM_THREADS), 2 * G6_STAGE, s, (const uint8_t *)W, rowbytes, nb, (int)M,
+        launch_k(k6, grid, dim3(GM_THREADS), 2 * G6_STAGE, s, (const uint8_t *)W, rowbytes, nb, (int)M,
                            xqs, xd, (int)N, (int)K, y, ldy);
         return hipGetLastError();
     }
@@ -1664,7 +1665,7 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
         attr_set = true;
     }
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL(kern, grid, dim3(GM_THREADS), 2 * GM_STAGE, s, (const uint8_t *)W, rowbytes, nb,
+    launch_k(kern, grid, dim3(GM_THREADS), 2 * GM_STAGE, s, (const uint8_t *)W, rowbytes, nb,
                        (int)M, xqs, xd, (int)N, (int)K, y, ldy);
     return hipGetLastError();
 }
@@ -1881,7 +1882,7 @@ static hipError_t launch_exact(const void *W, int64_t K, int64_t M, const int8_t
     }
     dim3 grid((unsigned)((M + EX_RB - 1) / EX_RB), (unsigned)((N + NC - 1) / NC));
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL(k_mm_exact_q4_0<NC>, grid, dim3(EX_THREADS), lds, s, (const uint8_t *)W, rowbytes, nb, (int)M,
+    launch_k(k_mm_exact_q4_0<NC>, grid, dim3(EX_THREADS), lds, s, (const uint8_t *)W, rowbytes, nb, (int)M,
                        xqs, xd, (int)N, (int)K, y, ldy);
     return hipGetLastError();
 }
@@ -1919,7 +1920,7 @@ hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const
     if (total == 0) return hipSuccess;
     if (nranks > SCATTER_MAX_RANKS) return hipErrorInvalidValue;
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL(k_scatter_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, slabs, nranks,
+    launch_k(k_scatter_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, slabs, nranks,
                        max_rows, row_begin, N, y, ldy);
     return hipGetLastError();
 }
@@ -1952,7 +1953,7 @@ hipError_t fill_gaussian(float *dst, int64_t n, uint64_t seed, float mean, float
     const int64_t pairs = (n + 1) / 2;
     if (pairs == 0) return hipSuccess;
     (void)hipGetLastError();  // report only this launch's error
-    hipLaunchKernelGGL(k_fill_gaussian, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, dst, n, seed, mean,
+    launch_k(k_fill_gaussian, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, dst, n, seed, mean,
                        stdv);
     return hipGetLastError();
 }

@@ -198,3 +198,45 @@ def test_fast_mode_fusion_bitwise_vs_unfused(tmp_path, hp, n_prompt, n_decode):
     fused = out[1][1]
     assert fused[6] >= 2 * n_decode * hp["n_layer"] and fused[8] >= n_decode * hp["n_layer"], fused
     assert (out[0][1] == 0).all()
+
+
+@pytest.mark.parametrize("exact", [0, 1], ids=["fast", "exact"])
+def test_launch_recorder_bitwise_vs_eager(tmp_path, exact):
+    """The launch recorder (GGML_HIP_GRAPH=1, csrc/launch.h): every kernel of a full-offload eval is
+    recorded and submitted as cached HIP graphs whose position-dependent nodes are updated in place.
+    Prompt + 120 decode steps give the same logits bit for bit as one launch at a time, and the
+    counters show graph replays with in-place updates rather than one instantiation per run."""
+    hp = HP128
+    L = ggml_hip.load()
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp, hp=hp)
+    nv = hp["n_vocab"]
+    lib = ctypes.CDLL(HIP_LIB)
+    lib.refllama_bench.restype = ctypes.c_int
+    lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    L.ggml_hip_debug_set_graph.argtypes = [ctypes.c_int]
+    L.ggml_hip_debug_graph_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    prev = L.ggml_hip_get_exact()
+    ggml_hip.check(L.ggml_hip_set_exact(exact), "set_exact")
+    out, stats = {}, {}
+    try:
+        for graph in (1, 0):
+            ggml_hip.check(L.ggml_hip_debug_set_graph(graph), "set_graph")
+            g0 = np.zeros(5, np.int64)
+            L.ggml_hip_debug_graph_stats(g0.ctypes.data, 1)
+            lg = np.zeros(nv, np.float32)
+            res = np.zeros(3, np.float64)
+            assert lib.refllama_bench(mp.encode(), 24, 120, 1, 99, 1024, 1, res.ctypes.data, lg.ctypes.data) == nv
+            g1 = np.zeros(5, np.int64)
+            L.ggml_hip_debug_graph_stats(g1.ctypes.data, 0)
+            out[graph], stats[graph] = lg, g1 - g0
+    finally:
+        L.ggml_hip_set_exact(prev)
+        L.ggml_hip_debug_set_graph(0)
+    assert np.isfinite(out[1]).all()
+    assert np.array_equal(out[1].view(np.uint32), out[0].view(np.uint32))
+    runs, kernels, updated, built = stats[1][:4]
+    assert runs >= 120 and kernels >= 120 * 10 * hp["n_layer"], stats[1]
+    assert updated > 0, stats[1]                  # n_past-dependent nodes change every step
+    assert built * 10 < runs, stats[1]            # replayed, not re-instantiated per run
+    assert (stats[0][:4] == 0).all(), stats[0]    # recorder off: nothing recorded

@@ -125,8 +125,13 @@ def main():
         if not args.no_cpu:
             res["cpu"], lg_cpu = bench(CPU_LIB, model, args.prompt, args.decode_cpu, args.threads_cpu, 0, 1, nv)
             print("cpu", res["cpu"], file=sys.stderr, flush=True)
+        L.ggml_hip_debug_graph_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
         for mode in args.modes.split(","):
-            gh.check(L.ggml_hip_set_exact(1 if mode == "exact" else 0))
+            # modes: fast, exact; a "-graph" suffix turns the launch recorder on (GGML_HIP_GRAPH=1)
+            gh.check(L.ggml_hip_set_exact(1 if mode.startswith("exact") else 0))
+            gh.check(L.ggml_hip_debug_set_graph(1 if mode.endswith("-graph") else 0))
+            g0 = np.zeros(5, np.int64)
+            L.ggml_hip_debug_graph_stats(g0.ctypes.data, 0)
             L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
             st = np.zeros(69 + 68, np.int64)
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
@@ -140,6 +145,12 @@ def main():
             r["backend_per_op"] = {OP_NAMES.get(i, str(i)): [round(float(st[i]) / (3 + args.decode), 1),
                                                              round(float(st[69 + i]) / 1e3 / (3 + args.decode), 1)]
                                    for i in range(68) if st[i] or st[69 + i]}
+            g1 = np.zeros(5, np.int64)
+            L.ggml_hip_debug_graph_stats(g1.ctypes.data, 0)
+            g = (g1 - g0) / (3 + args.decode)
+            r["graph_per_eval"] = {"runs": round(float(g[0]), 2), "kernels": round(float(g[1]), 1),
+                                   "nodes_updated": round(float(g[2]), 1), "instantiated": round(float(g[3]), 2),
+                                   "submit_ms": round(float(g[4]) / 1e6, 3)}
             r["finite"] = bool(np.isfinite(lg).all())
             if not args.no_cpu:       # same token sequence as the CPU run: compare the last logits
                 _, lg8 = bench(HIP_LIB, model, args.prompt, args.decode_cpu, args.threads_gpu, 99, 1, nv)
@@ -149,6 +160,7 @@ def main():
             res[f"offload_{mode}"] = r
             print(mode, r, file=sys.stderr, flush=True)
         gh.check(L.ggml_hip_set_exact(0))
+        gh.check(L.ggml_hip_debug_set_graph(0))
     finally:
         os.remove(model)
         os.rmdir(d)

@@ -718,7 +718,7 @@ std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of th
 // q4_0 mul_mat run under a pending silu, sibling q4_0 GEMVs (wq|wk|wv, w1|w3) run as one group,
 // independent rope / rope->cpy / cpy nodes held behind a group run as one launch, the decode
 // soft_max chain with its KQV and merged copy as one launch
-constexpr int N_FUSED = 9;
+constexpr int N_FUSED = 10;
 std::atomic<int64_t> g_fused[N_FUSED];
 
 // fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)
@@ -896,6 +896,16 @@ void run_device_op(tensor *t, const tensor *fused_cpy = nullptr) {
 // fused kernels store every intermediate tensor as its own node would, bit for bit.
 // GGML_HIP_FUSE=0 runs every node as its own launch.
 
+std::atomic<int> g_norm_fold{-1};   // GGML_HIP_NORM_FOLD=0: held norm chains run as their own launch
+bool norm_fold_enabled() {
+    int v = g_norm_fold.load(std::memory_order_relaxed);
+    if (v < 0) {
+        v = (!getenv("GGML_HIP_NORM_FOLD") || atoi(getenv("GGML_HIP_NORM_FOLD")) != 0) ? 1 : 0;
+        g_norm_fold.store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
 std::atomic<int> g_fuse{-1};
 bool fuse_enabled() {
     int v = g_fuse.load(std::memory_order_relaxed);
@@ -992,6 +1002,20 @@ struct Pending {
     tensor *node[4] = {};
 };
 Pending g_pend;
+
+// ---- a completed [add ->] rms_norm -> mul chain of one row (decode), held for the q4_0 GEMVs that
+// consume its output: they run it in their x prologue (ghip::gemv_q4_0_multi_norm), one launch less
+// per chain; anything else runs it as its own launch (op_add_rms_norm_mul_f32)
+struct NormChain {
+    bool on = false;
+    int nn = 0;
+    tensor *node[3] = {};          // held copies: add, rms_norm, mul (for the counters)
+    tensor *out_node = nullptr;    // the mul (its output is the GEMVs' src1)
+    const float *a = nullptr, *b = nullptr, *w = nullptr;
+    float *sum = nullptr, *norm = nullptr, *out = nullptr;
+    int64_t ncols = 0;
+};
+NormChain g_norm;
 void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst);
 
 char *dptr(const tensor *t) { return (char *)((ggml_tensor_extra_gpu *)t->extra)->data_device[g_main_device]; }
@@ -1059,6 +1083,9 @@ void flush_pending() {
     for (; i < p.n; i++) run_device_op(p.node[i]);
 }
 
+bool dev_overlap(const tensor *a, const tensor *b);
+size_t span_bytes(const tensor *t);
+
 // t arrives while a chain is pending: extend the chain, complete it in one launch, or let a q4_0
 // mul_mat that touches none of its buffers run first.  false: t does not fit (caller flushes).
 bool try_fuse(tensor *t) {
@@ -1082,6 +1109,33 @@ bool try_fuse(tensor *t) {
         dev_f32(t->src1) && t->src1->ne[0] == t->ne[0] && t->src1->ne[1] == 1 && t->src1->ne[2] == 1 && t->src1->ne[3] == 1) {
         const tensor *add = p.n == 2 ? p.node[0] : nullptr;
         const tensor *x = add ? add : last->src0;     // the rms_norm input
+        // one row (decode): hold it for the q4_0 GEMVs that follow (norm_fold)
+        NormChain c;
+        c.a = add ? (const float *)dptr(add->src0) : nullptr;
+        c.b = add ? (const float *)dptr(add->src1) : (const float *)dptr(x);
+        c.sum = add ? (float *)dptr(add) : nullptr;
+        c.norm = (float *)dptr(last);
+        c.w = (const float *)dptr(t->src1);
+        c.out = (float *)dptr(t);
+        c.ncols = t->ne[0];
+        auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+        bool fold = norm_fold_enabled() && !exact_mode() && gabi::nrows(t) == 1 && c.ncols % 64 == 0 &&
+                    c.ncols <= 16384 && al(c.a) && al(c.b) && al(c.sum) && al(c.norm) && al(c.w) && al(c.out);
+        // the chain's outputs must not alias its inputs (the GEMV's workgroups read the inputs while
+        // workgroup 0 stores the outputs)
+        for (const tensor *o : {add, (const tensor *)last, (const tensor *)t})
+            for (const tensor *i : {(const tensor *)(add ? add->src0 : nullptr), (const tensor *)(add ? add->src1 : x),
+                                    (const tensor *)t->src1})
+                if (o && i && dev_overlap(o, i)) fold = false;
+        if (fold) {
+            for (int i = 0; i < p.n; i++) c.node[c.nn++] = p.node[i];
+            c.node[c.nn++] = hold(t);
+            c.out_node = c.node[c.nn - 1];
+            c.on = true;
+            g_norm = c;
+            p = Pending{};
+            return true;
+        }
         HIP_FATAL(hipSetDevice(id));
         HIP_FATAL(ghip::op_add_rms_norm_mul_f32(add ? (const float *)dptr(add->src0) : nullptr,
                                                 add ? (const float *)dptr(add->src1) : (const float *)dptr(x),
@@ -1198,6 +1252,7 @@ struct Group {
     int n = 0, na = 0;
     tensor *mm[4] = {};
     tensor *after[16] = {};
+    NormChain norm;                // the held norm chain the GEMVs run in their prologue (or off)
 };
 Group g_grp;
 void execute_node(tensor *t);
@@ -1263,9 +1318,11 @@ bool group_after_ok(const tensor *t) {
 }
 
 // may q4_0 mul_mat m run before every held node and beside the current members?
+bool norm_feeds(const NormChain &c, const tensor *m);
 bool group_join_ok(const tensor *m) {
     const Group &g = g_grp;
     if (g.n >= 4 || !same_tensor(m->src1, g.mm[0]->src1) || m->src0->ne[0] != g.mm[0]->src0->ne[0]) return false;
+    if (g.norm.on && !norm_feeds(g.norm, m)) return false;
     for (int i = 0; i < g.n; i++)
         if (dev_overlap(m, g.mm[i]) || dev_overlap(m, g.mm[i]->src1)) return false;
     for (int i = 0; i < g.na; i++) {
@@ -1384,9 +1441,55 @@ int run_elem_prefix(tensor *const *held, int nh) {
     return used;
 }
 
+void launch_norm_chain(const NormChain &c) {
+    const int id = g_main_device;
+    HIP_FATAL(hipSetDevice(id));
+    HIP_FATAL(ghip::op_add_rms_norm_mul_f32(c.a, c.b, c.sum, c.norm, c.w, c.out, c.ncols, 1, g_dev[id].stream));
+    for (int i = 0; i < c.nn; i++) count_node(c.node[i]);
+    g_fused[0].fetch_add(1, std::memory_order_relaxed);
+}
+void flush_norm() {
+    const NormChain c = g_norm;
+    g_norm = NormChain{};
+    if (c.on) launch_norm_chain(c);
+}
+// may a held norm chain's output feed q4_0 mul_mat m through its GEMV prologue?
+bool norm_feeds(const NormChain &c, const tensor *m) {
+    if (!c.on || !same_tensor(m->src1, c.out_node) || m->src1->ne[1] != 1 || m->src0->ne[0] != c.ncols) return false;
+    // m's output must not alias anything the prologue reads or workgroup 0 stores
+    const char *y = dptr(m);
+    const size_t yb = span_bytes(m), row = (size_t)c.ncols * 4;
+    for (const void *q : {(const void *)c.a, (const void *)c.b, (const void *)c.w, (const void *)c.sum,
+                          (const void *)c.norm, (const void *)c.out})
+        if (q && (const char *)q < y + yb && y < (const char *)q + row) return false;
+    return true;
+}
+
 void flush_group() {
     const Group g = g_grp;
     g_grp = Group{};
+    if (g.norm.on) {                      // the GEMVs run the held norm chain in their prologue
+        const void *w[4];
+        int64_t m[4], ldy[4];
+        float *y[4];
+        for (int i = 0; i < g.n; i++) {
+            w[i] = dptr(g.mm[i]->src0);
+            m[i] = ldy[i] = g.mm[i]->src0->ne[1];
+            y[i] = (float *)dptr(g.mm[i]);
+        }
+        const ghip::GemvNorm nrm{g.norm.a, g.norm.w, g.norm.sum, g.norm.norm, g.norm.out};
+        HIP_FATAL(hipSetDevice(g_main_device));
+        HIP_FATAL(ghip::gemv_q4_0_multi_norm(g.n, w, m, g.norm.ncols, g.norm.b, nrm, y, ldy,
+                                             g_dev[g_main_device].info, g_dev[g_main_device].stream));
+        for (int i = 0; i < g.norm.nn; i++) count_node(g.norm.node[i]);
+        for (int i = 0; i < g.n; i++) count_node(g.mm[i]);
+        g_fused[0].fetch_add(1, std::memory_order_relaxed);
+        g_fused[9].fetch_add(1, std::memory_order_relaxed);
+        if (g.n > 1) g_fused[6].fetch_add(1, std::memory_order_relaxed);
+        const int done = run_elem_prefix(g.after, g.na);
+        for (int i = done; i < g.na; i++) execute_node(g.after[i]);
+        return;
+    }
     if (trace_nodes()) fprintf(stderr, "group flush: %d mul_mats (%s ...), %d held nodes\n", g.n, g.mm[0]->name, g.na);
     if (g.n == 1) {
         count_node(g.mm[0]);
@@ -1418,6 +1521,19 @@ void execute_node(tensor *t) {
         count_node(t);                      // no data touched: a pending chain stays pending
         return;
     }
+    // a held norm chain: a GEMV that consumes it opens a group that runs it in its prologue
+    auto open_norm_group = [&]() {
+        if (!g_norm.on || g_grp.n != 0 || g_pend.n != 0 || !group_mm_ok(t) || !norm_feeds(g_norm, t)) return false;
+        g_grp.mm[0] = hold(t);
+        g_grp.n = 1;
+        g_grp.norm = g_norm;
+        g_norm = NormChain{};
+        return true;
+    };
+    if (g_norm.on) {
+        if (open_norm_group()) return;
+        flush_norm();                         // anything else: the chain runs as its own launch
+    }
     if (g_grp.n > 0) {
         if (group_mm_ok(t) && group_join_ok(t)) {
             g_grp.mm[g_grp.n++] = hold(t);
@@ -1431,7 +1547,9 @@ void execute_node(tensor *t) {
             g_grp.after[g_grp.na++] = hold(t);
             return;
         }
-        flush_group();
+        flush_group();                        // its held nodes may complete a norm chain t consumes
+        if (open_norm_group()) return;
+        if (g_norm.on) flush_norm();
     }
     if (g_pend.n == 0 && group_mm_ok(t)) {
         g_grp.mm[0] = hold(t);
@@ -1477,6 +1595,7 @@ static inline bool graph_enabled() { return graph_flag().load(std::memory_order_
 
 static inline void flush_deferred() {
     if (g_grp.n > 0) flush_group();
+    if (g_norm.on) flush_norm();
     if (g_pend.n > 0) flush_pending();
     ghip::rec_flush_at("entry point");        // and submit the recorded launches (launch.h)
 }
@@ -1914,7 +2033,7 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
                 t->src1 ? t->src1->name : "-");
     const auto t0 = std::chrono::steady_clock::now();
     (void)f16_mul_mat;
-    if (g_grp.n == 0 && g_pend.n == 0) {
+    if (g_grp.n == 0 && g_pend.n == 0 && !g_norm.on) {
         snap_reset();                      // nothing held: the copies are garbage
     } else if (g_snaps.memo.count(t)) {
         flush_deferred();                  // t arrives again: a new graph at the old addresses
@@ -2779,6 +2898,13 @@ int ggml_hip_debug_graph_stats(long long *out, int clear) {
     flush_deferred();
     ghip::rec_stats(&out[0], &out[1], &out[2], &out[3], &out[4]);
     if (clear) ghip::rec_clear_cache();
+    return GGML_HIP_OK;
+}
+
+// not in the public header: the decode norm chain folded into the GEMV prologue on (1) / off (0)
+int ggml_hip_debug_set_norm_fold(int on) {
+    flush_deferred();
+    g_norm_fold.store(on ? 1 : 0);
     return GGML_HIP_OK;
 }
 

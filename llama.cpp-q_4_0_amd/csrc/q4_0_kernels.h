@@ -41,6 +41,18 @@ constexpr int GEMV_MULTI_MAX = 4;
 hipError_t gemv_q4_0_multi(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *x, int64_t N,
                            float *const *y, const int64_t *ldy, const DeviceInfo &dev, hipStream_t s);
 
+// The same for N = 1 with ggml's [add ->] rms_norm -> mul(norm weight row) chain folded into the x
+// prologue: x = (a ? a + b : b), x *= 1/sqrt(mean(x*x) + 1e-6) (double sum, as ggml_ops.hip's
+// k_row_norm4), x *= w; the GEMVs consume x, and workgroup 0 also stores the chain's tensors (sum =
+// a + b, norm, out; each may be null) bit for bit as the unfused launches.  K <= 16384.
+struct GemvNorm {
+    const float *a, *w;
+    float *sum, *norm, *out;
+};
+hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *b,
+                                const GemvNorm &nrm, float *const *y, const int64_t *ldy, const DeviceInfo &dev,
+                                hipStream_t s);
+
 // test hook: force the GEMV launch policy (row mapping 0/1/2, ring depth 1/2, row items 0/1,
 // workgroups per CU); -1 / 0 = automatic
 void gemv_set_policy(int map, int depth, int rowitems, int wg_per_cu);

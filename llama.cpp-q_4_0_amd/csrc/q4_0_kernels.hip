@@ -335,6 +335,7 @@ struct GemvTail {
     const uint8_t *W3;
     float *y[GEMV_MAXMAT];
     int64_t ldy[GEMV_MAXMAT];
+    GemvNorm nrm;                         // NORM instantiations only
 };
 // geom = nb | map << 16 | grid << 18  (nb < 2^16, grid < 2^14; checked by the launcher)
 
@@ -351,7 +352,13 @@ struct GemvTail {
 //                     row (PPL = ceil(pairs/64)), so one item is a whole row: all of its loads are
 //                     in flight together and it is reduced once (a row of K=4160 no longer costs two
 //                     items for one extra pair).  PPL == 0: 64-pair chunks, one item per chunk.
-template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0>
+__device__ __forceinline__ double wave_sum_d64(double v) {   // every lane gets the sum
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, bool NORM = false>
 __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restrict__ x_, const uint8_t *W0,
                                                           const uint8_t *W1, const uint8_t *W2, int rb1_, int rb2_,
                                                           int rb3_, int rowbytes_, int geom, int M_,
@@ -472,7 +479,87 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
     constexpr bool KO_LDS = DIAG == 9 || DIAG == 10;
     u32x4 xv[GEMV_PRO];
     ItemRegs buf[DEPTH];
-    if constexpr (XSPLIT) {
+    if constexpr (NORM) {
+        // [add ->] rms_norm -> mul fused into the x prologue (NT == 1, one round of x-waves: the
+        // launcher checks K <= 16 * 64 * 4 * GEMV_XPRO).  The x-waves hold the row in registers, sum
+        // its squares in double (order-free in practice, as k_row_norm4's), exchange the per-wave
+        // sums through LDS (one extra workgroup barrier), then scale, multiply by the norm weight and
+        // quantize; workgroup 0 also stores the chain's tensors.
+        static_assert(NT == 1 && XSPLIT, "norm prologue: decode x-wave form only");
+        double *npart = reinterpret_cast<double *>(xs + NT * nb);
+        const int XW = (total + 64 * GEMV_XPRO - 1) / (64 * GEMV_XPRO);
+        const int XT = XW * 64;
+        const GemvNorm nrm = tail.nrm;
+        float4 v[GEMV_XPRO];
+        u32x4 rg[GEMV_XPRO];                                   // the norm weight, loaded with x
+        if (wave < XW) {
+            const __amdgpu_buffer_rsrc_t ar = make_rsrc(nrm.a ? (const void *)nrm.a : (const void *)x,
+                                                        nrm.a ? (uint32_t)total * 16u : 0u);
+            const __amdgpu_buffer_rsrc_t gr = make_rsrc(nrm.w, (uint32_t)total * 16u);
+            u32x4 rb[GEMV_XPRO], ra[GEMV_XPRO];
+#pragma unroll
+            for (int i = 0; i < GEMV_XPRO; i++) {
+                rb[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * XT), 0, 0);
+                ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ar, 16 * (tid + i * XT), 0, 0);
+                rg[i] = __builtin_amdgcn_raw_buffer_load_b128(gr, 16 * (tid + i * XT), 0, 0);
+            }
+            if constexpr (!XHOLD) {
+#pragma unroll
+                for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+            }
+            double ss = 0.0;
+#pragma unroll
+            for (int i = 0; i < GEMV_XPRO; i++) {
+                float4 b4 = make_float4(__uint_as_float(rb[i].x), __uint_as_float(rb[i].y), __uint_as_float(rb[i].z),
+                                        __uint_as_float(rb[i].w));
+                if (nrm.a)                                     // a + b, as k_add_f32 / k_row_norm4
+                    b4 = make_float4(__uint_as_float(ra[i].x) + b4.x, __uint_as_float(ra[i].y) + b4.y,
+                                     __uint_as_float(ra[i].z) + b4.z, __uint_as_float(ra[i].w) + b4.w);
+                v[i] = b4;                                     // past the row: 0 (descriptor)
+                ss += (double)(b4.x * b4.x);
+                ss += (double)(b4.y * b4.y);
+                ss += (double)(b4.z * b4.z);
+                ss += (double)(b4.w * b4.w);
+            }
+            ss = wave_sum_d64(ss);
+            if (lane == 0) npart[wave] = ss;
+        } else {
+#pragma unroll
+            for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+        }
+        GEMV_STAMP(1);
+        __syncthreads();                                       // the per-wave sums
+        if (wave < XW) {
+            double t = 0.0;
+            for (int i = 0; i < XW; i++) t += npart[i];
+            const float mean = (float)(t / (double)(nb * QK));
+            const float scale = 1.0f / (float)__builtin_sqrt((double)(mean + 1e-6f));
+            const bool store = blockIdx.x == 0;
+#pragma unroll
+            for (int i = 0; i < GEMV_XPRO; i++) {
+                const int idx = tid + i * XT;
+                if (idx < total) {
+                    const float4 xv4 = v[i];
+                    const float4 y = make_float4(xv4.x * scale, xv4.y * scale, xv4.z * scale, xv4.w * scale);
+                    const float4 g = make_float4(__uint_as_float(rg[i].x), __uint_as_float(rg[i].y),
+                                                 __uint_as_float(rg[i].z), __uint_as_float(rg[i].w));
+                    const float4 o = make_float4(y.x * g.x, y.y * g.y, y.z * g.z, y.w * g.w);
+                    if (store) {
+                        if (nrm.sum) reinterpret_cast<float4 *>(nrm.sum)[idx] = xv4;
+                        if (nrm.norm) reinterpret_cast<float4 *>(nrm.norm)[idx] = y;
+                        if (nrm.out) reinterpret_cast<float4 *>(nrm.out)[idx] = o;
+                    }
+                    quantize_into_lds(u32x4{__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
+                                            __float_as_uint(o.w)}, idx);
+                }
+            }
+            if constexpr (XHOLD) {
+#pragma unroll
+                for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+            }
+        }
+        GEMV_STAMP(2);
+    } else if constexpr (XSPLIT) {
         // x-waves: wave < XW load + quantize x (XT threads, PRO float4 each per round), then issue
         // their weight loads; the other waves only issue weight loads
         const int XW0 = (total + 64 * GEMV_XPRO - 1) / (64 * GEMV_XPRO);
@@ -653,11 +740,12 @@ int gemv_max_tokens(int64_t K) {
 }
 
 
-template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0>
-static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s) {
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, bool NORM = false>
+static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s,
+                                const GemvNorm *nrm = nullptr) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
-    const size_t lds = (size_t)NT * nb * 40;
+    const size_t lds = (size_t)NT * nb * 40 + (NORM ? WAVES * sizeof(double) : 0);
     const int wg_per_cu_env = gemv_policy().wg_per_cu;
     const int64_t M = m.row_begin[m.n];
     const int64_t need = (M + WAVES - 1) / WAVES;
@@ -667,7 +755,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     static int occ = 0;                    // resident workgroups per CU for this instantiation
     if (occ == 0) {
         int nb_occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, NORM>,
                                                          WAVES * 64, lds) != hipSuccess || nb_occ < 1)
             nb_occ = 1;
         occ = nb_occ;
@@ -686,7 +774,8 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
             : ((M % ((int64_t)grid * WAVES)) % (cus * WAVES) == 0 ? 0 : ((int64_t)grid > cus ? 1 : 2));
     if (map == 2 && (int64_t)grid * M >= (int64_t)1 << 32) map = 1;   // the kernel's 32-bit row split
     if (nb >= (1 << 16) || grid >= (1u << 14) || rowbytes > INT_MAX || M > INT_MAX) return hipErrorInvalidValue;
-    GemvTail tail;
+    GemvTail tail{};
+    if (nrm) tail.nrm = *nrm;
     tail.W3 = m.W[3];
     for (int i = 0; i < GEMV_MAXMAT; i++) {
         tail.y[i] = m.y[i];
@@ -694,7 +783,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     }
     const int geom = nb | map << 16 | (int)(grid << 18);
     (void)hipGetLastError();  // report only this launch's error
-    launch_k((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
+    launch_k((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, NORM>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
                        m.W[1], m.W[2], m.row_begin[1], m.row_begin[2], m.row_begin[3], (int)rowbytes, geom, (int)M, tail);
     return hipGetLastError();
 }
@@ -800,6 +889,53 @@ hipError_t gemv_q4_0_multi(int nmat, const void *const *W, const int64_t *M, int
 hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_t N, float *y, int64_t ldy,
                      const DeviceInfo &dev, hipStream_t s) {
     return gemv_q4_0_multi(1, &W, &M, K, x, N, &y, &ldy, dev, s);
+}
+
+template <int VAR, int PPL>
+static hipError_t launch_gemv_norm(const GemvMats &m, int64_t K, const float *b, const DeviceInfo &dev, hipStream_t s,
+                                   const GemvNorm &nrm, int rd) {
+    return rd == 2 ? launch_gemv_w<1, 0, 16, 2, VAR, PPL, true>(m, K, b, dev, s, &nrm)
+                   : launch_gemv_w<1, 0, 16, 1, VAR, PPL, true>(m, K, b, dev, s, &nrm);
+}
+
+hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *b,
+                                const GemvNorm &nrm, float *const *y, const int64_t *ldy, const DeviceInfo &dev,
+                                hipStream_t s) {
+    // one round of x-waves holds the row: K / 4 float4 <= 16 waves * 64 lanes * GEMV_XPRO
+    if (nmat < 1 || nmat > GEMV_MAXMAT || K % 64 != 0 || K / 4 > 16 * 64 * GEMV_XPRO || !b || !nrm.w)
+        return hipErrorInvalidValue;
+    GemvMats m{};
+    m.n = nmat;
+    m.row_begin[0] = 0;
+    for (int i = 0; i < nmat; i++) {
+        m.W[i] = (const uint8_t *)W[i];
+        m.y[i] = y[i];
+        m.ldy[i] = ldy[i];
+        m.row_begin[i + 1] = m.row_begin[i] + (int)M[i];
+    }
+    for (int i = nmat; i < GEMV_MAXMAT; i++) {
+        m.W[i] = m.W[0];
+        m.y[i] = m.y[0];
+        m.ldy[i] = m.ldy[0];
+        m.row_begin[i + 1] = m.row_begin[i];
+    }
+    // the same policy as launch_gemv<1> (row items, ring depth, VAR 15 for short rows)
+    static const int var_env = env_int("GGML_HIP_GEMV_VAR", -1);
+    const int depth_env = gemv_policy().depth;
+    const int64_t Mrows = m.row_begin[m.n];
+    const int var = var_env == 15 || var_env == 3 ? var_env : (K <= 8192 && Mrows <= 2 * 512 * 16 ? 15 : 3);
+    const int rd = depth_env == 2 ? 2 : 1;
+    const int ppl = (int)((K / 64 + 63) / 64);
+    if (var == 15) {
+        if (ppl == 1) return launch_gemv_norm<15, 1>(m, K, b, dev, s, nrm, rd);
+        if (ppl == 2) return launch_gemv_norm<15, 2>(m, K, b, dev, s, nrm, rd);
+        if (ppl == 3) return launch_gemv_norm<15, 3>(m, K, b, dev, s, nrm, rd);
+    } else {
+        if (ppl == 1) return launch_gemv_norm<3, 1>(m, K, b, dev, s, nrm, rd);
+        if (ppl == 2) return launch_gemv_norm<3, 2>(m, K, b, dev, s, nrm, rd);
+        if (ppl == 3) return launch_gemv_norm<3, 3>(m, K, b, dev, s, nrm, rd);
+    }
+    return hipErrorInvalidValue;        // K > 12288: chunked items are not instantiated with the prologue
 }
 
 // ---------------------------------------------------------------------------------------------

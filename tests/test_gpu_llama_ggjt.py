@@ -31,7 +31,7 @@ pytestmark = [pytest.mark.gpu,
 OPS = json.load(open(os.path.join(GOLD, "ggml_op_enum.json")))
 
 
-N_FUSED = 9   # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
+N_FUSED = 10  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
 
 
 def op_stats(L, reset=True, fused=False):
@@ -197,7 +197,44 @@ def test_fast_mode_fusion_bitwise_vs_unfused(tmp_path, hp, n_prompt, n_decode):
     assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
     fused = out[1][1]
     assert fused[6] >= 2 * n_decode * hp["n_layer"] and fused[8] >= n_decode * hp["n_layer"], fused
+    # slot 9: the decode norm chains (attention and ffn norm; layer 0's attention norm reads the host
+    # embedding row, so it is no device chain) run in the q4_0 GEMVs' x prologue
+    assert fused[9] >= (2 * hp["n_layer"] - 1) * n_decode, fused
     assert (out[0][1] == 0).all()
+
+
+@pytest.mark.parametrize("hp,n_prompt,n_decode", [(HP128, 40, 60), (G.HP, 8, 40)], ids=["head128", "head64"])
+def test_norm_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode):
+    """The decode [add ->] rms_norm -> mul chain folded into the x prologue of the q4_0 GEMVs that
+    consume it (ghip::gemv_q4_0_multi_norm): the same logits bit for bit as the chain's own launch
+    followed by the GEMV group, and the fold fires for every device norm chain of a decode eval."""
+    L = ggml_hip.load()
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp, hp=hp)
+    nv = hp["n_vocab"]
+    lib = ctypes.CDLL(HIP_LIB)
+    lib.refllama_bench.restype = ctypes.c_int
+    lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    L.ggml_hip_debug_set_norm_fold.argtypes = [ctypes.c_int]
+    prev = L.ggml_hip_get_exact()
+    ggml_hip.check(L.ggml_hip_set_exact(0), "set_exact")
+    out = {}
+    try:
+        for fold in (1, 0):
+            ggml_hip.check(L.ggml_hip_debug_set_norm_fold(fold), "set_norm_fold")
+            op_stats(L)
+            lg = np.zeros(nv, np.float32)
+            res = np.zeros(3, np.float64)
+            assert lib.refllama_bench(mp.encode(), n_prompt, n_decode, 1, 99, 1024, 1, res.ctypes.data, lg.ctypes.data) == nv
+            out[fold] = (lg, op_stats(L, fused=True)[1])
+    finally:
+        L.ggml_hip_set_exact(prev)
+        L.ggml_hip_debug_set_norm_fold(1)
+    assert np.isfinite(out[1][0]).all()
+    assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
+    assert out[1][1][9] >= (2 * hp["n_layer"] - 1) * n_decode, out[1][1]
+    assert out[0][1][9] == 0, out[0][1]
+    assert out[1][1][0] == out[0][1][0], (out[1][1], out[0][1])     # every chain still counted once
 
 
 @pytest.mark.parametrize("exact", [0, 1], ids=["fast", "exact"])

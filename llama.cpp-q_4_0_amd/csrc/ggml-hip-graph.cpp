@@ -13,8 +13,12 @@
 // The results are the kernels' own, so every bitwise test of the eager path holds for the recorded one.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <mutex>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -51,9 +55,62 @@ struct Cached {
     uint64_t used = 0;
 };
 
+// ---- mode 2: a launcher thread.  The node walk appends each launch (function, geometry, argument
+// bytes) to a ring; one worker thread issues them with hipLaunchKernel in order.  The walk's own
+// logic and the ~2.6 us per hipLaunchKernel then run on two cores instead of one; every sync point
+// waits until the worker has issued everything before it (same stream order as eager launches).
+constexpr size_t RING = 1024, SLOT_BLOB = 1008;
+struct Slot {
+    const void *fn;
+    dim3 grid, block;
+    uint32_t lds;
+    int nargs;
+    uint16_t off[MAX_ARGS];
+    alignas(16) unsigned char blob[SLOT_BLOB];
+};
+struct Launcher {
+    std::atomic<uint64_t> head{0}, tail{0};
+    std::atomic<int> err{0};
+    std::atomic<bool> sleeping{false};
+    std::mutex mu;
+    std::condition_variable cv;
+    hipStream_t stream = nullptr;
+    int device = 0;
+    bool started = false;
+    Slot ring[RING];
+};
+Launcher &launcher() {
+    static Launcher *l = new Launcher;   // never destroyed: the worker may outlive static destructors
+    return *l;
+}
+void launcher_main(Launcher *L) {
+    (void)hipSetDevice(L->device);
+    void *argv[MAX_ARGS];
+    for (;;) {
+        uint64_t t = L->tail.load(std::memory_order_relaxed);
+        int spins = 0;
+        while (L->head.load(std::memory_order_acquire) == t) {
+            if (++spins < 20000) {
+                std::this_thread::yield();
+                continue;
+            }
+            std::unique_lock<std::mutex> lk(L->mu);
+            L->sleeping.store(true, std::memory_order_seq_cst);
+            L->cv.wait(lk, [&] { return L->head.load(std::memory_order_acquire) != t; });
+            L->sleeping.store(false, std::memory_order_relaxed);
+        }
+        Slot &sl = L->ring[t % RING];
+        for (int a = 0; a < sl.nargs; a++) argv[a] = sl.blob + sl.off[a];
+        const hipError_t e = hipLaunchKernel(sl.fn, sl.grid, sl.block, argv, sl.lds, L->stream);
+        if (e != hipSuccess) L->err.store((int)e, std::memory_order_relaxed);
+        L->tail.store(t + 1, std::memory_order_release);
+    }
+}
+
 struct Recorder {
     hipStream_t stream = nullptr;
     bool on = false;
+    int mode = 1;             // 1: HIP graphs, 2: launcher thread
     Run cur;
     std::vector<Cached *> cache;
     uint64_t clock = 0;
@@ -180,7 +237,60 @@ bool rec_active(hipStream_t s) {
     return r.on && s == r.stream;
 }
 
-bool rec_pending() { return !rec().cur.items.empty(); }
+bool rec_pending() {
+    if (!rec().cur.items.empty()) return true;
+    const Launcher &L = launcher();
+    return L.started && L.head.load(std::memory_order_relaxed) != L.tail.load(std::memory_order_acquire);
+}
+
+namespace {
+void async_push(const void *fn, dim3 grid, dim3 block, size_t lds, int nargs, void *const *args, const size_t *sizes,
+                const size_t *aligns) {
+    Launcher &L = launcher();
+    Recorder &r = rec();
+    if (!L.started) {
+        L.stream = r.stream;
+        (void)hipGetDevice(&L.device);
+        L.started = true;
+        std::thread(launcher_main, &L).detach();
+    }
+    if (L.stream != r.stream) {                // the worker serves one stream: drain, then switch
+        while (L.tail.load(std::memory_order_acquire) != L.head.load(std::memory_order_relaxed)) std::this_thread::yield();
+        L.stream = r.stream;
+    }
+    const uint64_t h = L.head.load(std::memory_order_relaxed);
+    while (h - L.tail.load(std::memory_order_acquire) >= RING) std::this_thread::yield();
+    Slot &sl = L.ring[h % RING];
+    sl.fn = fn;
+    sl.grid = grid;
+    sl.block = block;
+    sl.lds = (uint32_t)lds;
+    sl.nargs = nargs;
+    size_t used = 0;
+    for (int i = 0; i < nargs; i++) {
+        const size_t off = (used + aligns[i] - 1) & ~(aligns[i] - 1);
+        if (off + sizes[i] > SLOT_BLOB) {
+            fprintf(stderr, "ggml-hip: launcher thread: %zu argument bytes exceed the slot\n", off + sizes[i]);
+            exit(1);
+        }
+        memcpy(sl.blob + off, args[i], sizes[i]);
+        sl.off[i] = (uint16_t)off;
+        used = off + sizes[i];
+    }
+    L.head.store(h + 1, std::memory_order_release);
+    if (L.sleeping.load(std::memory_order_seq_cst)) {
+        std::lock_guard<std::mutex> lk(L.mu);
+        L.cv.notify_one();
+    }
+}
+void async_drain() {
+    Launcher &L = launcher();
+    if (!L.started) return;
+    const uint64_t h = L.head.load(std::memory_order_relaxed);
+    while (L.tail.load(std::memory_order_acquire) != h) std::this_thread::yield();
+    if (const int e = L.err.exchange(0)) fatal((hipError_t)e, "hipLaunchKernel (launcher thread)");
+}
+}  // namespace
 
 void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, int nargs, void *const *args,
                 const size_t *sizes, const size_t *aligns) {
@@ -190,6 +300,10 @@ void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s
         exit(1);
     }
     (void)s;
+    if (r.mode == 2) {
+        async_push(fn, grid, block, lds, nargs, args, sizes, aligns);
+        return;
+    }
     Item it;
     it.fn = fn;
     it.grid = grid;
@@ -221,7 +335,10 @@ void rec_flush_at(const char *why) {
     rec_flush();
 }
 
-void rec_flush() { submit(false); }
+void rec_flush() {
+    async_drain();
+    submit(false);
+}
 
 namespace {
 void submit(bool chunk) {
@@ -273,6 +390,11 @@ void submit(bool chunk) {
 
 // recording on / off for stream s; switching streams submits what is pending (turning recording off
 // does not: the next eager launch or sync point does)
+void rec_set_mode(int mode) {
+    rec_flush();
+    rec().mode = mode == 2 ? 2 : 1;
+}
+
 void rec_enable(hipStream_t s, bool on) {
     Recorder &r = rec();
     if (s != r.stream) rec_flush();

@@ -1587,11 +1587,17 @@ void execute_node(tensor *t) {
 static std::atomic<int> &graph_flag() {
     static std::atomic<int> f([] {
         const char *e = getenv("GGML_HIP_GRAPH");
-        return (e && atoi(e) != 0) ? 1 : 0;
+        return e ? atoi(e) : 0;
     }());
     return f;
 }
 static inline bool graph_enabled() { return graph_flag().load(std::memory_order_relaxed) != 0; }
+static inline void graph_apply_mode() {          // 1: HIP graphs, 2: launcher thread (launch.h)
+    static int applied = -1;
+    const int m = graph_flag().load(std::memory_order_relaxed);
+    if (m != applied && m != 0) ghip::rec_set_mode(m);
+    applied = m;
+}
 
 static inline void flush_deferred() {
     if (g_grp.n > 0) flush_group();
@@ -2042,6 +2048,7 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
     // graphs (launch.h)
     g_eval_computed = true;
     const bool use_graph = graph_enabled();
+    if (use_graph) graph_apply_mode();
     if (use_graph) ghip::rec_enable(g_dev[g_main_device].stream, true);
     execute_node(t);
     if (use_graph) ghip::rec_enable(g_dev[g_main_device].stream, false);
@@ -2908,10 +2915,10 @@ int ggml_hip_debug_set_norm_fold(int on) {
     return GGML_HIP_OK;
 }
 
-// not in the public header: launch recording on (1) / off (0) for the hook path (tests run both)
+// not in the public header: launch recording for the hook path: 0 off, 1 HIP graphs, 2 launcher thread
 int ggml_hip_debug_set_graph(int on) {
     flush_deferred();
-    graph_flag().store(on ? 1 : 0);
+    graph_flag().store(on);
     return GGML_HIP_OK;
 }
 

@@ -35,6 +35,8 @@ void rec_flush();
 void rec_flush_at(const char *why);      // the same, naming the caller (GGML_HIP_TRACE_GRAPH=1 prints it)
 // recording on / off for stream s (switching stream or turning it off submits what is pending)
 void rec_enable(hipStream_t s, bool on);
+// 1: runs submitted as cached HIP graphs; 2: a launcher thread issues the launches in order
+void rec_set_mode(int mode);
 // counters: submitted runs, kernels in them, nodes updated in place, graphs instantiated, host ns
 // spent submitting
 void rec_stats(long long *runs, long long *kernels, long long *updated, long long *built, long long *submit_ns);

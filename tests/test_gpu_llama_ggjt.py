@@ -237,12 +237,14 @@ def test_norm_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode):
     assert out[1][1][0] == out[0][1][0], (out[1][1], out[0][1])     # every chain still counted once
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["graphs", "thread"])
 @pytest.mark.parametrize("exact", [0, 1], ids=["fast", "exact"])
-def test_launch_recorder_bitwise_vs_eager(tmp_path, exact):
-    """The launch recorder (GGML_HIP_GRAPH=1, csrc/launch.h): every kernel of a full-offload eval is
-    recorded and submitted as cached HIP graphs whose position-dependent nodes are updated in place.
-    Prompt + 120 decode steps give the same logits bit for bit as one launch at a time, and the
-    counters show graph replays with in-place updates rather than one instantiation per run."""
+def test_launch_recorder_bitwise_vs_eager(tmp_path, exact, mode):
+    """The launch recorder (csrc/launch.h): GGML_HIP_GRAPH=1 records every kernel of a full-offload
+    eval and submits cached HIP graphs whose position-dependent nodes are updated in place;
+    GGML_HIP_GRAPH=2 hands the launches to a launcher thread.  Prompt + 120 decode steps give the same
+    logits bit for bit as one launch at a time; in graph mode the counters show replays with in-place
+    updates rather than one instantiation per run."""
     hp = HP128
     L = ggml_hip.load()
     mp = str(tmp_path / "m.ggjt")
@@ -257,7 +259,7 @@ def test_launch_recorder_bitwise_vs_eager(tmp_path, exact):
     ggml_hip.check(L.ggml_hip_set_exact(exact), "set_exact")
     out, stats = {}, {}
     try:
-        for graph in (1, 0):
+        for graph in (mode, 0):
             ggml_hip.check(L.ggml_hip_debug_set_graph(graph), "set_graph")
             g0 = np.zeros(5, np.int64)
             L.ggml_hip_debug_graph_stats(g0.ctypes.data, 1)
@@ -270,10 +272,12 @@ def test_launch_recorder_bitwise_vs_eager(tmp_path, exact):
     finally:
         L.ggml_hip_set_exact(prev)
         L.ggml_hip_debug_set_graph(0)
-    assert np.isfinite(out[1]).all()
-    assert np.array_equal(out[1].view(np.uint32), out[0].view(np.uint32))
+    assert np.isfinite(out[mode]).all()
+    assert np.array_equal(out[mode].view(np.uint32), out[0].view(np.uint32))
+    assert (stats[0][:4] == 0).all(), stats[0]    # recorder off: nothing recorded
+    if mode == 2:
+        return
     runs, kernels, updated, built = stats[1][:4]
     assert runs >= 120 and kernels >= 120 * 10 * hp["n_layer"], stats[1]
     assert updated > 0, stats[1]                  # n_past-dependent nodes change every step
     assert built * 10 < runs, stats[1]            # replayed, not re-instantiated per run
-    assert (stats[0][:4] == 0).all(), stats[0]    # recorder off: nothing recorded

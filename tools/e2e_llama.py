@@ -127,9 +127,10 @@ def main():
             print("cpu", res["cpu"], file=sys.stderr, flush=True)
         L.ggml_hip_debug_graph_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
         for mode in args.modes.split(","):
-            # modes: fast, exact; a "-graph" suffix turns the launch recorder on (GGML_HIP_GRAPH=1)
+            # modes: fast, exact; suffix "-graph": launch recorder with HIP graphs (GGML_HIP_GRAPH=1),
+            # "-thread": launcher thread (GGML_HIP_GRAPH=2)
             gh.check(L.ggml_hip_set_exact(1 if mode.startswith("exact") else 0))
-            gh.check(L.ggml_hip_debug_set_graph(1 if mode.endswith("-graph") else 0))
+            gh.check(L.ggml_hip_debug_set_graph(1 if mode.endswith("-graph") else 2 if mode.endswith("-thread") else 0))
             g0 = np.zeros(5, np.int64)
             L.ggml_hip_debug_graph_stats(g0.ctypes.data, 0)
             L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]

@@ -1550,6 +1550,9 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
     i32x16 S0, S1 = im;
     f32x16 P1 = fz, P0;
     auto compute = [&](int st) __attribute__((always_inline)) {
+#ifdef G7_IGLP
+        __builtin_amdgcn_iglp_opt(G7_IGLP);      // A/B knob (tools/build_variant.sh -DG7_IGLP=0|1)
+#endif
         G6Ops o0 = ld_ops(st, 0);
         G6Ops o1 = ld_ops(st, 1);
         mfma2(o0, S0, P0);

@@ -718,7 +718,7 @@ std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of th
 // q4_0 mul_mat run under a pending silu, sibling q4_0 GEMVs (wq|wk|wv, w1|w3) run as one group,
 // independent rope / rope->cpy / cpy nodes held behind a group run as one launch, the decode
 // soft_max chain with its KQV and merged copy as one launch
-constexpr int N_FUSED = 10;
+constexpr int N_FUSED = 11;
 std::atomic<int64_t> g_fused[N_FUSED];
 
 // fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)
@@ -1003,16 +1003,20 @@ struct Pending {
 };
 Pending g_pend;
 
-// ---- a completed [add ->] rms_norm -> mul chain of one row (decode), held for the q4_0 GEMVs that
-// consume its output: they run it in their x prologue (ghip::gemv_q4_0_multi_norm), one launch less
-// per chain; anything else runs it as its own launch (op_add_rms_norm_mul_f32)
+// ---- a completed chain of one row (decode) that produces the src1 of q4_0 mul_mats, held for them:
+// they run it in their x prologue (ghip::gemv_q4_0_multi_norm), one launch less per chain; anything
+// else runs it as its own launch.  kind 1: [add ->] rms_norm -> mul (op_add_rms_norm_mul_f32; out =
+// the mul), kind 2: silu -> mul (op_silu_mul_f32; a = the silu input, b = the mul's other operand,
+// norm = the silu output)
 struct NormChain {
     bool on = false;
+    int kind = 1;
     int nn = 0;
-    tensor *node[3] = {};          // held copies: add, rms_norm, mul (for the counters)
-    tensor *out_node = nullptr;    // the mul (its output is the GEMVs' src1)
+    tensor *node[3] = {};          // held copies of the chain's nodes (for the counters)
+    tensor *out_node = nullptr;    // the chain's last node (its output is the GEMVs' src1)
     const float *a = nullptr, *b = nullptr, *w = nullptr;
     float *sum = nullptr, *norm = nullptr, *out = nullptr;
+    const uint16_t *table = nullptr;
     int64_t ncols = 0;
 };
 NormChain g_norm;
@@ -1192,6 +1196,30 @@ bool try_fuse(tensor *t) {
     if (p.n == 1 && last->op == gabi::OP_SILU && t->op == gabi::OP_MUL && same_tensor(t->src0, last) && dev_f32(t) &&
         same_shape(t, last) && dev_f32(t->src1) && same_shape(t, t->src1)) {
         const OpTables &tb = op_tables(id, s);
+        // one row (decode): hold it for the q4_0 GEMV that follows (norm_fold)
+        NormChain c;
+        c.kind = 2;
+        c.a = (const float *)dptr(last->src0);
+        c.b = (const float *)dptr(t->src1);
+        c.norm = (float *)dptr(last);
+        c.out = (float *)dptr(t);
+        c.table = tb.silu;
+        c.ncols = t->ne[0];
+        auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+        bool fold = norm_fold_enabled() && !exact_mode() && gabi::nrows(t) == 1 && c.ncols % 64 == 0 &&
+                    c.ncols <= 16384 && al(c.a) && al(c.b) && al(c.norm) && al(c.out);
+        for (const tensor *o : {(const tensor *)last, (const tensor *)t})
+            for (const tensor *i : {(const tensor *)last->src0, (const tensor *)t->src1})
+                if (dev_overlap(o, i)) fold = false;
+        if (fold) {
+            c.node[c.nn++] = last;
+            c.node[c.nn++] = hold(t);
+            c.out_node = c.node[1];
+            c.on = true;
+            g_norm = c;
+            p = Pending{};
+            return true;
+        }
         HIP_FATAL(hipSetDevice(id));
         HIP_FATAL(ghip::op_silu_mul_f32((const float *)dptr(last->src0), (const float *)dptr(t->src1), (float *)dptr(last),
                                         (float *)dptr(t), t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3], tb.silu, s));
@@ -1444,9 +1472,12 @@ int run_elem_prefix(tensor *const *held, int nh) {
 void launch_norm_chain(const NormChain &c) {
     const int id = g_main_device;
     HIP_FATAL(hipSetDevice(id));
-    HIP_FATAL(ghip::op_add_rms_norm_mul_f32(c.a, c.b, c.sum, c.norm, c.w, c.out, c.ncols, 1, g_dev[id].stream));
+    if (c.kind == 2)
+        HIP_FATAL(ghip::op_silu_mul_f32(c.a, c.b, c.norm, c.out, c.ncols, c.table, g_dev[id].stream));
+    else
+        HIP_FATAL(ghip::op_add_rms_norm_mul_f32(c.a, c.b, c.sum, c.norm, c.w, c.out, c.ncols, 1, g_dev[id].stream));
     for (int i = 0; i < c.nn; i++) count_node(c.node[i]);
-    g_fused[0].fetch_add(1, std::memory_order_relaxed);
+    g_fused[c.kind == 2 ? 2 : 0].fetch_add(1, std::memory_order_relaxed);
 }
 void flush_norm() {
     const NormChain c = g_norm;
@@ -1477,14 +1508,14 @@ void flush_group() {
             m[i] = ldy[i] = g.mm[i]->src0->ne[1];
             y[i] = (float *)dptr(g.mm[i]);
         }
-        const ghip::GemvNorm nrm{g.norm.a, g.norm.w, g.norm.sum, g.norm.norm, g.norm.out};
+        const ghip::GemvNorm nrm{g.norm.a, g.norm.w, g.norm.sum, g.norm.norm, g.norm.out, g.norm.kind, g.norm.table};
         HIP_FATAL(hipSetDevice(g_main_device));
         HIP_FATAL(ghip::gemv_q4_0_multi_norm(g.n, w, m, g.norm.ncols, g.norm.b, nrm, y, ldy,
                                              g_dev[g_main_device].info, g_dev[g_main_device].stream));
         for (int i = 0; i < g.norm.nn; i++) count_node(g.norm.node[i]);
         for (int i = 0; i < g.n; i++) count_node(g.mm[i]);
-        g_fused[0].fetch_add(1, std::memory_order_relaxed);
-        g_fused[9].fetch_add(1, std::memory_order_relaxed);
+        g_fused[g.norm.kind == 2 ? 2 : 0].fetch_add(1, std::memory_order_relaxed);
+        g_fused[g.norm.kind == 2 ? 10 : 9].fetch_add(1, std::memory_order_relaxed);
         if (g.n > 1) g_fused[6].fetch_add(1, std::memory_order_relaxed);
         const int done = run_elem_prefix(g.after, g.na);
         for (int i = done; i < g.na; i++) execute_node(g.after[i]);

@@ -41,13 +41,18 @@ constexpr int GEMV_MULTI_MAX = 4;
 hipError_t gemv_q4_0_multi(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *x, int64_t N,
                            float *const *y, const int64_t *ldy, const DeviceInfo &dev, hipStream_t s);
 
-// The same for N = 1 with ggml's [add ->] rms_norm -> mul(norm weight row) chain folded into the x
-// prologue: x = (a ? a + b : b), x *= 1/sqrt(mean(x*x) + 1e-6) (double sum, as ggml_ops.hip's
-// k_row_norm4), x *= w; the GEMVs consume x, and workgroup 0 also stores the chain's tensors (sum =
-// a + b, norm, out; each may be null) bit for bit as the unfused launches.  K <= 16384.
+// The same for N = 1 with the chain that produces x folded into the x prologue (K <= 16384); the
+// GEMVs consume x, and workgroup 0 also stores the chain's tensors (each may be null) bit for bit as
+// the unfused launches:
+//   kind 1, ggml's [add ->] rms_norm -> mul(norm weight row): x = (a ? a + b : b) -> sum,
+//           x *= 1/sqrt(mean(x*x) + 1e-6) (double sum, as ggml_ops.hip's k_row_norm4) -> norm,
+//           x *= w -> out;
+//   kind 2, silu -> mul: u = fp16 table[fp16(a)] (ggml's GGML_SILU_FP16) -> norm, x = u * b -> out.
 struct GemvNorm {
     const float *a, *w;
     float *sum, *norm, *out;
+    int kind = 1;
+    const uint16_t *table = nullptr;     // kind 2: ggml's silu table (65536 fp16 bit patterns)
 };
 hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *b,
                                 const GemvNorm &nrm, float *const *y, const int64_t *ldy, const DeviceInfo &dev,

@@ -358,7 +358,7 @@ __device__ __forceinline__ double wave_sum_d64(double v) {   // every lane gets 
     return v;
 }
 
-template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, bool NORM = false>
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, int PRO = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restrict__ x_, const uint8_t *W0,
                                                           const uint8_t *W1, const uint8_t *W2, int rb1_, int rb2_,
                                                           int rb3_, int rowbytes_, int geom, int M_,
@@ -479,7 +479,57 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
     constexpr bool KO_LDS = DIAG == 9 || DIAG == 10;
     u32x4 xv[GEMV_PRO];
     ItemRegs buf[DEPTH];
-    if constexpr (NORM) {
+    if constexpr (PRO == 2) {
+        // silu -> mul fused into the x prologue (NT == 1, one round of x-waves; see GemvNorm)
+        static_assert(NT == 1 && XSPLIT, "silu prologue: decode x-wave form only");
+        const int XW = (total + 64 * GEMV_XPRO - 1) / (64 * GEMV_XPRO);
+        const int XT = XW * 64;
+        const GemvNorm nrm = tail.nrm;
+        if (wave < XW) {
+            const __amdgpu_buffer_rsrc_t ar = make_rsrc(nrm.a, (uint32_t)total * 16u);
+            u32x4 rb[GEMV_XPRO], ra[GEMV_XPRO];
+#pragma unroll
+            for (int i = 0; i < GEMV_XPRO; i++) {
+                rb[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * XT), 0, 0);
+                ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ar, 16 * (tid + i * XT), 0, 0);
+            }
+            if constexpr (!XHOLD) {
+#pragma unroll
+                for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+            }
+            typedef __attribute__((address_space(1))) const uint16_t g_u16;
+            const bool store = blockIdx.x == 0;
+#pragma unroll
+            for (int i = 0; i < GEMV_XPRO; i++) {
+                const int idx = tid + i * XT;
+                if (idx < total) {
+                    const uint32_t av[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+                    const uint32_t bv[4] = {rb[i].x, rb[i].y, rb[i].z, rb[i].w};
+                    float u[4], o[4];
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {    // as k_silu_mul: s = table[fp16(a)], out = s * b
+                        u[c] = h2f(((g_u16 *)nrm.table)[f2h(__uint_as_float(av[c]))]);
+                        o[c] = u[c] * __uint_as_float(bv[c]);
+                    }
+                    if (store) {
+                        if (nrm.norm) reinterpret_cast<float4 *>(nrm.norm)[idx] = make_float4(u[0], u[1], u[2], u[3]);
+                        if (nrm.out) reinterpret_cast<float4 *>(nrm.out)[idx] = make_float4(o[0], o[1], o[2], o[3]);
+                    }
+                    quantize_into_lds(u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]),
+                                            __float_as_uint(o[3])}, idx);
+                }
+            }
+            if constexpr (XHOLD) {
+#pragma unroll
+                for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
+        }
+        GEMV_STAMP(1);
+        GEMV_STAMP(2);
+    } else if constexpr (PRO == 1) {
         // [add ->] rms_norm -> mul fused into the x prologue (NT == 1, one round of x-waves: the
         // launcher checks K <= 16 * 64 * 4 * GEMV_XPRO).  The x-waves hold the row in registers, sum
         // its squares in double (order-free in practice, as k_row_norm4's), exchange the per-wave
@@ -740,12 +790,12 @@ int gemv_max_tokens(int64_t K) {
 }
 
 
-template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, bool NORM = false>
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, int PRO = 0>
 static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s,
                                 const GemvNorm *nrm = nullptr) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
-    const size_t lds = (size_t)NT * nb * 40 + (NORM ? WAVES * sizeof(double) : 0);
+    const size_t lds = (size_t)NT * nb * 40 + (PRO == 1 ? WAVES * sizeof(double) : 0);
     const int wg_per_cu_env = gemv_policy().wg_per_cu;
     const int64_t M = m.row_begin[m.n];
     const int64_t need = (M + WAVES - 1) / WAVES;
@@ -755,7 +805,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     static int occ = 0;                    // resident workgroups per CU for this instantiation
     if (occ == 0) {
         int nb_occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, NORM>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, PRO>,
                                                          WAVES * 64, lds) != hipSuccess || nb_occ < 1)
             nb_occ = 1;
         occ = nb_occ;
@@ -783,7 +833,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     }
     const int geom = nb | map << 16 | (int)(grid << 18);
     (void)hipGetLastError();  // report only this launch's error
-    launch_k((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, NORM>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
+    launch_k((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, PRO>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
                        m.W[1], m.W[2], m.row_begin[1], m.row_begin[2], m.row_begin[3], (int)rowbytes, geom, (int)M, tail);
     return hipGetLastError();
 }
@@ -894,15 +944,19 @@ hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_
 template <int VAR, int PPL>
 static hipError_t launch_gemv_norm(const GemvMats &m, int64_t K, const float *b, const DeviceInfo &dev, hipStream_t s,
                                    const GemvNorm &nrm, int rd) {
-    return rd == 2 ? launch_gemv_w<1, 0, 16, 2, VAR, PPL, true>(m, K, b, dev, s, &nrm)
-                   : launch_gemv_w<1, 0, 16, 1, VAR, PPL, true>(m, K, b, dev, s, &nrm);
+    if (nrm.kind == 2)
+        return rd == 2 ? launch_gemv_w<1, 0, 16, 2, VAR, PPL, 2>(m, K, b, dev, s, &nrm)
+                       : launch_gemv_w<1, 0, 16, 1, VAR, PPL, 2>(m, K, b, dev, s, &nrm);
+    return rd == 2 ? launch_gemv_w<1, 0, 16, 2, VAR, PPL, 1>(m, K, b, dev, s, &nrm)
+                   : launch_gemv_w<1, 0, 16, 1, VAR, PPL, 1>(m, K, b, dev, s, &nrm);
 }
 
 hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *b,
                                 const GemvNorm &nrm, float *const *y, const int64_t *ldy, const DeviceInfo &dev,
                                 hipStream_t s) {
     // one round of x-waves holds the row: K / 4 float4 <= 16 waves * 64 lanes * GEMV_XPRO
-    if (nmat < 1 || nmat > GEMV_MAXMAT || K % 64 != 0 || K / 4 > 16 * 64 * GEMV_XPRO || !b || !nrm.w)
+    if (nmat < 1 || nmat > GEMV_MAXMAT || K % 64 != 0 || K / 4 > 16 * 64 * GEMV_XPRO || !b ||
+        (nrm.kind == 1 && !nrm.w) || (nrm.kind == 2 && (!nrm.a || !nrm.table)) || (nrm.kind != 1 && nrm.kind != 2))
         return hipErrorInvalidValue;
     GemvMats m{};
     m.n = nmat;

@@ -31,7 +31,7 @@ pytestmark = [pytest.mark.gpu,
 OPS = json.load(open(os.path.join(GOLD, "ggml_op_enum.json")))
 
 
-N_FUSED = 10  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
+N_FUSED = 11  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
 
 
 def op_stats(L, reset=True, fused=False):
@@ -205,9 +205,10 @@ def test_fast_mode_fusion_bitwise_vs_unfused(tmp_path, hp, n_prompt, n_decode):
 
 @pytest.mark.parametrize("hp,n_prompt,n_decode", [(HP128, 40, 60), (G.HP, 8, 40)], ids=["head128", "head64"])
 def test_norm_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode):
-    """The decode [add ->] rms_norm -> mul chain folded into the x prologue of the q4_0 GEMVs that
-    consume it (ghip::gemv_q4_0_multi_norm): the same logits bit for bit as the chain's own launch
-    followed by the GEMV group, and the fold fires for every device norm chain of a decode eval."""
+    """The decode [add ->] rms_norm -> mul and silu -> mul chains folded into the x prologue of the
+    q4_0 GEMVs that consume them (ghip::gemv_q4_0_multi_norm): the same logits bit for bit as the
+    chains' own launches followed by the GEMVs, and the folds fire for every device chain of a decode
+    eval (q|k|v and w1|w3 behind the norms, w2 behind silu -> mul)."""
     L = ggml_hip.load()
     mp = str(tmp_path / "m.ggjt")
     G.write(mp, hp=hp)
@@ -233,8 +234,10 @@ def test_norm_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode):
     assert np.isfinite(out[1][0]).all()
     assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
     assert out[1][1][9] >= (2 * hp["n_layer"] - 1) * n_decode, out[1][1]
-    assert out[0][1][9] == 0, out[0][1]
-    assert out[1][1][0] == out[0][1][0], (out[1][1], out[0][1])     # every chain still counted once
+    assert out[1][1][10] >= hp["n_layer"] * n_decode, out[1][1]      # silu -> mul in the w2 prologue
+    assert out[0][1][9] == 0 and out[0][1][10] == 0, out[0][1]
+    for k in (0, 2):                                                 # every chain still counted once
+        assert out[1][1][k] == out[0][1][k], (out[1][1], out[0][1])
 
 
 @pytest.mark.parametrize("mode", [1, 2], ids=["graphs", "thread"])

@@ -178,11 +178,13 @@ void pool_free(int id, void *p, size_t size) {
     d.pool.push_back({p, size});
 }
 
-// workspace for the q8_0 activations of one mul_mat: qs [N][K] int8 + d [N][K/32] f32
-size_t workspace_bytes(int64_t K, int64_t N) {
+// workspace for the q8_0 activations of one mul_mat: qs [N][K] int8 + d [N][K/32] f32 + the same d as
+// fp16, block-major [K/32][N rounded up to 4] (the LDS GEMM's operand layout)
+size_t ws_d16_offset(int64_t K, int64_t N) {
     const size_t qs = (size_t)(N * K + 255) & ~(size_t)255;
-    return qs + (size_t)N * (K / QK) * 4;
+    return qs + (((size_t)N * (K / QK) * 4 + 255) & ~(size_t)255);
 }
+size_t workspace_bytes(int64_t K, int64_t N) { return ws_d16_offset(K, N) + (size_t)((N + 3) & ~3) * (K / QK) * 2; }
 
 int reserve_workspace(int id, size_t bytes, hipStream_t s = nullptr) {
     Device &d = g_dev[id];
@@ -447,13 +449,14 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
     if (wrc != GGML_HIP_OK) return wrc;
     int8_t *qs = (int8_t *)ws;
     float *xd = (float *)((char *)ws + ((size_t)(N * K + 255) & ~(size_t)255));
-    if (!x_quantized) HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s));
+    uint16_t *xd16 = (uint16_t *)((char *)ws + ws_d16_offset(K, N));
+    if (!x_quantized) HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s, algo == 2 ? xd16 : nullptr));
     if (algo == 4)
         HIP_RET(ghip::mm_exact_q4_0(w, K, M, qs, xd, N, y, ldy, s));
     else if (algo == 3)
         HIP_RET(ghip::gemm_sk_q4_0(w, K, M, qs, xd, N, y, ldy, g_dev[id].info.num_cus, s));
     else
-        HIP_RET(ghip::gemm_q4_0(w, K, M, qs, xd, N, y, ldy, s));
+        HIP_RET(ghip::gemm_q4_0(w, K, M, qs, xd, N, y, ldy, s, xd16));
     return GGML_HIP_OK;
 }
 

@@ -24,7 +24,8 @@ struct DeviceInfo {
 // A5 (AVX2 branch semantics, bit-exact): x f32 [N][K] -> block_q8_0 AoS [N][K/32].
 hipError_t quantize_q8_0_aos(const float *x, int64_t K, int64_t N, void *xq8, hipStream_t s);
 // Same quantizer, GEMM operand layout.
-hipError_t quantize_q8_0_soa(const float *x, int64_t K, int64_t N, int8_t *qs, float *d, hipStream_t s);
+hipError_t quantize_q8_0_soa(const float *x, int64_t K, int64_t N, int8_t *qs, float *d, hipStream_t s,
+                             uint16_t *d16 = nullptr);   // d16: optional fp16 copy of d, block-major [K/32][N]
 // A3 (quantize_row_q4_0_reference semantics, bit-exact): w f32 [M][K] -> block_q4_0 rows.
 hipError_t quantize_q4_0(const float *w, int64_t K, int64_t M, void *wq, hipStream_t s);
 // A4: block_q4_0 rows -> f32 [M][K].
@@ -68,8 +69,10 @@ hipError_t gemm_read_stamps(unsigned long long *host, int n);
 
 // Prefill path: int8 MFMA (v_mfma_i32_32x32x32_i8, K=32 = one q4_0 block) GEMM on the
 // pre-quantized activations xs (quantize_q8_0_soa).
+// xd16: the same d_x as fp16 bits, block-major [K/32][N] (quantize_q8_0_soa's d16 copy; the default
+// LDS GEMM DMAs it straight into its operand layout)
 hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd,
-                     int64_t N, float *y, int64_t ldy, hipStream_t s);
+                     int64_t N, float *y, int64_t ldy, hipStream_t s, const uint16_t *xd16);
 
 // Small / medium N (split-K over the waves of a 32x32-tile workgroup, operands straight to registers).
 hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,

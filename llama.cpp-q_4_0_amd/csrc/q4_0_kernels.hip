@@ -123,7 +123,8 @@ __device__ __forceinline__ uint32_t q8_block_lane(float4 v, uint32_t &d16, int &
 template <bool AOS>
 __global__ __launch_bounds__(256) void k_quantize_q8_0(const float *__restrict__ x, int64_t K, int64_t total8,
                                                          uint8_t *__restrict__ aos, int8_t *__restrict__ qs,
-                                                         float *__restrict__ dout) {
+                                                         float *__restrict__ dout, uint16_t *__restrict__ d16out,
+                                                         int64_t N) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= total8) return;                           // total8 % 8 == 0: whole groups exit together
     const int64_t blk = t >> 3;                        // global block index = n*nb + b
@@ -140,7 +141,13 @@ __global__ __launch_bounds__(256) void k_quantize_q8_0(const float *__restrict__
         if (sub == 0) *reinterpret_cast<uint16_t *>(o) = (uint16_t)d16;
     } else {
         reinterpret_cast<uint32_t *>(qs)[t] = packed;  // qs[n][32b + 4sub]
-        if (sub == 0) dout[blk] = h2f(d16);
+        if (sub == 0) {
+            dout[blk] = h2f(d16);
+            if (d16out) {                              // block-major fp16 copy [nb][Np] (the LDS GEMM)
+                const int64_t nb = K / QK, Np = (N + 3) & ~(int64_t)3;   // 8-byte aligned block rows
+                d16out[(blk % nb) * Np + blk / nb] = (uint16_t)d16;
+            }
+        }
     }
 }
 
@@ -150,17 +157,18 @@ hipError_t quantize_q8_0_aos(const float *x, int64_t K, int64_t N, void *xq8, hi
     const int64_t grid = (total8 + 255) / 256;
     (void)hipGetLastError();  // report only this launch's error
     launch_k(k_quantize_q8_0<true>, dim3((unsigned)grid), dim3(256), 0, s, x, K, total8,
-                       (uint8_t *)xq8, (int8_t *)nullptr, (float *)nullptr);
+                       (uint8_t *)xq8, (int8_t *)nullptr, (float *)nullptr, (uint16_t *)nullptr, N);
     return hipGetLastError();
 }
 
-hipError_t quantize_q8_0_soa(const float *x, int64_t K, int64_t N, int8_t *qs, float *d, hipStream_t s) {
+hipError_t quantize_q8_0_soa(const float *x, int64_t K, int64_t N, int8_t *qs, float *d, hipStream_t s,
+                             uint16_t *d16) {
     const int64_t total8 = N * (K / QK) * 8;
     if (total8 == 0) return hipSuccess;
     const int64_t grid = (total8 + 255) / 256;
     (void)hipGetLastError();  // report only this launch's error
     launch_k(k_quantize_q8_0<false>, dim3((unsigned)grid), dim3(256), 0, s, x, K, total8,
-                       (uint8_t *)nullptr, qs, d);
+                       (uint8_t *)nullptr, qs, d, d16, N);
     return hipGetLastError();
 }
 
@@ -1483,13 +1491,15 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm6_q4_0(const uint8_t *__r
 // choosing each lane's SOURCE address.
 static constexpr int G7_NX = 4;                                  // activation ring depth (stages)
 static constexpr int G7_X = GM_KB * GM_BN * 32;                  // int8 acts   [KB][BN][32]  16 KB
-static constexpr int G7_XD = GM_KB * GM_BN * 4;                  // f32 d_x     [KB][BN]       2 KB
+static constexpr int G7_XD = GM_KB * GM_BN * 2;                  // fp16 d_x    [KB][BN]       1 KB
 static constexpr int G7_W = GM_KB * GM_BM * 32;                  // int8 weights [KB][BM][32]  8 KB
 static constexpr int G7_WD = GM_KB * GM_BM * 2;                  // fp16 d_w    [KB][BM]
-static constexpr int G7_LDS = G7_NX * (G7_X + G7_XD) + 2 * (G7_W + G7_WD);   // 89 KB
+static constexpr int G7_WDZ = 2 * G7_WD;                         // zeros: the upper half-wave's d_w
+static constexpr int G7_DUMMY = 256;                              // target of the zero-size d_x DMAs
+static constexpr int G7_LDS = G7_NX * (G7_X + G7_XD) + 2 * (G7_W + G7_WD) + G7_WDZ + G7_DUMMY;   // 86 KB
 static constexpr int G7_OPS = 3 + 2 + 1;                        // per thread per stage: W pair, 2 x glds, d_x glds
 static_assert(G7_X / 1024 == 2 * GM_WAVES, "two 1-KiB activation DMA instructions per wave per stage");
-static_assert(G7_XD / 256 == GM_WAVES, "one 256-B d_x DMA instruction per wave per stage");
+static_assert(G7_XD / 256 == GM_WAVES / 2, "one 256-B d_x DMA instruction per wave of the first half per stage");
 
 struct G7W {
     u32x4 wa, wb;
@@ -1498,13 +1508,15 @@ struct G7W {
 
 __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes, int nb,
                                                                int M, const int8_t *__restrict__ xqs,
-                                                               const float *__restrict__ xd, int N, int K,
+                                                               const uint16_t *__restrict__ xd16, int N, int K,
                                                                float *__restrict__ y, int64_t ldy) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *xring = smem;                                          // [NX][X]
-    float *xdring = reinterpret_cast<float *>(smem + G7_NX * G7_X);    // [NX][KB][BN]
+    uint16_t *xdring = reinterpret_cast<uint16_t *>(smem + G7_NX * G7_X);   // [NX][KB][BN] fp16
     uint8_t *wbuf = smem + G7_NX * (G7_X + G7_XD);                  // [2][W]
     uint16_t *wdbuf = reinterpret_cast<uint16_t *>(wbuf + 2 * G7_W);   // [2][KB][BM]
+    uint16_t *wdzero = wdbuf + G7_WD;                               // [2][KB][BM] zeros
+    uint8_t *dummy = reinterpret_cast<uint8_t *>(wdzero) + G7_WDZ;   // waves 4..7's d_x DMA lands here
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1515,9 +1527,13 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
 
     const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W + (int64_t)m0 * rowbytes, (uint32_t)((int64_t)(M - m0) * rowbytes));
     const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)(N - n0) * K));
-    const __amdgpu_buffer_rsrc_t drs = make_rsrc(xd + (int64_t)n0 * nb, (uint32_t)((int64_t)(N - n0) * nb * 4));
+    // fp16 d_x, block-major [nb][Np] (quantize_q8_0_soa's copy, Np = N rounded up to 4 so that every
+    // block row is dword aligned for the DMA): a block's 128 tokens are 256 bytes
+    const int Np = (N + 3) & ~3;
+    const __amdgpu_buffer_rsrc_t drs = make_rsrc(xd16, (uint32_t)((int64_t)nb * Np * 2));
     const __amdgpu_buffer_rsrc_t nul = make_rsrc(W, 0);
     const int sr = tid >> 3, sb = (tid >> 1) & 3, sh = tid & 1;     // weight staging role (as v6)
+    if (tid < G7_WDZ / 4) reinterpret_cast<uint32_t *>(wdzero)[tid] = 0u;   // ordered by the first barrier
 
     // activation DMA: this wave's instructions j = 2*wave, 2*wave+1 of the stage; instruction j fills
     // LDS bytes [j KiB, (j+1) KiB) = block j/4, tokens 32*(j%4) .. +31; lane i lands at slot i =
@@ -1530,8 +1546,9 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
         const int hh = (lane & 1) ^ ((t >> 3) & 1);
         xsrc[q] = t * K + (j >> 2) * QK + 16 * hh;                  // + kb0*32 per stage
     }
-    // d_x DMA: wave w fills [block w/2][tokens 64*(w&1) .. +63] (f32)
-    const int dsrc = ((64 * (wave & 1) + lane) * nb + (wave >> 1)) * 4;   // + kb0*4 per stage
+    // d_x DMA: wave w < 4 fills [block w][tokens 0 .. 127] (fp16, 2 per lane); waves 4..7 issue the
+    // same instruction through the zero-size descriptor, so every wave counts 6 VM operations a stage
+    const int dsrc = (wave & 3) * Np * 2 + n0 * 2 + lane * 4;       // + kb0*Np*2 per stage
 
     auto issue = [&](int st, G7W &g) __attribute__((always_inline)) {
         const int kb0 = st * GM_KB;
@@ -1543,13 +1560,14 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
         g.wc = __builtin_amdgcn_raw_buffer_load_b32(wr_, woff + 32, 0, 0);
         const int slot = st & (G7_NX - 1);
         const __amdgpu_buffer_rsrc_t xr_ = valid ? xrs : nul;
-        const __amdgpu_buffer_rsrc_t dr_ = valid ? drs : nul;
+        const __amdgpu_buffer_rsrc_t dr_ = (valid && wave < 4) ? drs : nul;
 #pragma unroll
         for (int q = 0; q < 2; q++)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xr_, (lds_void_t *)(xring + slot * G7_X + (2 * wave + q) * 1024), 16,
                                                      xsrc[q] + kb0 * QK, 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(dr_, (lds_void_t *)(xdring + slot * (G7_XD / 4) + wave * 64), 4,
-                                                 dsrc + kb0 * 4, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            dr_, (lds_void_t *)(wave < 4 ? (uint8_t *)(xdring + slot * (G7_XD / 2) + wave * GM_BN) : dummy), 4,
+            dsrc + kb0 * Np * 2, 0, 0, 0);
     };
     auto write_w = [&](int st, const G7W &g) __attribute__((always_inline)) {
         const int kb0 = st * GM_KB;
@@ -1572,16 +1590,20 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
 
     const int tok = 32 * wt + c;
     const int wrow = 32 * wr + c;
+    // scale MFMA operands: every lane holds d_x at element 0 (k = 0 for h = 0, k = 8 for h = 1), the
+    // weights' d_w only for h = 0 (h = 1 reads the zero region): P = d_x * d_w + d_x * 0, exact, with
+    // no per-block select or conversion
+    const uint16_t *wdb = h ? wdzero : wdbuf;
     auto ld_ops = [&](int st, int b) __attribute__((always_inline)) {
         const uint8_t *xs = xring + (st & (G7_NX - 1)) * G7_X;
-        const float *xds = xdring + (st & (G7_NX - 1)) * (G7_XD / 4);
+        const uint16_t *xds = xdring + (st & (G7_NX - 1)) * (G7_XD / 2);
         const uint8_t *ws = wbuf + (st & 1) * G7_W;
-        const uint16_t *wds = wdbuf + (st & 1) * (G7_WD / 2);
+        const uint16_t *wds = wdb + (st & 1) * (G7_WD / 2);
         G6Ops o;
         o.a = *reinterpret_cast<const i32x4 *>(xs + b * GM_BN * 32 + gm_half_off(tok, h));
         o.b = *reinterpret_cast<const i32x4 *>(ws + b * GM_BM * 32 + gm_half_off(wrow, h));
-        o.sx = f2h(xds[b * GM_BN + tok]);                          // exact: d_x is an fp16 value
-        o.sw = wds[b * GM_BM + wrow];
+        o.sx = xds[b * GM_BN + tok];
+        o.sw = wds[b * GM_BM + wrow];            // the upper half-wave reads zeros (see mfma2)
         return o;
     };
     const int mg = 0x4B400000;
@@ -1589,8 +1611,8 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
     const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     auto mfma2 = [&](const G6Ops &o, i32x16 &S, f32x16 &P) __attribute__((always_inline)) {
         S = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a, o.b, im, 0, 0, 0);
-        const u32x4 as = {h == 0 ? o.sx : 0u, 0u, 0u, 0u};
-        const u32x4 bs = {h == 0 ? o.sw : 0u, 0u, 0u, 0u};
+        const u32x4 as = {o.sx, 0u, 0u, 0u};
+        const u32x4 bs = {o.sw, 0u, 0u, 0u};
         P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs), fz,
                                                    0, 0, 0);
     };
@@ -1804,7 +1826,7 @@ hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, 
 }
 
 hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
-                     float *y, int64_t ldy, hipStream_t s) {
+                     float *y, int64_t ldy, hipStream_t s, const uint16_t *xd16) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     dim3 grid((unsigned)((M + GM_BM - 1) / GM_BM), (unsigned)((N + GM_BN - 1) / GM_BN));
@@ -1821,8 +1843,9 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
             attr7 = true;
         }
         (void)hipGetLastError();  // report only this launch's error
+        if (!xd16) return hipErrorInvalidValue;
         launch_k(k_gemm7_q4_0, grid, dim3(GM_THREADS), G7_LDS, s, (const uint8_t *)W, rowbytes, nb, (int)M,
-                           xqs, xd, (int)N, (int)K, y, ldy);
+                           xqs, xd16, (int)N, (int)K, y, ldy);
         return hipGetLastError();
     }
     if (ver == 6) {

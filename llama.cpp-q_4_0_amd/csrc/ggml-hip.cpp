@@ -2148,6 +2148,23 @@ int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *
         total += M[i];
     }
     if (N == 0) return GGML_HIP_OK;
+    if (exact_mode() && n > 1 && N >= 1 && dev_x && K > 0 && K % 64 == 0 && aligned(dev_x, 16) && total < (1 << 30)) {
+        // exact mode: x quantized once, every sibling in ONE exact launch (bitwise the same as one
+        // launch per matrix: each output row's chain does not depend on the grid)
+        for (int i = 0; i < n; i++)
+            if (M[i] * (K / QK) * Q4B >= ((int64_t)1 << 31)) return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large");
+        const int id = current_device();
+        void *ws = nullptr;
+        const int wrc = stream_workspace(id, s, workspace_bytes(K, N), &ws);
+        if (wrc != GGML_HIP_OK) return wrc;
+        int8_t *qs = (int8_t *)ws;
+        float *xd = (float *)((char *)ws + ((size_t)(N * K + 255) & ~(size_t)255));
+        HIP_RET(ghip::quantize_q8_0_soa(dev_x, K, N, qs, xd, s));
+        int64_t ldy[ghip::GEMV_MULTI_MAX];
+        for (int i = 0; i < n; i++) ldy[i] = M[i];
+        HIP_RET(ghip::mm_exact_q4_0_multi(n, dev_w, M, K, qs, xd, N, dev_y, ldy, s));
+        return GGML_HIP_OK;
+    }
     if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30) || exact_mode()) {
         for (int i = 0; i < n; i++) {       // GEMM / exact path: x quantized once, one launch per matrix
             int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 0, s, i > 0);

@@ -82,6 +82,9 @@ hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, 
 // per-lane sequential fma chains in block order; any N.
 hipError_t mm_exact_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
                          float *y, int64_t ldy, hipStream_t s);
+// the same for up to 4 matrices of the same K sharing x, one launch (sibling groups in exact mode)
+hipError_t mm_exact_q4_0_multi(int n, const void *const *W, const int64_t *M, int64_t K, const int8_t *xqs,
+                               const float *xd, int64_t N, float *const *y, const int64_t *ldy, hipStream_t s);
 
 // Multi-GPU helper: y[n*ldy + row0[r] + i] = slab[r][n][i] for i < rows[r] (gather compaction).
 // row_begin travels as a kernel argument (no host->device copy, capture-safe)

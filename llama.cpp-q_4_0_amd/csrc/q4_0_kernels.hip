@@ -1930,17 +1930,42 @@ struct ExLayout {
     static_assert(OPS <= 63, "vmcnt immediate");
 };
 
+// Up to 4 matrices of the same K sharing x (siblings: wq|wk|wv, w1|w3) in one launch: workgroup
+// rows [wg_begin[i], wg_begin[i+1]) of grid.x belong to matrix i (16 rows each, never straddling
+// two matrices); the per-workgroup choice is written as sums of selected deltas (constant indices
+// only: a dynamic index into the by-value struct becomes a scratch table)
+struct ExMats {
+    const uint8_t *W[4];
+    float *y[4];
+    int64_t ldy[4];
+    int M[4];
+    int wg_begin[5];
+};
+
 template <int NC>
-__global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const uint8_t *__restrict__ W, int64_t rowbytes,
-                                                               int nb, int M, const int8_t *__restrict__ xqs,
-                                                               const float *__restrict__ xd, int N, int K,
-                                                               float *__restrict__ y, int64_t ldy) {
+__global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const ExMats mats, int64_t rowbytes,
+                                                               int nb, const int8_t *__restrict__ xqs,
+                                                               const float *__restrict__ xd, int N, int K) {
     using Lay = ExLayout<NC>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int t = threadIdx.x, l64 = t & 63, lane = t & 7, r = t >> 3;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int q = lane & 3, shift = lane & 4;               // qs word q; low (j < 4) / high nibbles
-    const int m0 = blockIdx.x * EX_RB, n0 = blockIdx.y * NC;
+    const int bx = blockIdx.x;
+    const bool g1 = bx >= mats.wg_begin[1], g2 = bx >= mats.wg_begin[2], g3 = bx >= mats.wg_begin[3];
+    const uint8_t *W = reinterpret_cast<const uint8_t *>(
+        (uint64_t)mats.W[0] + (g1 ? (uint64_t)mats.W[1] - (uint64_t)mats.W[0] : 0) +
+        (g2 ? (uint64_t)mats.W[2] - (uint64_t)mats.W[1] : 0) + (g3 ? (uint64_t)mats.W[3] - (uint64_t)mats.W[2] : 0));
+    float *y = reinterpret_cast<float *>(
+        (uint64_t)mats.y[0] + (g1 ? (uint64_t)mats.y[1] - (uint64_t)mats.y[0] : 0) +
+        (g2 ? (uint64_t)mats.y[2] - (uint64_t)mats.y[1] : 0) + (g3 ? (uint64_t)mats.y[3] - (uint64_t)mats.y[2] : 0));
+    const int64_t ldy = mats.ldy[0] + (g1 ? mats.ldy[1] - mats.ldy[0] : 0) + (g2 ? mats.ldy[2] - mats.ldy[1] : 0) +
+                        (g3 ? mats.ldy[3] - mats.ldy[2] : 0);
+    const int M = mats.M[0] + (g1 ? mats.M[1] - mats.M[0] : 0) + (g2 ? mats.M[2] - mats.M[1] : 0) +
+                  (g3 ? mats.M[3] - mats.M[2] : 0);
+    const int wb = (g1 ? mats.wg_begin[1] : 0) + (g2 ? mats.wg_begin[2] - mats.wg_begin[1] : 0) +
+                   (g3 ? mats.wg_begin[3] - mats.wg_begin[2] : 0);
+    const int m0 = (bx - wb) * EX_RB, n0 = blockIdx.y * NC;
     const int rows = min(EX_RB, M - m0), cols = min(NC, N - n0);
     const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W + (int64_t)m0 * rowbytes, (uint32_t)((int64_t)rows * rowbytes));
     const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)cols * K));
@@ -2084,8 +2109,8 @@ __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const uint8_t *__r
 }
 
 template <int NC>
-static hipError_t launch_exact(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
-                               float *y, int64_t ldy, hipStream_t s) {
+static hipError_t launch_exact(const ExMats &m, int n, int64_t K, const int8_t *xqs, const float *xd, int64_t N,
+                               hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     const int lds = EX_S * ExLayout<NC>::SLOT;
@@ -2096,22 +2121,37 @@ static hipError_t launch_exact(const void *W, int64_t K, int64_t M, const int8_t
         if (e != hipSuccess) return e;
         attr = true;
     }
-    dim3 grid((unsigned)((M + EX_RB - 1) / EX_RB), (unsigned)((N + NC - 1) / NC));
+    dim3 grid((unsigned)m.wg_begin[n], (unsigned)((N + NC - 1) / NC));
     (void)hipGetLastError();  // report only this launch's error
-    launch_k(k_mm_exact_q4_0<NC>, grid, dim3(EX_THREADS), lds, s, (const uint8_t *)W, rowbytes, nb, (int)M,
-                       xqs, xd, (int)N, (int)K, y, ldy);
+    launch_k(k_mm_exact_q4_0<NC>, grid, dim3(EX_THREADS), lds, s, m, rowbytes, nb, xqs, xd, (int)N, (int)K);
     return hipGetLastError();
+}
+
+hipError_t mm_exact_q4_0_multi(int n, const void *const *W, const int64_t *M, int64_t K, const int8_t *xqs,
+                               const float *xd, int64_t N, float *const *y, const int64_t *ldy, hipStream_t s) {
+    if (n < 1 || n > 4) return hipErrorInvalidValue;
+    ExMats m{};
+    m.wg_begin[0] = 0;
+    for (int i = 0; i < 4; i++) {
+        const int j = i < n ? i : n - 1;                    // unused slots repeat the last matrix
+        m.W[i] = (const uint8_t *)W[j];
+        m.y[i] = y[j];
+        m.ldy[i] = ldy[j];
+        m.M[i] = (int)M[j];
+        m.wg_begin[i + 1] = m.wg_begin[i] + (i < n ? (int)((M[i] + EX_RB - 1) / EX_RB) : 0);
+    }
+    static const int nc_env = env_int("GGML_HIP_EXACT_NC", 0);   // tuning: columns per workgroup
+    // measured (tools/exact_nc.sh, 4096 x 4096): 8 columns best at N = 8, 2 at N = 40 and 512
+    const int nc = nc_env ? nc_env : N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : 2;
+    if (nc == 1) return launch_exact<1>(m, n, K, xqs, xd, N, s);
+    if (nc == 2) return launch_exact<2>(m, n, K, xqs, xd, N, s);
+    if (nc == 4) return launch_exact<4>(m, n, K, xqs, xd, N, s);
+    return launch_exact<8>(m, n, K, xqs, xd, N, s);
 }
 
 hipError_t mm_exact_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
                          float *y, int64_t ldy, hipStream_t s) {
-    static const int nc_env = env_int("GGML_HIP_EXACT_NC", 0);   // tuning: columns per workgroup
-    // measured (tools/exact_nc.sh, 4096 x 4096): 8 columns best at N = 8, 2 at N = 40 and 512
-    const int nc = nc_env ? nc_env : N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : 2;
-    if (nc == 1) return launch_exact<1>(W, K, M, xqs, xd, N, y, ldy, s);
-    if (nc == 2) return launch_exact<2>(W, K, M, xqs, xd, N, y, ldy, s);
-    if (nc == 4) return launch_exact<4>(W, K, M, xqs, xd, N, y, ldy, s);
-    return launch_exact<8>(W, K, M, xqs, xd, N, y, ldy, s);
+    return mm_exact_q4_0_multi(1, &W, &M, K, xqs, xd, N, &y, &ldy, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -111,3 +111,20 @@ def test_exact_switch_routes_auto_multi_and_tensor_paths(exact_off):
     assert L.ggml_hip_compute_forward(ctypes.byref(p), ctypes.byref(yt))
     assert_bitwise(y2, O.mul_mat(wq, K, x2))
     ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+
+
+@pytest.mark.parametrize("N", [1, 8, 40])
+def test_exact_sibling_group_one_launch_bitwise(exact_off, N):
+    """Exact mode runs a sibling group (ggml_hip_mul_mat_q4_0_multi) as ONE exact launch over the
+    concatenated 16-row workgroups of up to four matrices: every y still bit-identical to the
+    oracle's AVX2 schedule, ragged M (a matrix that ends mid-workgroup) included."""
+    L = exact_off
+    K, Ms = 1024, [512, 48, 300, 16]
+    cases = [make_case(K, M, N, seed=90 + i) for i, M in enumerate(Ms)]
+    x = cases[0][1]
+    assert L.ggml_hip_set_exact(1) == 0
+    wds, xd = [DB.from_array(c[0]) for c in cases], DB.from_array(x)
+    ys = [DB(N * M * 4) for M in Ms]
+    ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
+    for (wq, _), yd, M in zip(cases, ys, Ms):
+        assert_bitwise(yd.download((N, M), np.float32), O.mul_mat(wq, K, x))

@@ -1553,7 +1553,11 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
     auto issue = [&](int st, G7W &g) __attribute__((always_inline)) {
         const int kb0 = st * GM_KB;
         const bool valid = kb0 < nb;                                // past the end: no traffic
+#ifdef G7_NOWSTAGE
+        const __amdgpu_buffer_rsrc_t wr_ = nul;        // timing diagnostic: weights cost nothing
+#else
         const __amdgpu_buffer_rsrc_t wr_ = valid ? wrs : nul;
+#endif
         const int woff = (int)(sr * rowbytes) + (kb0 + (sb & ~1)) * Q4B;
         g.wa = __builtin_amdgcn_raw_buffer_load_b128(wr_, woff, 0, 0);
         g.wb = __builtin_amdgcn_raw_buffer_load_b128(wr_, woff + 16, 0, 0);
@@ -1570,6 +1574,9 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
             dsrc + kb0 * Np * 2, 0, 0, 0);
     };
     auto write_w = [&](int st, const G7W &g) __attribute__((always_inline)) {
+#ifdef G7_NOWSTAGE
+        return;
+#endif
         const int kb0 = st * GM_KB;
         uint8_t *ws = wbuf + (st & 1) * G7_W;
         uint16_t *wds = wdbuf + (st & 1) * (G7_WD / 2);

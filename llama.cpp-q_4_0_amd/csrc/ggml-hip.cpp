@@ -2925,6 +2925,13 @@ int ggml_hip_debug_set_gemv_policy(int map, int depth, int rowitems, int wg_per_
     return GGML_HIP_OK;
 }
 
+// not in the public header: the chunk-balanced decode GEMV (BAL) for K > 12288: -1 auto, 0 off, 1 on
+int ggml_hip_debug_set_gemv_bal(int bal) {
+    if (bal < -1 || bal > 1) return fail(GGML_HIP_ERR_INVALID, "bad GEMV balance mode");
+    ghip::gemv_set_bal(bal);
+    return GGML_HIP_OK;
+}
+
 // not in the public header: the smallest host Q4_0 weight (elements) taken at N < 32 through the
 // residency cache (-1 = GGML_HIP_DECODE_MIN_WEIGHTS or 2^19); returns the previous value
 int64_t ggml_hip_debug_set_decode_min_weights(int64_t n) {

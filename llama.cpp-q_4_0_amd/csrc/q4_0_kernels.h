@@ -62,6 +62,7 @@ hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M
 // test hook: force the GEMV launch policy (row mapping 0/1/2, ring depth 1/2, row items 0/1,
 // workgroups per CU); -1 / 0 = automatic
 void gemv_set_policy(int map, int depth, int rowitems, int wg_per_cu);
+void gemv_set_bal(int bal);   // -1 auto, 0 off, 1 every chunked decode launch (K > 12288)
 
 // diagnostic: copy the per-wave phase stamps of the last GGML_HIP_GEMV_DIAG=7 launch
 hipError_t gemv_read_stamps(unsigned long long *host, int n);

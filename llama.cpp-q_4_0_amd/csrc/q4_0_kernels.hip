@@ -360,13 +360,22 @@ struct GemvTail {
 //                     row (PPL = ceil(pairs/64)), so one item is a whole row: all of its loads are
 //                     in flight together and it is reduced once (a row of K=4160 no longer costs two
 //                     items for one extra pair).  PPL == 0: 64-pair chunks, one item per chunk.
+// BAL (PPL == 0, NT == 1, PRO == 0; long rows, K > 12288): the row-granular mappings leave a tail
+//                     when M is a little above the wave count (Falcon-7B's 18176 -> 4544: 4544 rows on
+//                     4096 waves, so 448 waves stream two whole rows while the rest stream one).  BAL
+//                     balances at chunk granularity instead: workgroup b owns the blocked row range,
+//                     its (row, chunk) items go round-robin to its waves (item i -> wave i % WAVES),
+//                     every item is reduced across its lanes on its own and its sum parked in LDS, and
+//                     after one workgroup barrier thread t adds row t's chunk sums in chunk order.
+//                     Deterministic (no atomics, fixed order), but a different fp32 summation order
+//                     from the row-granular policies (within the same oracle bound, not bitwise).
 __device__ __forceinline__ double wave_sum_d64(double v) {   // every lane gets the sum
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, int PRO = 0>
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, int PRO = 0, int BAL = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restrict__ x_, const uint8_t *W0,
                                                           const uint8_t *W1, const uint8_t *W2, int rb1_, int rb2_,
                                                           int rb3_, int rowbytes_, int geom, int M_,
@@ -421,8 +430,12 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
         rend = M;
         rstride = grid * WAVES;
     }
+    static_assert(!BAL || (PPL == 0 && NT == 1 && PRO == 0), "balanced items: decode chunk form only");
+    const int rbeg = row0 - wave;                                   // BAL: the workgroup's blocked range
+    const int nwg_items = BAL ? (rend - rbeg) * nchunk : 0;         // BAL: (row, chunk) items of the WG
     const int nrows_w = row0 < rend ? (int)((uint32_t)(rend - 1 - row0) / (uint32_t)rstride) + 1 : 0;
-    const int nitems = nrows_w * nchunk;                            // (row, chunk) items of this wave
+    const int nitems = BAL ? (wave < nwg_items ? (nwg_items - 1 - wave) / WAVES + 1 : 0)
+                           : nrows_w * nchunk;                      // (row, chunk) items of this wave
     GEMV_STAMP(0);
 
     static_assert(GEMV_MAXMAT == 4, "matrix selection below is written for 4 siblings");
@@ -463,7 +476,12 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             }
         }
     };
-    auto item_row = [&](int it) __attribute__((always_inline)) { return row0 + (it / nchunk) * rstride; };
+    auto item_row = [&](int it) __attribute__((always_inline)) {
+        return BAL ? rbeg + (wave + WAVES * it) / nchunk : row0 + (it / nchunk) * rstride;
+    };
+    auto item_chunk = [&](int it) __attribute__((always_inline)) {
+        return BAL ? (wave + WAVES * it) % nchunk : it % nchunk;
+    };
     constexpr bool GLB = (VAR & 1) != 0, XSPLIT = (VAR & 2) != 0, XFIRST = (VAR & 4) != 0, XHOLD = (VAR & 8) != 0;
     static_assert(PPL == 0 || GLB, "row items use the global-load form");
     auto issue = [&](int it) __attribute__((always_inline)) {
@@ -474,12 +492,12 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             const uint8_t *rp = row_ptr(valid ? r : 0);
 #pragma unroll
             for (int j = 0; j < NPR; j++) {
-                const int pp = 64 * (PPL > 0 ? j : it % nchunk) + lane;
+                const int pp = 64 * (PPL > 0 ? j : item_chunk(it)) + lane;
                 const int pc = valid ? (pp < npairs ? pp : npairs - 1) : 0;
                 v.pr[j] = load_pair_g(rp + 36 * pc);
             }
         } else {
-            v.pr[0] = load_pair(row_ptr(valid ? r : 0), valid ? rowbytes : 0, 64 * (it % nchunk) + lane);
+            v.pr[0] = load_pair(row_ptr(valid ? r : 0), valid ? rowbytes : 0, 64 * item_chunk(it) + lane);
         }
         return v;
     };
@@ -706,8 +724,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
     float acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; n++) acc[n] = 0.0f;
+    float *const part = reinterpret_cast<float *>(xs + NT * nb);   // BAL: [rows of the WG][nchunk]
     auto process = [&](const ItemRegs &vi, int it) __attribute__((always_inline)) {
-        const int chunk = it % nchunk;
+        const int chunk = item_chunk(it);
 #pragma unroll
         for (int j = 0; j < NPR; j++) {
         const PairRegs &v = vi.pr[j];
@@ -734,7 +753,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             }
         }
         }
-        if (chunk == nchunk - 1) {                                  // row complete: reduce + store
+        if constexpr (BAL) {                                        // this item's sum -> LDS
+            const float t = wave_sum_lane63(acc[0]);
+            if (lane == 63) part[wave + WAVES * it] = t;
+            acc[0] = 0.0f;
+        } else if (chunk == nchunk - 1) {                           // row complete: reduce + store
             const int r = item_row(it);
             const bool g1 = r >= rb1, g2 = r >= rb2, g3 = r >= rb3;
             const int rb = (g1 ? rb1 : 0) + (g2 ? rb2 - rb1 : 0) + (g3 ? rb3 - rb2 : 0);
@@ -767,6 +790,19 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             buf[d] = issue(it + d + DEPTH);
         }
     }
+    if constexpr (BAL) {                                            // rows' chunk sums, in chunk order
+        __syncthreads();
+        typedef __attribute__((address_space(1))) float gfloat;
+        for (int rr = tid; rr < rend - rbeg; rr += WAVES * 64) {
+            float out = 0.0f;
+            for (int c = 0; c < nchunk; c++) out += part[rr * nchunk + c];
+            const int r = rbeg + rr;
+            const bool g1 = r >= rb1, g2 = r >= rb2, g3 = r >= rb3;
+            const int rb = (g1 ? rb1 : 0) + (g2 ? rb2 - rb1 : 0) + (g3 ? rb3 - rb2 : 0);
+            gfloat *yo = reinterpret_cast<gfloat *>(y0 + (g1 ? yd1 : 0) + (g2 ? yd2 : 0) + (g3 ? yd3 : 0)) + (r - rb);
+            *yo = out;
+        }
+    }
     GEMV_STAMP(6);
 }
 
@@ -779,16 +815,19 @@ static int env_int(const char *name, int dflt) {
 // (GGML_HIP_GEMV_MAP / _DEPTH / _ROWITEMS / _WG_PER_CU) and settable at run time by the
 // non-header debug entry point ggml_hip_debug_set_gemv_policy (tests sweep every path).
 struct GemvPolicy {
-    int map, depth, rowitems, wg_per_cu;
+    int map, depth, rowitems, wg_per_cu, bal;
 };
 static GemvPolicy &gemv_policy() {
     static GemvPolicy p = {env_int("GGML_HIP_GEMV_MAP", -1), env_int("GGML_HIP_GEMV_DEPTH", 0),
-                           env_int("GGML_HIP_GEMV_ROWITEMS", 1), env_int("GGML_HIP_GEMV_WG_PER_CU", 0)};
+                           env_int("GGML_HIP_GEMV_ROWITEMS", 1), env_int("GGML_HIP_GEMV_WG_PER_CU", 0),
+                           env_int("GGML_HIP_GEMV_BAL", -1)};
     return p;
 }
 void gemv_set_policy(int map, int depth, int rowitems, int wg_per_cu) {
-    gemv_policy() = {map, depth, rowitems, wg_per_cu};
+    const int bal = gemv_policy().bal;
+    gemv_policy() = {map, depth, rowitems, wg_per_cu, bal};
 }
+void gemv_set_bal(int bal) { gemv_policy().bal = bal; }
 
 int gemv_max_tokens(int64_t K) {
     const int64_t nb = K / QK;
@@ -798,12 +837,12 @@ int gemv_max_tokens(int64_t K) {
 }
 
 
-template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, int PRO = 0>
+template <int NT, int DIAG, int WAVES, int DEPTH, int VAR = 0, int PPL = 0, int PRO = 0, int BAL = 0>
 static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s,
                                 const GemvNorm *nrm = nullptr) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
-    const size_t lds = (size_t)NT * nb * 40 + (PRO == 1 ? WAVES * sizeof(double) : 0);
+    size_t lds = (size_t)NT * nb * 40 + (PRO == 1 ? WAVES * sizeof(double) : 0);
     const int wg_per_cu_env = gemv_policy().wg_per_cu;
     const int64_t M = m.row_begin[m.n];
     const int64_t need = (M + WAVES - 1) / WAVES;
@@ -813,7 +852,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     static int occ = 0;                    // resident workgroups per CU for this instantiation
     if (occ == 0) {
         int nb_occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, PRO>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, PRO, BAL>,
                                                          WAVES * 64, lds) != hipSuccess || nb_occ < 1)
             nb_occ = 1;
         occ = nb_occ;
@@ -831,6 +870,13 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     int map = map_env >= 0 ? map_env
             : ((M % ((int64_t)grid * WAVES)) % (cus * WAVES) == 0 ? 0 : ((int64_t)grid > cus ? 1 : 2));
     if (map == 2 && (int64_t)grid * M >= (int64_t)1 << 32) map = 1;   // the kernel's 32-bit row split
+    if (BAL) {                           // blocked rows; chunk sums of the workgroup's rows in LDS
+        if ((int64_t)grid * M >= (int64_t)1 << 32) return hipErrorInvalidValue;
+        map = 2;
+        const int64_t nchunk = (nb / 2 + 63) / 64;
+        lds += (size_t)((M + grid - 1) / grid) * nchunk * sizeof(float);
+        if (lds > 65536) return hipErrorInvalidValue;
+    }
     if (nb >= (1 << 16) || grid >= (1u << 14) || rowbytes > INT_MAX || M > INT_MAX) return hipErrorInvalidValue;
     GemvTail tail{};
     if (nrm) tail.nrm = *nrm;
@@ -841,7 +887,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     }
     const int geom = nb | map << 16 | (int)(grid << 18);
     (void)hipGetLastError();  // report only this launch's error
-    launch_k((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, PRO>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
+    launch_k((k_gemv_q4_0<NT, DIAG, WAVES, DEPTH, VAR, PPL, PRO, BAL>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
                        m.W[1], m.W[2], m.row_begin[1], m.row_begin[2], m.row_begin[3], (int)rowbytes, geom, (int)M, tail);
     return hipGetLastError();
 }
@@ -896,7 +942,24 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
                  : var == 7 ? launch_gemv_rows<NT, 0, 7>(m, K, x, dev, s, ppl, rd)
                             : launch_gemv_rows<NT, 0, 3>(m, K, x, dev, s, ppl, rd);
         }
-        // K > 12288: chunked items below (measured equal or faster at 4-5 pairs per lane)
+        // K > 12288: chunked items below (measured equal or faster at 4-5 pairs per lane), balanced at
+        // chunk granularity (BAL) when whole rows per wave leave a long tail: the busiest wave of the
+        // row-granular mapping streams ceil(M / waves) rows, a BAL wave ceil(rows per WG * chunks / 16)
+        // chunks; BAL when that is at most 0.65 of the rows' chunks (GGML_HIP_GEMV_BAL=0/1 overrides).
+        // Measured (tools/r2_bal.sh, 2 rounds): Falcon 18176 -> 4544 14.6 -> 13.2-14.1 us (the bench's
+        // Falcon-7B line 845 -> 875 tok/s), LLaMA-13B 13824 -> 5120 11.25 either way, NeoX 24576 -> 6144
+        // 20.2 -> 20.9-21.1 (0.75: not taken)
+        const int bal_env = gemv_policy().bal;
+        if (diag == 0 && var == 3 && bal_env != 0 && ppl > 3) {
+            const int64_t cus = dev.num_cus;
+            const int64_t wg = gemv_policy().wg_per_cu > 0 ? gemv_policy().wg_per_cu : (Mrows <= 2 * cus * 16 ? 1 : 2);
+            const int64_t grid = cus * wg, nchunk = (K / 64 + 63) / 64;
+            const int64_t rows_w = (Mrows + grid * 16 - 1) / (grid * 16);
+            const int64_t items_w = (((Mrows + grid - 1) / grid) * nchunk + 15) / 16;
+            if (bal_env == 1 || 20 * items_w <= 13 * rows_w * nchunk)
+                return depth == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 0, 0, 1>(m, K, x, dev, s)
+                                  : launch_gemv_w<NT, 0, 16, 2, 3, 0, 0, 1>(m, K, x, dev, s);
+        }
         if (diag == 7) return depth == 1 ? launch_gemv_w<NT, 7, 16, 1, 3>(m, K, x, dev, s)
                                          : launch_gemv_w<NT, 7, 16, 2, 3>(m, K, x, dev, s);
     }

@@ -445,6 +445,40 @@ def test_gemv_launch_policies_bitwise_identical(K, M, N):
         ggml_hip.check(L.ggml_hip_debug_set_gemv_policy(-1, 0, 1, 0), "policy reset")
 
 
+@pytest.mark.parametrize("K,M", [(18176, 4544), (13824, 5120), (12352, 333), (13824, 17), (24576, 6144)],
+                         ids=["falcon-4h_to_h", "llama13b-w2", "k12352-ragged", "m17", "neox-4h_to_h"])
+def test_gemv_balanced_chunks(K, M):
+    """The chunk-balanced decode GEMV (BAL, K > 12288: (row, chunk) items round-robin over a
+    workgroup's waves, per-item sums combined in chunk order) against the oracle, forced on and off;
+    deterministic (two runs bitwise equal), and independent of the row mapping: a sibling batch
+    whose rows straddle workgroups gives the single calls' y bitwise."""
+    L = ggml_hip.load()
+    L.ggml_hip_debug_set_gemv_bal.argtypes = [ctypes.c_int]
+    wq, x = make_case(K, M, 1, seed=7 * K + M)
+    y_ref = O.mul_mat(wq, K, x, nthreads=8, mode="avx2", pool=False)
+    s_abs = upper_s_abs(wq, O.quantize_q8_0(x, "avx2"), K)
+    try:
+        ys = {}
+        for bal in (1, 0):
+            ggml_hip.check(L.ggml_hip_debug_set_gemv_bal(bal), "bal")
+            ys[bal], _ = gpu_mul_mat(wq, K, x, algo=1)
+            check_y(ys[bal], y_ref, s_abs, RTOL, ATOL_BLOCKS)
+        ggml_hip.check(L.ggml_hip_debug_set_gemv_bal(1), "bal")
+        again, _ = gpu_mul_mat(wq, K, x, algo=1)
+        assert np.array_equal(again.view(np.uint32), ys[1].view(np.uint32))
+        if M >= 64:
+            Ms = [M // 3, M - M // 3]
+            parts = [np.ascontiguousarray(wq[:Ms[0]]), np.ascontiguousarray(wq[Ms[0]:])]
+            wds = [DB.from_array(p) for p in parts]
+            xd = DB.from_array(x)
+            yds = [DB(m * 4) for m in Ms]
+            ggml_hip.mul_mat_multi(wds, Ms, K, xd, 1, yds)
+            got = np.concatenate([yd.download((1, m), np.float32) for yd, m in zip(yds, Ms)], axis=1)
+            assert np.array_equal(got.view(np.uint32), ys[1].view(np.uint32))
+    finally:
+        ggml_hip.check(L.ggml_hip_debug_set_gemv_bal(-1), "bal reset")
+
+
 # ------------------------------------------------------------------------------- weight-residency cache
 def test_weight_cache_reuses_and_revalidates_host_weights():
     """a CPU-backend Q4_0 src0 is uploaded once per device and reused (bitwise

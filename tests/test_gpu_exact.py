@@ -128,3 +128,27 @@ def test_exact_sibling_group_one_launch_bitwise(exact_off, N):
     ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
     for (wq, _), yd, M in zip(cases, ys, Ms):
         assert_bitwise(yd.download((N, M), np.float32), O.mul_mat(wq, K, x))
+
+
+@pytest.mark.parametrize("K", [64, 4544, 11008, 18176, 22528, 22592])
+def test_exact_n1_long_rows_bitwise(exact_off, K):
+    """Exact-mode decode (N = 1) up to K = 22592 (Falcon's 18176 and past it, ragged final chunks):
+    single matrices, a sibling group, and the extreme rows the quantizer's tests cover — all
+    bitwise to the oracle's AVX2 schedule."""
+    L = exact_off
+    Ms = [48, 17, 33]
+    cases = [make_case(K, M, 1, seed=K + 7 * i) for i, M in enumerate(Ms)]
+    x = cases[0][1]
+    for wq, _ in cases[:1]:
+        y, _ = gpu_mul_mat(wq, K, x, algo=4)
+        assert_bitwise(y, O.mul_mat(wq, K, x, nthreads=4))
+    for row in (np.where(np.arange(K) % 7 == 0, 3.0e4, 0.0), np.full(K, -1e-30), np.zeros(K)):
+        xr = np.ascontiguousarray(row.reshape(1, K), np.float32)
+        y, _ = gpu_mul_mat(cases[0][0], K, xr, algo=4)
+        assert_bitwise(y, O.mul_mat(cases[0][0], K, xr))
+    assert L.ggml_hip_set_exact(1) == 0
+    wds, xd = [DB.from_array(c[0]) for c in cases], DB.from_array(x)
+    ys = [DB(M * 4) for M in Ms]
+    ggml_hip.mul_mat_multi(wds, Ms, K, xd, 1, ys)
+    for (wq, _), yd, M in zip(cases, ys, Ms):
+        assert_bitwise(yd.download((1, M), np.float32), O.mul_mat(wq, K, x))

@@ -5,7 +5,9 @@
 // 1192-1275) + COMPUTE (ggml_vec_dot_q4_0_q8_0 per row, ggml.c:2339-2607), with stream order
 // between them: task t reads its activation x_t only after every task < t has written its y.
 // The per-task arithmetic is the decode GEMV's (q4_0_kernels.hip, k_gemv_q4_0 with row items), so
-// every y is bitwise equal to the one-launch-per-mul_mat path.
+// every y is bitwise equal to the one-launch-per-mul_mat path — except for a launch the per-launch
+// GEMV runs chunk-balanced (BAL: K > 12288 with a row tail, e.g. Falcon's 18176 -> 4544), which sums
+// a row's 64-pair chunks separately; the chain keeps the per-lane row order (same oracle bound).
 //
 // Why one launch: a decode mul_mat streams 9-51 MB of weights in 2-8 us, and each launch pays a
 // kernel boundary (~1.5 us) plus a ramp in which the x prologue gates the first rows.  The WEIGHTS

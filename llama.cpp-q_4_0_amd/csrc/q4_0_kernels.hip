@@ -953,7 +953,9 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
         if (diag == 0 && var == 3 && bal_env != 0 && ppl > 3) {
             const int64_t cus = dev.num_cus;
             const int64_t wg = gemv_policy().wg_per_cu > 0 ? gemv_policy().wg_per_cu : (Mrows <= 2 * cus * 16 ? 1 : 2);
-            const int64_t grid = cus * wg, nchunk = (K / 64 + 63) / 64;
+            const int64_t need = (Mrows + 15) / 16, cap = cus * wg;        // launch_gemv_w's grid rule
+            const int64_t bgrid = need <= cus ? need : cus * ((need + cus - 1) / cus);
+            const int64_t grid = bgrid < cap ? bgrid : cap, nchunk = (K / 64 + 63) / 64;
             const int64_t rows_w = (Mrows + grid * 16 - 1) / (grid * 16);
             const int64_t items_w = (((Mrows + grid - 1) / grid) * nchunk + 15) / 16;
             if (bal_env == 1 || 20 * items_w <= 13 * rows_w * nchunk)

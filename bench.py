@@ -153,7 +153,15 @@ def main():
     if world > 1 or args.force_split:
         uid, uid_path = exchange_unique_id(gh, L, rank, world)
         comm = ctypes.c_void_p()
-        gh.check(L.ggml_hip_comm_init(ctypes.byref(comm), world, rank, uid), "comm_init")
+        # RCCL prints a version banner on fd 1 at init: keep stdout to the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            gh.check(L.ggml_hip_comm_init(ctypes.byref(comm), world, rank, uid), "comm_init")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         if rank == 0 and world > 1:
             try:
                 os.remove(uid_path)      # every rank has joined (comm init is collective)

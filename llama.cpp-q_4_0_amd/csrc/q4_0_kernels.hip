@@ -892,16 +892,19 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     return hipGetLastError();
 }
 
+#ifndef GEMV_RW
+#define GEMV_RW 16
+#endif
 template <int NT, int DIAG, int VAR>
 static hipError_t launch_gemv_rows(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s,
                                    int ppl, int rd) {
     switch (ppl) {
-        case 1: return rd == 1 ? launch_gemv_w<NT, DIAG, 16, 1, VAR, 1>(m, K, x, dev, s)
-                               : launch_gemv_w<NT, DIAG, 16, 2, VAR, 1>(m, K, x, dev, s);
-        case 2: return rd == 1 ? launch_gemv_w<NT, DIAG, 16, 1, VAR, 2>(m, K, x, dev, s)
-                               : launch_gemv_w<NT, DIAG, 16, 2, VAR, 2>(m, K, x, dev, s);
-        default: return rd == 1 ? launch_gemv_w<NT, DIAG, 16, 1, VAR, 3>(m, K, x, dev, s)
-                                : launch_gemv_w<NT, DIAG, 16, 2, VAR, 3>(m, K, x, dev, s);
+        case 1: return rd == 1 ? launch_gemv_w<NT, DIAG, GEMV_RW, 1, VAR, 1>(m, K, x, dev, s)
+                               : launch_gemv_w<NT, DIAG, GEMV_RW, 2, VAR, 1>(m, K, x, dev, s);
+        case 2: return rd == 1 ? launch_gemv_w<NT, DIAG, GEMV_RW, 1, VAR, 2>(m, K, x, dev, s)
+                               : launch_gemv_w<NT, DIAG, GEMV_RW, 2, VAR, 2>(m, K, x, dev, s);
+        default: return rd == 1 ? launch_gemv_w<NT, DIAG, GEMV_RW, 1, VAR, 3>(m, K, x, dev, s)
+                                : launch_gemv_w<NT, DIAG, GEMV_RW, 2, VAR, 3>(m, K, x, dev, s);
     }
 }
 

@@ -875,7 +875,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
         map = 2;
         const int64_t nchunk = (nb / 2 + 63) / 64;
         lds += (size_t)((M + grid - 1) / grid) * nchunk * sizeof(float);
-        if (lds > 65536) return hipErrorInvalidValue;
+        if (lds > GEMV_LDS_MAX) return hipErrorInvalidValue;   // launch_gemv checks before choosing BAL
     }
     if (nb >= (1 << 16) || grid >= (1u << 14) || rowbytes > INT_MAX || M > INT_MAX) return hipErrorInvalidValue;
     GemvTail tail{};
@@ -961,7 +961,8 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
             const int64_t grid = bgrid < cap ? bgrid : cap, nchunk = (K / 64 + 63) / 64;
             const int64_t rows_w = (Mrows + grid * 16 - 1) / (grid * 16);
             const int64_t items_w = (((Mrows + grid - 1) / grid) * nchunk + 15) / 16;
-            if (bal_env == 1 || 20 * items_w <= 13 * rows_w * nchunk)
+            const int64_t lds_bal = (K / QK) * 40 + ((Mrows + grid - 1) / grid) * nchunk * 4;
+            if (lds_bal <= GEMV_LDS_MAX && (bal_env == 1 || 20 * items_w <= 13 * rows_w * nchunk))
                 return depth == 1 ? launch_gemv_w<NT, 0, 16, 1, 3, 0, 0, 1>(m, K, x, dev, s)
                                   : launch_gemv_w<NT, 0, 16, 2, 3, 0, 0, 1>(m, K, x, dev, s);
         }

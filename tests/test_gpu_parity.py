@@ -445,8 +445,10 @@ def test_gemv_launch_policies_bitwise_identical(K, M, N):
         ggml_hip.check(L.ggml_hip_debug_set_gemv_policy(-1, 0, 1, 0), "policy reset")
 
 
-@pytest.mark.parametrize("K,M", [(18176, 4544), (13824, 5120), (12352, 333), (13824, 17), (24576, 6144)],
-                         ids=["falcon-4h_to_h", "llama13b-w2", "k12352-ragged", "m17", "neox-4h_to_h"])
+@pytest.mark.parametrize("K,M", [(18176, 4544), (13824, 5120), (12352, 333), (13824, 17), (24576, 6144),
+                                 (49152, 600), (52224, 600)],
+                         ids=["falcon-4h_to_h", "llama13b-w2", "k12352-ragged", "m17", "neox-4h_to_h",
+                              "lds-61k", "lds-over-64k-falls-back"])
 def test_gemv_balanced_chunks(K, M):
     """The chunk-balanced decode GEMV (BAL, K > 12288: (row, chunk) items round-robin over a
     workgroup's waves, per-item sums combined in chunk order) against the oracle, forced on and off;

@@ -1972,8 +1972,8 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
 //   y      = ((acc0+acc4) + (acc2+acc6)) + ((acc1+acc5) + (acc3+acc7))   (hsum_float_8, ggml.c:591)
 // Eight threads per output row each run one lane's chain in block order, so all the freedom left
 // is the memory schedule.  Chunks of EX_C = 64 blocks move global -> LDS by LDS-DMA only (no
-// register staging, so nothing in flight is tied to a loop-carried register): a 3-slot ring, two
-// chunks in flight, one counted `s_waitcnt vmcnt` + raw `s_barrier` per chunk (the slot refilled
+// register staging, so nothing in flight is tied to a loop-carried register): an S-slot ring (2 at
+// N = 1, 3 above), S - 1 chunks in flight, one counted `s_waitcnt vmcnt` + raw `s_barrier` per chunk (the slot refilled
 // after the barrier is the one every wave finished before it).  Per slot:
 //   weights: the 16 rows' 1152-byte row pieces as 16-byte units interleaved across rows (unit
 //            (row r, piece k) at u = 16k + r, 9 x 1 KiB `buffer_load_dwordx4 ... lds` per wave):
@@ -1993,7 +1993,14 @@ constexpr int EX_THREADS = EX_RB * 8;                // 128 = 2 waves
 constexpr int EX_C = 64;                             // blocks per chunk
 constexpr int EX_WB = EX_RB * EX_C * Q4B;            // weight bytes per slot (18 KiB)
 constexpr int EX_WI = EX_WB / 1024 / 2;              // 1-KiB weight DMAs per wave per chunk (9)
-constexpr int EX_S = 3;                              // ring slots
+// ring slots (S - 1 chunks in flight), per column count: decode (NC = 1) runs 2 slots = 41 KB of LDS,
+// three workgroups per CU instead of two (tools/r2_exs.sh: exact decode 467 -> 532 tok/s; 4 slots 377);
+// -DEX_SLOTS overrides every NC for A/B builds
+#ifdef EX_SLOTS
+constexpr int ex_slots(int) { return EX_SLOTS; }
+#else
+constexpr int ex_slots(int nc) { return nc == 1 ? 2 : 3; }
+#endif
 static_assert(EX_WB % 2048 == 0, "whole 1-KiB weight DMAs per wave");
 
 template <int NC>
@@ -2003,6 +2010,7 @@ struct ExLayout {
     static constexpr int DXB = DXW * 2 * 64 * 4;                 // d_x bytes per slot
     static constexpr int SLOT = EX_WB + XB + DXB;
     static constexpr int OPS = EX_WI + NC + DXW;                 // vector-memory ops per wave per chunk
+    static constexpr int S = ex_slots(NC);                       // ring slots
     static_assert(OPS <= 63, "vmcnt immediate");
 };
 
@@ -2055,7 +2063,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const ExMats mats,
     auto issue = [&](int ch) __attribute__((always_inline)) {
         const bool valid = ch < nchunks;                    // past the end: counted, no traffic
         const int b0 = valid ? ch * EX_C : 0;
-        uint8_t *slot = smem + (ch % EX_S) * Lay::SLOT;
+        uint8_t *slot = smem + (ch % Lay::S) * Lay::SLOT;
         const __amdgpu_buffer_rsrc_t w_ = valid ? wrs : nul;
 #pragma unroll
         for (int i = 0; i < EX_WI; i++)
@@ -2129,13 +2137,13 @@ __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const ExMats mats,
     };
     constexpr int BB = NC <= 2 ? 4 : 2;                      // steps per pipelined batch (lgkmcnt <= 15)
 
-    issue(0);
-    issue(1);
+#pragma unroll
+    for (int c = 0; c < Lay::S - 1; c++) issue(c);
     for (int ch = 0; ch < nchunks; ch++) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Lay::OPS) : "memory");   // my DMAs of chunk ch landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Lay::OPS * (Lay::S - 2)) : "memory");   // chunk ch landed
         __builtin_amdgcn_s_barrier();                       // everyone's landed; chunk ch-1 consumed
-        issue(ch + 2);                                      // into chunk ch-1's slot
-        const uint8_t *slot = smem + (ch % EX_S) * Lay::SLOT;
+        issue(ch + Lay::S - 1);                             // into chunk ch-1's slot
+        const uint8_t *slot = smem + (ch % Lay::S) * Lay::SLOT;
         const int cb = min(EX_C, nb - ch * EX_C);
         if (cb == EX_C) {
             Op ops[2][BB];
@@ -2189,7 +2197,7 @@ static hipError_t launch_exact(const ExMats &m, int n, int64_t K, const int8_t *
                                hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
-    const int lds = EX_S * ExLayout<NC>::SLOT;
+    const int lds = ExLayout<NC>::S * ExLayout<NC>::SLOT;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void *)k_mm_exact_q4_0<NC>,

@@ -310,7 +310,8 @@ def main():
     if rank == 0 and world == 1 and comm is None:
         result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
         if not args.no_prefill and args.prefill_tokens > 0:
-            result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens)
+            result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens,
+                                              groups=[tuple(g) for g in groups])
         if not args.no_exact:
             result["exact_mode"] = exact_decode(gh, L, decode_step, stream, args)
         if not args.no_extra:
@@ -487,14 +488,28 @@ def run_launch(gh, L, kind, a, xs, stream):
         gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, 1, yb.ptr, m_loc, 1, stream))
 
 
-def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3):
+def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0, 1, 2), (3,), (4, 5), (6,))):
     """N-token prefill through `layers` layers of the stack (7 mul_mats each, q8_0 quantize +
-    int8-MFMA GEMM).  GB/s = (W + 4KN + 4MN) / t."""
+    int8-MFMA GEMM), sibling groups as in decode (wq|wk|wv and w1|w3 share src1: one q8_0 quantize
+    per group, ggml_hip_mul_mat_q4_0_multi, the call the hook makes for a held sibling group).
+    GB/s = (W + 4KN + 4MN) / t."""
     mats = [m for row in stack.mats[:layers] for m in row]
+    ybuf = {}
+    calls = []
+    for row in stack.mats[:layers]:
+        for g in groups:
+            K = row[g[0]][1]
+            n = len(g)
+            for i in g:                                  # one output per sibling (distinct buffers)
+                ybuf.setdefault(i, gh.DeviceBuffer(row[i][3] * 4 * N))
+            wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
+            mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
+            yp = (ctypes.c_void_p * n)(*[ybuf[i].ptr for i in g])
+            calls.append((n, wp, mp, K, yp))
 
     def run():
-        for name, K, M, m_loc, buf, rb in mats:
-            gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, N, ys[M].ptr, m_loc, 2, stream))
+        for n, wp, mp, K, yp in calls:
+            gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, N, yp, stream))
     run()
     gh.check(L.ggml_hip_stream_synchronize(stream))
     a, b = gh.Event(), gh.Event()

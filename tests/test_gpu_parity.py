@@ -169,9 +169,11 @@ def test_gemv_and_gemm_agree(N):
         check_y(y1, y2, s_abs, RTOL, ATOL_BLOCKS)
 
 
-@pytest.mark.parametrize("N", [1, 3, 8, 20])
+@pytest.mark.parametrize("N", [1, 3, 8, 20, 200, 512])
 def test_multi_matrix_siblings_match_single_calls(N):
-    """wq|wk|wv-style sibling batch (shared x, different M) == separate calls, bitwise."""
+    """wq|wk|wv-style sibling batch (shared x, different M) == separate calls, bitwise: one GEMV launch
+    (N <= 8), one x quantize + a GEMM per matrix (split-K range), one GEMM launch over the concatenated
+    row tiles (N > 128; M = 300 ends mid-tile)."""
     K = 4096
     Ms = [256, 128, 300]
     cases = [make_case(K, M, N, seed=40 + i) for i, M in enumerate(Ms)]

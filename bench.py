@@ -15,8 +15,9 @@ one grouped RCCL all-gather of their y slices over xGMI (4 collectives per layer
 value = tokens/s of the sharded model (strong scaling: total work fixed).
 
 Extra fields: per-kernel roofline of the dominant kernel (the decode GEMV) from HIP events on
-the launch stream, prefill (N=512) GB/s and int8-MFMA TOP/s, and the CPU baseline (the oracle's
-AVX2 restatement of ggml.c's path on this host).
+the launch stream, prefill (N=512, the same sibling groups: one x quantize per group) GB/s and
+int8-MFMA TOP/s, exact-mode decode, the LLaMA-13B / Falcon-7B decode shapes, and the CPU baseline
+(the reference's own ggml.c built from /root/reference into oracle/_ref, on this host's cores).
 """
 import argparse
 import ctypes

@@ -394,11 +394,13 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
         nlaunch += len(sel)
     achieved = tot_bytes / tot_t / 1e9
     traffic, src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01_gemv_pmc_traffic.json")
-    if os.path.exists(pmc):          # measured by tools/pmc_traffic.sh (rocprofv3 --pmc passes)
+    # the newest round's PMC pass (tools/pmc_traffic.sh: rocprofv3 --pmc passes over this bench's
+    # decode graph), so the line cites a profile of the current GEMV code
+    pmcs = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_gemv_pmc_traffic.json"))
+    if pmcs:
         try:
-            traffic = round(json.load(open(pmc))["traffic_bytes_per_launch_mean"])
-            src = "profiles/r01_gemv_pmc_traffic.json: 2*FETCH_SIZE+WRITE_SIZE (x1024) per GEMV launch, mean"
+            traffic = round(json.load(open(os.path.join(ROOT, "profiles", pmcs[-1])))["traffic_bytes_per_launch_mean"])
+            src = f"profiles/{pmcs[-1]}: 2*FETCH_SIZE+WRITE_SIZE (x1024) per GEMV launch, mean"
         except Exception:
             traffic = None
     return {"bound": "hbm", "kernel": "k_gemv_q4_0<NT=1,...> (fused q8_0 quantize + q4_0.q8_0 GEMV, one row item per wave ring slot)",

@@ -168,9 +168,14 @@ int ggml_hip_reserve_workspace(int64_t K, int64_t N);
  * A chain runs tasks 0..n-1 in order inside one launch: task t reads x only after every task < t
  * has written its y (so x of a task may be, or overlap, the y of an earlier task), while the
  * weight loads of later tasks stream ahead.  Results are bitwise equal to n separate
- * ggml_hip_mul_mat_q4_0_multi(N = 1) calls.  Weights must not change while a launch runs; a
- * task's y must not overlap its own x.  Exact mode (ggml_hip_set_exact) runs the tasks as
- * separate exact-mode calls.  No ggml-cuda.h counterpart.
+ * ggml_hip_mul_mat_q4_0_multi(N = 1) calls, except for long rows (K > 12288) whose separate call
+ * takes the chunk-balanced GEMV (BAL, a different fp32 order within the same parity bound).
+ * Weights must not change while a launch runs; a task's y must not overlap its own x (create
+ * rejects it).  The launch is persistent: its grid (one workgroup per CU) must be co-resident, so
+ * do not run other kernels concurrently on the device while it runs; a dependency wait that never
+ * completes gives up after a bounded spin, and results are UNDEFINED until ggml_hip_chain_status
+ * returns 0.  Exact mode (ggml_hip_set_exact) runs the tasks as separate exact-mode calls.  No
+ * ggml-cuda.h counterpart; default off (slower than per-launch GEMVs).
  * ---------------------------------------------------------------------------------------- */
 typedef struct ggml_hip_chain_task {
     int nmat;                 /* 1..4 sibling matrices sharing x (e.g. wq|wk|wv) */

@@ -62,6 +62,7 @@ struct Cached {
 constexpr size_t RING = 1024, SLOT_BLOB = 1008;
 struct Slot {
     const void *fn;
+    int device;               // the device the launch was recorded on (the worker follows it)
     dim3 grid, block;
     uint32_t lds;
     int nargs;
@@ -84,7 +85,8 @@ Launcher &launcher() {
     return *l;
 }
 void launcher_main(Launcher *L) {
-    (void)hipSetDevice(L->device);
+    int cur_dev = L->device;
+    (void)hipSetDevice(cur_dev);
     void *argv[MAX_ARGS];
     for (;;) {
         uint64_t t = L->tail.load(std::memory_order_relaxed);
@@ -100,6 +102,10 @@ void launcher_main(Launcher *L) {
             L->sleeping.store(false, std::memory_order_relaxed);
         }
         Slot &sl = L->ring[t % RING];
+        if (sl.device != cur_dev) {            // the recorded stream moved to another device
+            cur_dev = sl.device;
+            (void)hipSetDevice(cur_dev);
+        }
         for (int a = 0; a < sl.nargs; a++) argv[a] = sl.blob + sl.off[a];
         const hipError_t e = hipLaunchKernel(sl.fn, sl.grid, sl.block, argv, sl.lds, L->stream);
         if (e != hipSuccess) L->err.store((int)e, std::memory_order_relaxed);
@@ -121,6 +127,14 @@ Recorder &rec() {
     static Recorder r;
     return r;
 }
+// One recorder per process, used by every thread that launches (the hook thread, loopback ranks,
+// tensor-free callers): every entry point below holds this lock, so a thread's flush can never
+// interleave with another thread's half-recorded run (the vector and the argument blob).
+std::recursive_mutex &rec_mu() {
+    static std::recursive_mutex *m = new std::recursive_mutex;   // never destroyed (atexit order)
+    return *m;
+}
+#define REC_LOCK std::lock_guard<std::recursive_mutex> rec_lock_(rec_mu())
 
 void fatal(hipError_t e, const char *what) {
     fprintf(stderr, "ggml-hip: launch recorder: %s failed: %s\n", what, hipGetErrorString(e));
@@ -233,11 +247,13 @@ bool update(Cached *c, Run &run) {
 }  // namespace
 
 bool rec_active(hipStream_t s) {
+    REC_LOCK;
     const Recorder &r = rec();
     return r.on && s == r.stream;
 }
 
 bool rec_pending() {
+    REC_LOCK;
     if (!rec().cur.items.empty()) return true;
     const Launcher &L = launcher();
     return L.started && L.head.load(std::memory_order_relaxed) != L.tail.load(std::memory_order_acquire);
@@ -257,11 +273,13 @@ void async_push(const void *fn, dim3 grid, dim3 block, size_t lds, int nargs, vo
     if (L.stream != r.stream) {                // the worker serves one stream: drain, then switch
         while (L.tail.load(std::memory_order_acquire) != L.head.load(std::memory_order_relaxed)) std::this_thread::yield();
         L.stream = r.stream;
+        (void)hipGetDevice(&L.device);         // the new stream's device (ggml_hip_set_main_device)
     }
     const uint64_t h = L.head.load(std::memory_order_relaxed);
     while (h - L.tail.load(std::memory_order_acquire) >= RING) std::this_thread::yield();
     Slot &sl = L.ring[h % RING];
     sl.fn = fn;
+    sl.device = L.device;
     sl.grid = grid;
     sl.block = block;
     sl.lds = (uint32_t)lds;
@@ -294,6 +312,7 @@ void async_drain() {
 
 void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, int nargs, void *const *args,
                 const size_t *sizes, const size_t *aligns) {
+    REC_LOCK;
     Recorder &r = rec();
     if (nargs > MAX_ARGS) {
         fprintf(stderr, "ggml-hip: launch recorder: %d kernel arguments (max %d)\n", nargs, MAX_ARGS);
@@ -329,6 +348,7 @@ void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s
 }
 
 void rec_flush_at(const char *why) {
+    REC_LOCK;
     static const bool trace = getenv("GGML_HIP_TRACE_GRAPH") != nullptr;
     if (trace && !rec().cur.items.empty())
         fprintf(stderr, "rec_flush: %zu launches, by %s\n", rec().cur.items.size(), why);
@@ -336,6 +356,7 @@ void rec_flush_at(const char *why) {
 }
 
 void rec_flush() {
+    REC_LOCK;
     async_drain();
     submit(false);
 }
@@ -388,21 +409,23 @@ void submit(bool chunk) {
 }
 }  // namespace
 
-// recording on / off for stream s; switching streams submits what is pending (turning recording off
-// does not: the next eager launch or sync point does)
+// recording on / off for stream s; switching streams or turning recording off submits what is pending
 void rec_set_mode(int mode) {
+    REC_LOCK;
     rec_flush();
     rec().mode = mode == 2 ? 2 : 1;
 }
 
 void rec_enable(hipStream_t s, bool on) {
+    REC_LOCK;
     Recorder &r = rec();
-    if (s != r.stream) rec_flush();
+    if (s != r.stream || !on) rec_flush();
     r.stream = s;
     r.on = on;
 }
 
 void rec_stats(long long *runs, long long *kernels, long long *updated, long long *built, long long *submit_ns) {
+    REC_LOCK;
     const Recorder &r = rec();
     *submit_ns = r.submit_ns;
     *runs = r.runs;
@@ -412,6 +435,7 @@ void rec_stats(long long *runs, long long *kernels, long long *updated, long lon
 }
 
 void rec_clear_cache() {
+    REC_LOCK;
     Recorder &r = rec();
     rec_flush();
     for (Cached *c : r.cache) destroy(c);

@@ -104,6 +104,21 @@ int g_device_count = 0;
 Device *g_dev = nullptr;
 int g_main_device = 0;
 float g_tensor_split[GGML_HIP_MAX_DEVICES] = {0};
+
+// ggml-cuda.cu:1874-1881: cumulative start fractions in float, each divided by the float sum
+static void split_fractions(const float *tensor_split, int n, float *frac) {
+    float split_sum = 0.0f;
+    for (int i = 0; i < n; i++) {
+        frac[i] = split_sum;
+        split_sum += tensor_split[i];
+    }
+    for (int i = 0; i < n; i++) frac[i] /= split_sum;
+}
+
+// ggml-cuda.cu:2363, 2785: row_low = nrows0*g_tensor_split[id] -- int64*float is a float product
+static inline int64_t split_row_low(int64_t nrows, const float *frac, int id) {
+    return id == 0 ? 0 : (int64_t)(nrows * frac[id]);
+}
 size_t g_scratch_size = 0;
 void *g_scratch = nullptr;
 size_t g_scratch_offset = 0;
@@ -476,8 +491,8 @@ bool on_device(const tensor *t) {
 
 void split_range(int64_t nrows, int id, int64_t *lo, int64_t *hi) {
     // ggml-cuda.cu:2361-2368 / 2779-2786
-    *lo = id == 0 ? 0 : (int64_t)(nrows * g_tensor_split[id]);
-    *hi = id == g_device_count - 1 ? nrows : (int64_t)(nrows * g_tensor_split[id + 1]);
+    *lo = split_row_low(nrows, g_tensor_split, id);
+    *hi = id == g_device_count - 1 ? nrows : split_row_low(nrows, g_tensor_split, id + 1);
 }
 
 bool supported_mul_mat(const tensor *src0, const tensor *src1, const tensor *dst) {
@@ -1655,12 +1670,7 @@ void ggml_hip_set_tensor_split(const float *tensor_split) {
     for (int i = 0; i < g_device_count; i++)
         if (tensor_split[i] != 0.0f) all_zero = false;
     if (all_zero) return;
-    float sum = 0.0f;
-    for (int i = 0; i < g_device_count; i++) {
-        g_tensor_split[i] = sum;
-        sum += tensor_split[i];
-    }
-    for (int i = 0; i < g_device_count; i++) g_tensor_split[i] /= sum;
+    split_fractions(tensor_split, g_device_count, g_tensor_split);
 }
 
 bool ggml_hip_can_mul_mat(const struct ggml_tensor *src0_, const struct ggml_tensor *src1_, struct ggml_tensor *dst_) {
@@ -2251,6 +2261,11 @@ int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip
             w[2 * i + 1] = (uint32_t)(wp >> 32);
             w[8 + 2 * i] = (uint32_t)yp;
             w[8 + 2 * i + 1] = (uint32_t)(yp >> 32);
+            if (used) {                   // a task's y may not overlap its own x (its rows read x while others write y)
+                const uint64_t xlo = (uint64_t)(uintptr_t)k.x, xhi = xlo + 4 * (uint64_t)k.K;
+                if (yp < xhi && xlo < yp + 4 * (uint64_t)k.M[i])
+                    return fail(GGML_HIP_ERR_INVALID, "a task's y overlaps its own x");
+            }
             total += used ? k.M[i] : 0;
             rb[i + 1] = (int)std::min<int64_t>(total, 1 << 30);
         }
@@ -2591,16 +2606,17 @@ int ggml_hip_split_rows(int64_t M, int nranks, const float *tensor_split, int64_
         for (int r = 0; r <= nranks; r++) row_begin[r] = M * r / nranks;
         return GGML_HIP_OK;
     }
-    // cumulative start fractions, as ggml_cuda_set_tensor_split normalises them
-    double sum = 0;
-    for (int r = 0; r < nranks; r++) sum += tensor_split[r];
-    if (sum <= 0) return ggml_hip_split_rows(M, nranks, nullptr, row_begin);
-    float acc = 0.0f;
-    for (int r = 0; r < nranks; r++) {
-        const float start = (float)(acc / sum);
-        row_begin[r] = r == 0 ? 0 : (int64_t)(M * start);
-        acc += tensor_split[r];
-    }
+    // the reference's rule, in its float arithmetic: cumulative start fractions normalised as
+    // ggml_cuda_set_tensor_split does (ggml-cuda.cu:1874-1881), then row_low = nrows0*split[id]
+    // (float product truncated, ggml-cuda.cu:2363-2364) -- one routine with set_tensor_split
+    if (nranks > GGML_HIP_MAX_DEVICES) return fail(GGML_HIP_ERR_INVALID, "too many ranks");
+    bool all_zero = true;
+    for (int r = 0; r < nranks; r++)
+        if (tensor_split[r] != 0.0f) all_zero = false;
+    if (all_zero) return ggml_hip_split_rows(M, nranks, nullptr, row_begin);
+    float frac[GGML_HIP_MAX_DEVICES];
+    split_fractions(tensor_split, nranks, frac);
+    for (int r = 0; r < nranks; r++) row_begin[r] = split_row_low(M, frac, r);
     row_begin[nranks] = M;
     for (int r = 1; r <= nranks; r++)
         if (row_begin[r] < row_begin[r - 1]) row_begin[r] = row_begin[r - 1];

@@ -924,7 +924,7 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
     // when a wave has at most two rows and x is short (wq|wk|wv 7.33 -> 7.19 us, wo 4.82 -> 4.24);
     // VAR 3 otherwise (w1|w3 at 2.7 rows per wave 10.56 vs 10.73, w2 at K = 11008 7.33 vs 8.06)
     const int64_t Mrows = m.row_begin[m.n];
-    const int var = var_env >= 0 ? var_env : (NT == 1 && K <= 8192 && Mrows <= 2 * 512 * 16 ? 15 : 3);
+    const int var = var_env >= 0 ? var_env : (NT == 1 && K <= 8192 && Mrows <= 2 * 16 * (int64_t)dev.num_cus * 2 ? 15 : 3);
     const int depth = depth_env ? depth_env : (K / 64 > 64 ? 2 : 1);
     if constexpr (NT == 1) {
         if (diag == 8) return launch_gemv_w<NT, 8, 16, 1>(m, K, x, dev, s);
@@ -1054,7 +1054,7 @@ hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M
     static const int var_env = env_int("GGML_HIP_GEMV_VAR", -1);
     const int depth_env = gemv_policy().depth;
     const int64_t Mrows = m.row_begin[m.n];
-    const int var = var_env == 15 || var_env == 3 ? var_env : (K <= 8192 && Mrows <= 2 * 512 * 16 ? 15 : 3);
+    const int var = var_env == 15 || var_env == 3 ? var_env : (K <= 8192 && Mrows <= 2 * 16 * (int64_t)dev.num_cus * 2 ? 15 : 3);
     const int rd = depth_env == 2 ? 2 : 1;
     const int ppl = (int)((K / 64 + 63) / 64);
     if (var == 15) {

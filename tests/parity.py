@@ -7,9 +7,17 @@ y comparison uses the per-element bound of SURVEY.md §7.3:
     |y_gpu - y_ref| <= rtol * |y_ref| + atol_blocks * S_abs,
     S_abs[n, m] = sum_b |d_w[m,b] * d_x[n,b] * sumi[n,m,b]|
 
-and also reports max relative error over |y_ref| > 1e-3 * max|y_ref|.
+and also reports max relative error over |y_ref| > 1e-3 * max|y_ref|.  SURVEY §7.3 sets
+atol_blocks = 1e-6; a float32 simulation of the GEMM's block-sequential fma chain against the
+oracle at 4096x4096x512 needs at most 8.2e-8 (12x margin).  Every check_y call records its
+worst relative error and the smallest atol_blocks that would have passed; conftest.py prints the
+table at the end of the run (`parity report`).
 """
+import os
+
 import numpy as np
+
+REPORT = []          # (test id, n elements, max rel (well conditioned), atol_blocks needed)
 
 QK = 32
 
@@ -44,12 +52,35 @@ def block_terms(wq, xq, K):
     return t.sum(axis=2), np.abs(t).sum(axis=2)
 
 
+def s_abs_exact(wq, xq, K, n_chunk=None):
+    """S_abs[n, m] = sum_b |d_w d_x sumi| exactly (integer block sums through float32 BLAS: every
+    partial sum is an integer below 2^24, so the products are exact), chunked over blocks so that
+    full LLaMA shapes (512 x 11008 x 128 blocks) fit in memory.  Replaces the elementwise
+    |W_deq| @ |X_deq|^T upper bound, which is ~sqrt(32)x looser."""
+    dw, w = split_q4_0(wq, K)
+    dx, q = split_q8_0(xq, K)
+    N, M, nb = q.shape[0], w.shape[0], K // QK
+    out = np.zeros((N, M), np.float32)
+    wf = w.astype(np.float32)
+    qf = q.astype(np.float32)
+    for b in range(nb):
+        s = qf[:, b, :] @ wf[:, b, :].T
+        np.abs(s, out=s)
+        s *= np.abs(dx[:, b])[:, None]
+        s *= np.abs(dw[:, b])[None, :]
+        out += s
+    return out.astype(np.float64)
+
+
 def check_y(y_got, y_ref, s_abs, rtol=1e-3, atol_blocks=1e-6):
     """Assert the per-element bound; return (max_rel_well_conditioned, max_abs_err)."""
     y_got = np.asarray(y_got, dtype=np.float64)
     y_ref = np.asarray(y_ref, dtype=np.float64)
     err = np.abs(y_got - y_ref)
     bound = rtol * np.abs(y_ref) + atol_blocks * s_abs
+    with np.errstate(divide="ignore", invalid="ignore"):
+        need = np.where(s_abs > 0, (err - rtol * np.abs(y_ref)) / s_abs, np.where(err > rtol * np.abs(y_ref), np.inf, 0))
+    need_max = float(max(need.max(), 0.0)) if need.size else 0.0
     bad = err > bound
     if bad.any():
         i = np.argwhere(bad)[0]
@@ -57,4 +88,5 @@ def check_y(y_got, y_ref, s_abs, rtol=1e-3, atol_blocks=1e-6):
                              f"ref {y_ref[tuple(i)]} bound {bound[tuple(i)]}")
     big = np.abs(y_ref) > 1e-3 * np.abs(y_ref).max()
     rel = (err[big] / np.abs(y_ref[big])).max() if big.any() else 0.0
+    REPORT.append((os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0], int(err.size), float(rel), need_max))
     return float(rel), float(err.max())

@@ -75,6 +75,36 @@ def test_split_rows_fractions_match_reference_rule(lib):
     assert list(rb) == expect
 
 
+def _reference_split_rows_f32(M, ts):
+    """float32 restatement of ggml-cuda.cu:1874-1881 (cumulative start fractions summed and divided
+    in float) and :2363-2364 (row_low = nrows0*g_tensor_split[id], an int64*float product truncated)."""
+    s = np.float32(0)
+    starts = []
+    for t in np.asarray(ts, np.float32):
+        starts.append(s)
+        s = np.float32(s + t)
+    frac = [np.float32(c / s) for c in starts]
+    return [0] + [int(np.float32(np.float32(M) * f)) for f in frac[1:]] + [M]
+
+
+SPLITS = [[0.1, 0.2, 0.3, 0.4], [1 / 3, 1 / 3, 1 / 3], [0.3, 0.3, 0.4], [0.7, 0.1, 0.1, 0.1],
+          [0.125] * 8, [0.15, 0.05, 0.2, 0.1, 0.1, 0.1, 0.1, 0.1], [1 / 7] * 7, [0.6, 0.4]]
+
+
+@pytest.mark.parametrize("ts", SPLITS, ids=lambda t: "x".join(f"{v:.3g}" for v in t))
+def test_split_rows_non_representable_fractions_bit_exact(lib, ts):
+    """Non-representable fractions: every boundary row equals the reference's float rule bit for
+    bit (a double-precision sum puts some boundaries one row away, e.g. M=9 with the 8-way split).
+    The LLaMA/Falcon/13B row counts plus every M < 2048."""
+    n = len(ts)
+    tsa = np.asarray(ts, np.float32)
+    for M in list(range(0, 2048)) + [4096, 4544, 4672, 5120, 11008, 13824, 18176, 32000]:
+        rb = np.zeros(n + 1, np.int64)
+        ggml_hip.check(lib.ggml_hip_split_rows(M, n, tsa.ctypes.data_as(ctypes.c_void_p),
+                                               rb.ctypes.data_as(ctypes.c_void_p)))
+        assert list(rb) == _reference_split_rows_f32(M, tsa), (M, ts)
+
+
 def test_can_mul_mat_declines_without_device(lib):
     """No HIP device: every node is declined, so ggml.c plans and runs its own CPU mul_mat (the
     shape rule itself, ggml-cuda.cu:2595-2610, is tests/test_gpu_parity.py::test_can_mul_mat_rule)."""

@@ -153,7 +153,7 @@ def test_chain_against_oracle():
             y = ys[t][i].download((1, M), np.float32)
             y_ref = O.mul_mat(wq[t][i], K, xin.reshape(1, K), nthreads=1)
             _, s_abs = block_terms(wq[t][i], xq, K)
-            check_y(y, y_ref, s_abs, rtol=1e-3, atol_blocks=1e-5)
+            check_y(y, y_ref, s_abs, rtol=1e-3, atol_blocks=1e-6)
 
 
 def test_chain_graph_replay_bitwise():

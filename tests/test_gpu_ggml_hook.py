@@ -30,7 +30,7 @@ pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not gpu_available(), reason="needs a HIP device and libggml_hip.so"),
               pytest.mark.skipif(not os.path.exists(LIB), reason="oracle/_ref/libggml_ref_hip.so not built")]
 
-RTOL, ATOL_BLOCKS = 1e-3, 1e-5
+RTOL, ATOL_BLOCKS = 1e-3, 1e-6
 GGML_BACKEND_CPU = 0
 
 
@@ -96,6 +96,41 @@ def test_declined_node_runs_reference_cpu_op(ref):
     y, be = ggml_mul_mat(ref, wq, 4096, x, 0, 2)
     assert be == GGML_BACKEND_CPU
     assert np.array_equal(y.view(np.uint32), load("avx2", "y4096_mul_mat").view(np.uint32))
+
+
+@pytest.mark.parametrize("N", [1, 4, 31])
+def test_large_cpu_weight_taken_at_decode(ref, N):
+    """The deliberate deviation from ggml-cuda.cu:2595-2610: a CPU-backend Q4_0
+    weight of >= GGML_HIP_DECODE_MIN_WEIGHTS (2^19) elements is taken at N < 32 (the reference would
+    decline it, since it re-uploads host weights per call, ggml-cuda.cu:2496-2502).  The node must
+    reach the backend (one residency-cache upload, then hits), with y within the bound of the oracle."""
+    from hip_env import ggml_hip
+    L = ggml_hip.load()
+    ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+    K, M = 4096, 128                                       # 2^19 elements: exactly the threshold
+    wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED7500 + N, 0.0, 0.02).reshape(M, K))
+    x = O.gaussian(N * K, 0x5EED7600 + N, 0.0, 1.0).reshape(N, K)
+
+    def stats():
+        h, m, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        ggml_hip.check(L.ggml_hip_weight_cache_stats(ctypes.byref(h), ctypes.byref(m), ctypes.byref(r)))
+        return h.value, m.value
+
+    try:
+        y, be = ggml_mul_mat(ref, wq, K, x, 0, 2)
+        assert be == GGML_BACKEND_CPU
+        assert stats() == (0, 1)                            # taken: the weight was uploaded once
+        y2, _ = ggml_mul_mat(ref, wq, K, x, 0, 2)
+        assert stats() == (1, 1)                            # and reused on the next call
+        assert np.array_equal(y.view(np.uint32), y2.view(np.uint32))
+        assert_close(wq, x, K, y, O.mul_mat(wq, K, x))
+        # one row short of the threshold: declined, ggml's own CPU op (bitwise the oracle)
+        w_small = np.ascontiguousarray(wq[:M - 1])
+        ys, _ = ggml_mul_mat(ref, w_small, K, x, 0, 2)
+        assert stats() == (1, 1)
+        assert np.array_equal(ys.view(np.uint32), O.mul_mat(w_small, K, x).view(np.uint32))
+    finally:
+        ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
 
 
 def _device_count():

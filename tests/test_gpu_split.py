@@ -29,7 +29,7 @@ pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not gpu_available(), reason="needs a HIP device and libggml_hip.so")]
 
 DB = ggml_hip.DeviceBuffer
-RTOL, ATOL_BLOCKS = 1e-3, 1e-5
+RTOL, ATOL_BLOCKS = 1e-3, 1e-6
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 

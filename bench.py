@@ -188,8 +188,8 @@ def main():
         gh.check(L.ggml_hip_fill_gaussian(b.ptr, K * max(1, args.prefill_tokens), 0x5EED1000 + K, 0.0, 1.0, None))
         xs[K] = b
     ys = {M: gh.DeviceBuffer(M * 4 * max(1, args.prefill_tokens)) for M in (4096, 11008)}
-    for K in (4096, 11008):
-        gh.check(L.ggml_hip_reserve_workspace(K, max(1, args.prefill_tokens)))
+    for K, M in ((4096, 11008), (11008, 4096)):     # prefill: the GEMM's per-call weight image of M rows
+        gh.check(L.ggml_hip_reserve_workspace_mm(K, max(1, args.prefill_tokens), M))
     gh.synchronize()
 
     batch = not args.no_batch_siblings
@@ -513,20 +513,39 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0,
     def run():
         for n, wp, mp, K, yp in calls:
             gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, N, yp, stream))
-    run()
-    gh.check(L.ggml_hip_stream_synchronize(stream))
-    a, b = gh.Event(), gh.Event()
-    a.record(stream)
-    for _ in range(reps):
+
+    def timed():
         run()
-    b.record(stream)
-    t = a.elapsed_ms(b) * 1e-3 / reps
+        gh.check(L.ggml_hip_stream_synchronize(stream))
+        a, b = gh.Event(), gh.Event()
+        a.record(stream)
+        for _ in range(reps):
+            run()
+        b.record(stream)
+        return a.elapsed_ms(b) * 1e-3 / reps
+
     nbytes = sum(q4_bytes(K, m) + 4 * K * N + 4 * m * N for _, K, M, m, _, _ in mats)
     ops = sum(2 * K * m * N for _, K, M, m, _, _ in mats)
+    # default path: each weight's int8 image built once, as the hook does on a resident weight's first
+    # prefill (ggml_hip_weight_image_create; DESIGN.md §4 k_gemm8), then k_gemm8 per call
+    for _, K, M, m, buf, _ in mats:
+        gh.check(L.ggml_hip_weight_image_create(buf.ptr, K, m, stream))
+    image_bytes = L.ggml_hip_weight_image_bytes()
+    try:
+        t = timed()
+    finally:
+        for _, K, M, m, buf, _ in mats:
+            L.ggml_hip_weight_image_free(buf.ptr)
+    t7 = timed()                                      # no images: k_gemm7 on the q4_0 bytes in place
     return {"tokens": N, "layers": layers, "ms_per_layer": round(t / layers * 1e3, 4),
             "GBps": round(nbytes / t / 1e9, 1), "TOPs": round(ops / t / 1e12, 1),
             "mfma_frac": round(ops / t / 1e12 / INT8_PEAK_TOPS, 4), "peak_TOPs": INT8_PEAK_TOPS,
-            "stack_7B_prefill_ms": round(t / layers * 32 * 1e3, 3)}
+            "stack_7B_prefill_ms": round(t / layers * 32 * 1e3, 3),
+            "kernel": "k_gemm8_q4_0 on per-weight int8 images built once (34 B per 32 weights; image bytes "
+                      f"{image_bytes} for {layers} layers)",
+            "q4_0_in_place": {"kernel": "k_gemm7_q4_0 (no image: the q4_0 blocks read in place)",
+                              "ms_per_layer": round(t7 / layers * 1e3, 4), "TOPs": round(ops / t7 / 1e12, 1),
+                              "mfma_frac": round(ops / t7 / 1e12 / INT8_PEAK_TOPS, 4)}}
 
 
 def _cpu_name():

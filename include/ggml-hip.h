@@ -160,6 +160,24 @@ int ggml_hip_get_exact(void);
 /* Ensure the current device's workspace can serve mul_mat for N tokens of K (call before
  * capturing a HIP graph). */
 int ggml_hip_reserve_workspace(int64_t K, int64_t N);
+/* The same for prefill mul_mats (N > 128) of matrices up to M rows: the LDS GEMM also keeps a per-call
+ * int8 image of the weights in the workspace (34 bytes per 32 weights). */
+int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M);
+
+/* Prefill weight images (no ggml-cuda.h counterpart).  The LDS GEMM (N > 128) runs fastest on an int8
+ * image of the weight (w = nibble - 8, fp16 d verbatim; 34 B per 32 weights, 1.9x the q4_0 bytes):
+ * create builds it once (stream-ordered, outside capture) and every later prefill mul_mat of that device
+ * pointer with the same K, M uses it; without one the GEMM reads the q4_0 bytes directly.  The weight
+ * must not change while its image exists (free it first).  Device-resident ggml weights
+ * (transform_tensor, the residency cache) get their image on their first prefill use, dropped with the
+ * buffer.  Results are identical either way in exact arithmetic per block; the fp32 accumulation order
+ * of the two GEMMs differs (both within the parity bound). */
+int ggml_hip_weight_image_create(const void *dev_w, int64_t K, int64_t M, void *stream);
+int ggml_hip_weight_image_free(const void *dev_w);        /* number of images dropped */
+int64_t ggml_hip_weight_image_bytes(void);                  /* device bytes held by images */
+/* test hook: prefill GEMM version 7 (q4_0 bytes), 8 (image when registered, default), 9 (image always,
+ * built per call into the workspace when unregistered); -1 = GGML_HIP_GEMM_V */
+int ggml_hip_debug_set_gemm_version(int v);
 
 /* ------------------------------------------------------------------------------------------
  * Decode chains: a sequence of dependent N = 1 q4_0 mul_mats as ONE persistent launch.

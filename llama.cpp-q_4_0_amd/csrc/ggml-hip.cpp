@@ -26,6 +26,7 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <map>
 #include <unordered_map>
 #include <vector>
 
@@ -200,6 +201,88 @@ size_t ws_d16_offset(int64_t K, int64_t N) {
     return qs + (((size_t)N * (K / QK) * 4 + 255) & ~(size_t)255);
 }
 size_t workspace_bytes(int64_t K, int64_t N) { return ws_d16_offset(K, N) + (size_t)((N + 3) & ~3) * (K / QK) * 2; }
+// the LDS GEMM (algo 2, v8) adds its x image and the per-call int8 weight image of an M-row matrix
+size_t ws_g8x_offset(int64_t K, int64_t N) { return (workspace_bytes(K, N) + 255) & ~(size_t)255; }
+size_t ws_g8w_offset(int64_t K, int64_t N) { return (ws_g8x_offset(K, N) + ghip::gemm8_x_bytes(K, N) + 255) & ~(size_t)255; }
+size_t workspace_bytes_mm(int64_t K, int64_t N, int64_t M) { return ws_g8w_offset(K, N) + ghip::gemm8_w_bytes(K, M); }
+// prefill GEMM version (GGML_HIP_GEMM_V / ggml_hip_debug_set_gemm_version): 8 (default) = k_gemm8 when
+// the weight has an int8 image (ggml_hip_weight_image_create, or built on first prefill use of a
+// device-resident ggml weight), else k_gemm7 on the q4_0 bytes; 9 = k_gemm8 always (an unregistered
+// weight is converted into the workspace per call); 7 = k_gemm7 always
+std::atomic<int> g_gemm_v{-1};
+int gemm_version() {
+    int v = g_gemm_v.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = getenv("GGML_HIP_GEMM_V");
+        int want = e ? atoi(e) : 8, expect = -1;
+        g_gemm_v.compare_exchange_strong(expect, want);
+        v = g_gemm_v.load(std::memory_order_relaxed);
+    }
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// int8 weight images for the prefill GEMM (k_gemm8): per device, keyed by the device
+// address of the q4_0 weight.  The image is w = nibble - 8 as int8 plus the fp16 d verbatim (34 B per
+// 32 weights, 1.9x the q4_0 bytes), built once by k_prep8_w; the weight must not change while an
+// image of it exists (ggml weights on the device never do; every hipFree of a weight buffer here
+// drops its images first).
+struct WImage {
+    int64_t K, M;
+    void *img;
+    size_t bytes;
+};
+std::mutex g_wi_mu;
+std::map<std::pair<int, uintptr_t>, WImage> g_wi;          // (device, weight address)
+int64_t g_wi_resident = 0;
+
+const void *wimage_find(int id, const void *w, int64_t K, int64_t M) {
+    std::lock_guard<std::mutex> lk(g_wi_mu);
+    auto it = g_wi.find({id, (uintptr_t)w});
+    return it != g_wi.end() && it->second.K == K && it->second.M == M ? it->second.img : nullptr;
+}
+
+// build (stream-ordered on s) unless present; returns the image or nullptr on failure
+const void *wimage_ensure(int id, const void *w, int64_t K, int64_t M, hipStream_t s) {
+    if (const void *p = wimage_find(id, w, K, M)) return p;
+    std::lock_guard<std::mutex> lk(g_wi_mu);
+    auto it = g_wi.find({id, (uintptr_t)w});
+    if (it != g_wi.end()) {                                  // same address, other shape: rebuild
+        if (GHIP_SYNC(hipFree)(it->second.img) != hipSuccess) return nullptr;
+        g_wi_resident -= (int64_t)it->second.bytes;
+        g_wi.erase(it);
+    }
+    WImage im{K, M, nullptr, ghip::gemm8_w_bytes(K, M)};
+    if (hipMalloc(&im.img, im.bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (ghip::gemm8_prep_w(w, K, M, im.img, s) != hipSuccess) {
+        (void)GHIP_SYNC(hipFree)(im.img);
+        return nullptr;
+    }
+    g_wi[{id, (uintptr_t)w}] = im;
+    g_wi_resident += (int64_t)im.bytes;
+    return im.img;
+}
+
+// drop the images of every weight that starts in [dev, dev + bytes) on any device (bytes == 0: at dev)
+int64_t wimage_drop(const void *dev, size_t bytes) {
+    const uintptr_t lo = (uintptr_t)dev, hi = lo + (bytes ? bytes : 1);
+    std::lock_guard<std::mutex> lk(g_wi_mu);
+    int64_t n = 0;
+    for (auto it = g_wi.begin(); it != g_wi.end();) {
+        if (it->first.second >= lo && it->first.second < hi) {
+            HIP_FATAL(GHIP_SYNC(hipFree)(it->second.img));   // waits for kernels still reading it
+            g_wi_resident -= (int64_t)it->second.bytes;
+            it = g_wi.erase(it);
+            n++;
+        } else {
+            ++it;
+        }
+    }
+    return n;
+}
 
 int reserve_workspace(int id, size_t bytes, hipStream_t s = nullptr) {
     Device &d = g_dev[id];
@@ -359,6 +442,7 @@ const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, ui
     }
     g_wc_misses++;
     if (it != g_wc.end()) {                                        // stale: same address, new bytes
+        wimage_drop(it->second.dev, it->second.bytes);
         HIP_FATAL(GHIP_SYNC(hipFree)(it->second.dev));
         g_wc_resident -= it->second.bytes;
         g_wc.erase(it);
@@ -369,6 +453,7 @@ const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, ui
             if (e->second.last_use != call_id && (victim == g_wc.end() || e->second.last_use < victim->second.last_use))
                 victim = e;
         if (victim == g_wc.end()) break;                           // everything is in use: over budget
+        wimage_drop(victim->second.dev, victim->second.bytes);
         HIP_FATAL(GHIP_SYNC(hipFree)(victim->second.dev));
         g_wc_resident -= victim->second.bytes;
         g_wc.erase(victim);
@@ -396,6 +481,7 @@ int64_t wcache_invalidate(const void *host, size_t bytes) {
     for (auto it = g_wc.begin(); it != g_wc.end();) {
         const uintptr_t a = (uintptr_t)it->first.host, b = a + it->first.bytes;
         if (a < hi && lo < b) {
+            wimage_drop(it->second.dev, it->second.bytes);
             HIP_FATAL(GHIP_SYNC(hipFree)(it->second.dev));   // hipFree waits for work that still reads it
             g_wc_resident -= it->second.bytes;
             it = g_wc.erase(it);
@@ -436,10 +522,14 @@ bool exact_mode() {
     return v == 1;
 }
 
-// x_quantized: the workspace already holds q8_0(x) from the previous call on this stream (siblings
-// that share x: ggml_hip_mul_mat_q4_0_multi quantizes once); ignored by the fused GEMV
+// xq: in/out mask of the q8_0(x) forms already in this stream's workspace from the previous call
+// (siblings that share x: ggml_hip_mul_mat_q4_0_multi quantizes once per form): XQ_SOA = qs + d (split-K,
+// exact, gemm7), XQ_G8 = the k_gemm8 x image; null = quantize; ignored by the fused GEMV
+enum { XQ_SOA = 1, XQ_G8 = 2 };
 int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, float *y, int64_t ldy, int algo,
-                hipStream_t s, bool x_quantized = false) {
+                hipStream_t s, unsigned *xq = nullptr) {
+    unsigned xq_local = 0;
+    if (!xq) xq = &xq_local;
     if (!w || !x || !y || K <= 0 || M <= 0 || N < 0) return fail(GGML_HIP_ERR_INVALID, "null pointer or bad shape");
     if (N == 0) return GGML_HIP_OK;
     if (K % 64 != 0) return fail(GGML_HIP_ERR_INVALID, "K must be a multiple of 64 (ggml.c:2344 nb % 2 == 0)");
@@ -460,12 +550,30 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
     }
     if (algo < 2 || algo > 4) return fail(GGML_HIP_ERR_INVALID, "algo must be 0, 1, 2, 3 or 4");
     void *ws = nullptr;
+    const int gv = gemm_version();
+    const void *wimg = algo == 2 && gv >= 8 ? wimage_find(id, w, K, M) : nullptr;
+    if (algo == 2 && (wimg || gv == 9)) {      // k_gemm8: x image + int8 weight image
+        const int wrc = stream_workspace(id, s, workspace_bytes_mm(K, N, wimg ? 0 : M), &ws);
+        if (wrc != GGML_HIP_OK) return wrc;
+        void *xws = (char *)ws + ws_g8x_offset(K, N);
+        if (!(*xq & XQ_G8)) HIP_RET(ghip::gemm8_prep_x(x, K, N, xws, s));
+        *xq |= XQ_G8;
+        if (!wimg) {                            // unregistered weight: converted per call
+            void *wws = (char *)ws + ws_g8w_offset(K, N);
+            HIP_RET(ghip::gemm8_prep_w(w, K, M, wws, s));
+            wimg = wws;
+        }
+        HIP_RET(ghip::gemm8_run(wimg, K, M, xws, N, y, ldy, s));
+        return GGML_HIP_OK;
+    }
     const int wrc = stream_workspace(id, s, workspace_bytes(K, N), &ws);
     if (wrc != GGML_HIP_OK) return wrc;
     int8_t *qs = (int8_t *)ws;
     float *xd = (float *)((char *)ws + ((size_t)(N * K + 255) & ~(size_t)255));
     uint16_t *xd16 = (uint16_t *)((char *)ws + ws_d16_offset(K, N));
-    if (!x_quantized) HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s, algo == 2 ? xd16 : nullptr));
+    // the fp16 block-major d_x copy (gemm7) is written whenever qs/d are: a sibling group may mix algos
+    if (!(*xq & XQ_SOA)) HIP_RET(ghip::quantize_q8_0_soa(x, K, N, qs, xd, s, xd16));
+    *xq |= XQ_SOA;
     if (algo == 4)
         HIP_RET(ghip::mm_exact_q4_0(w, K, M, qs, xd, N, y, ldy, s));
     else if (algo == 3)
@@ -1771,6 +1879,7 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
             // weights: resident slice, or upload the row slice (the reference re-uploads every
             // call too, ggml-cuda.cu:2496-2502)
             const void *w;
+            bool w_resident = true;                // device weight or cached copy: may get an int8 image
             if (src0_dev) {
                 const auto *ex = (const ggml_tensor_extra_gpu *)src0->extra;
                 w = (const char *)ex->data_device[id] + (size_t)b * rows * wrow;
@@ -1782,7 +1891,11 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
                 HIP_FATAL(GHIP_SYNC(hipMemcpyAsync)(p, (const char *)src0->data + (size_t)b * src0->nb[2] + lo * wrow, rows * wrow,
                                          hipMemcpyHostToDevice, s));
                 w = p;
+                w_resident = false;
             }
+            // prefill (the LDS GEMM, N > 128) of a resident weight: build its int8 image once (k_gemm8;
+            // a failure to allocate it leaves k_gemm7 on the q4_0 bytes)
+            if (w_resident && N > 128 && !exact_mode() && gemm_version() == 8) (void)wimage_ensure(id, w, K, rows, s);
             // activations
             const float *x;
             const size_t xbytes = (size_t)N * K * 4;
@@ -1964,6 +2077,8 @@ void ggml_hip_free_data(struct ggml_tensor *tensor_) {
     for (int id = 0; id < g_device_count; id++) {
         if (!extra->data_device[id] || !release_device_buffer(extra->data_device[id])) continue;
         HIP_FATAL(hipSetDevice(id));
+        // int8 prefill images of this weight (any batch slice; the whole tensor's bytes bound them)
+        wimage_drop(extra->data_device[id], (size_t)t->nb[3] * (size_t)t->ne[3]);
         HIP_FATAL(GHIP_SYNC(hipFree)(extra->data_device[id]));
     }
     HIP_FATAL(hipSetDevice(saved));
@@ -2176,8 +2291,18 @@ int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *
         return GGML_HIP_OK;
     }
     if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30) || exact_mode()) {
+        if (N > 128 && !exact_mode() && dev_x && K > 0 && K % 64 == 0) {
+            // the v8 GEMM's weight image grows with M: size the workspace for the largest sibling
+            // first, so that a later sibling cannot reallocate it under the shared x image
+            int64_t mmax = 0;
+            for (int i = 0; i < n; i++) mmax = std::max(mmax, M[i]);
+            void *ws = nullptr;
+            const int wrc = stream_workspace(current_device(), s, workspace_bytes_mm(K, N, mmax), &ws);
+            if (wrc != GGML_HIP_OK) return wrc;
+        }
+        unsigned xq = 0;
         for (int i = 0; i < n; i++) {       // GEMM / exact path: x quantized once, one launch per matrix
-            int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 0, s, i > 0);
+            int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 0, s, &xq);
             if (rc != GGML_HIP_OK) return rc;
         }
         return GGML_HIP_OK;
@@ -2203,6 +2328,47 @@ int ggml_hip_reserve_workspace(int64_t K, int64_t N) {
     ensure_init();
     if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
     return reserve_workspace(current_device(), workspace_bytes(K, N));
+}
+
+int ggml_hip_weight_image_create(const void *dev_w, int64_t K, int64_t M, void *stream) {
+    ensure_init();
+    if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
+    if (!dev_w || K <= 0 || K % 64 != 0 || M <= 0 || !aligned(dev_w, 16))
+        return fail(GGML_HIP_ERR_INVALID, "bad weight pointer or shape (K % 64 == 0, 16-byte aligned)");
+    if (M * (K / QK) * Q4B >= ((int64_t)1 << 31) || (K / QK) * 2048 >= ((int64_t)1 << 31))
+        return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large");
+    hipStream_t s = resolve_stream(stream);
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
+        return fail(GGML_HIP_ERR_INVALID, "weight images are built outside stream capture");
+    ghip::rec_flush_at("weight image");
+    if (!wimage_ensure(current_device(), dev_w, K, M, s)) return fail(GGML_HIP_ERR_NOMEM, "weight image allocation failed");
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_weight_image_free(const void *dev_w) {
+    ensure_init();
+    ghip::rec_flush_at("weight image");
+    return (int)wimage_drop(dev_w, 0);
+}
+
+int64_t ggml_hip_weight_image_bytes(void) {
+    std::lock_guard<std::mutex> lk(g_wi_mu);
+    return g_wi_resident;
+}
+
+int ggml_hip_debug_set_gemm_version(int v) {
+    if (v != -1 && v != 7 && v != 8 && v != 9) return fail(GGML_HIP_ERR_INVALID, "version must be 7, 8, 9 or -1");
+    g_gemm_v.store(v, std::memory_order_relaxed);
+    if (v == -1) (void)gemm_version();            // re-read GGML_HIP_GEMM_V
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M) {
+    ensure_init();
+    if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
+    if (K <= 0 || N < 0 || M < 0) return fail(GGML_HIP_ERR_INVALID, "bad shape");
+    return reserve_workspace(current_device(), workspace_bytes_mm(K, N, M));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2734,7 +2900,10 @@ int ggml_hip_weight_cache_clear(void) {
         HIP_RET(hipSetDevice(id));
         HIP_RET(GHIP_SYNC(hipStreamSynchronize)(g_dev[id].stream));
     }
-    for (auto &e : g_wc) HIP_RET(GHIP_SYNC(hipFree)(e.second.dev));
+    for (auto &e : g_wc) {
+        wimage_drop(e.second.dev, e.second.bytes);
+        HIP_RET(GHIP_SYNC(hipFree)(e.second.dev));
+    }
     g_wc.clear();
     g_wc_resident = 0;
     g_wc_hits = g_wc_misses = g_wc_invalidations = 0;

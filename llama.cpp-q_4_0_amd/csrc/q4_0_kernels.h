@@ -75,6 +75,17 @@ hipError_t gemm_read_stamps(unsigned long long *host, int n);
 hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd,
                      int64_t N, float *y, int64_t ldy, hipStream_t s, const uint16_t *xd16);
 
+// Prefill GEMM v8 (default for the LDS GEMM path): x as a block-major int8 image + fp16 d_x
+// (gemm8_prep_x, bit-exact q8_0 values), the q4_0 weights converted per call into an int8 image
+// (w = nibble - 8, fp16 d verbatim) in the workspace wws, then the MFMA GEMM over both images.
+int64_t gemm8_np(int64_t N);
+size_t gemm8_x_bytes(int64_t K, int64_t N);       // x image + d_x
+size_t gemm8_w_bytes(int64_t K, int64_t M);       // weight image + d_w
+hipError_t gemm8_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStream_t s);
+hipError_t gemm8_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStream_t s);
+hipError_t gemm8_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
+                     hipStream_t s);
+
 // Small / medium N (split-K over the waves of a 32x32-tile workgroup, operands straight to registers).
 hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,
                         float *y, int64_t ldy, int num_cus, hipStream_t s);

@@ -1768,6 +1768,335 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
 }
 
 // ---------------------------------------------------------------------------------------------
+// Prefill GEMM, round 3 (`k_gemm8_q4_0`, default for N > 128): int8-operand images DMA'd straight
+// into LDS, two 32x32 output tiles per wave, the K range of every LDS stage split between the two
+// halves of the workgroup.
+//
+// Why (tools/gemm_mb.hip, the compute phase alone with operands in LDS): per 32x32
+// tile and q4_0 block the exact formulation issues an i8 MFMA, the f16 rank-1 scale MFMA and 32
+// dependent VALU (acc += (S - bias) * P); on gfx950 that VALU does not overlap its own MFMAs, so the
+// loop runs near the SUM of the two streams.  Two tiles per wave sharing the weight operand, with the
+// scale operands carried across blocks (no per-block v_and / v_mov rebuild), is the fastest compute
+// structure measured (~175 vs ~245 cycles per tile-block at two waves per SIMD for gemm7's one tile
+// per wave).  M = 4096, N = 512 has only 2048 output tiles, i.e. one 2-tile wave per SIMD; the two
+// workgroup halves therefore split each stage's four blocks (blocks 0-1 / 2-3) and add their partial
+// tiles once at the end in a fixed order (deterministic, x -> 2x bitwise).
+//
+// Operands, all by LDS-DMA (`buffer_load ... lds`, no register staging, no ds_write):
+//   weights: an int8 image of the q4_0 rows built per call by k_prep8_w (w = nibble - 8, exactly the
+//            values the q4_0 block encodes; fp16 d copied verbatim): [M/64][nb][64 rows][32 B] with
+//            the 16-byte halves of row r swapped when (r>>3)&1, so a 1 KiB DMA lands 32 rows of one
+//            block in the conflict-free operand layout, + fp16 d_w [M/64][nb][64];
+//   x:       the q8_0 int8 values block-major [nb][Np][32 B] (same half swap per token) + fp16 d_x
+//            [nb][Np] from k_prep8_x (quantize_row_q8_0 AVX2 semantics, bit-exact, as every other
+//            quantizer here).
+// Every per-block integer sum stays exact (i8 MFMA, K = 32 = one block); the fp32 accumulation per
+// output runs over the blocks in order within each workgroup half, the halves added at the end.
+// Reference: ggml.c:11304-11351 (mul_mat_q_f32), ggml-cuda.cu:2143-2182 (dequantize + GEMM).
+static constexpr int G8_BM = 64, G8_BN = 128, G8_KB = 8, G8_NS = 3, G8_LOADERS = 4;
+static constexpr int G8_THREADS = (8 + G8_LOADERS) * 64;            // 8 compute waves + 4 loader waves
+static constexpr int G8_W = G8_KB * G8_BM * 32;                  // int8 weights [KB][BM][32]  16 KB
+static constexpr int G8_X = G8_KB * G8_BN * 32;                  // int8 x       [KB][BN][32]  32 KB
+static constexpr int G8_WD = G8_KB * G8_BM * 2;                  // fp16 d_w     [KB][BM]        1 KB
+static constexpr int G8_XD = G8_KB * G8_BN * 2;                  // fp16 d_x     [KB][BN]        2 KB
+static constexpr int G8_STAGE = G8_W + G8_X + G8_WD + G8_XD;     // 51 KB
+static constexpr int G8_ZERO = 256;                               // zeros: the upper half-wave's d_w
+static constexpr int G8_LDS = G8_NS * G8_STAGE + G8_ZERO;        // 153.25 KB
+static constexpr int G8_OPS = 15;                                 // DMA instructions per loader wave per stage
+static_assert(G8_W / 1024 == 4 * G8_LOADERS && G8_X / 1024 == 8 * G8_LOADERS, "loader l moves blocks 2l, 2l+1");
+static_assert(4 * 2 * 16 * 64 * 4 <= G8_NS * G8_STAGE, "the partial-tile exchange fits in the ring");
+
+// x: one lane per 4 floats (8 lanes per block, k_quantize_q8_0's lane code), written block-major.
+__global__ __launch_bounds__(256) void k_prep8_x(const float *__restrict__ x, int64_t K, int64_t total8,
+                                                  int8_t *__restrict__ ximg, uint16_t *__restrict__ xd16, int64_t Np) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total8) return;
+    const int64_t nb = K / QK;
+    const int64_t blk = t >> 3, n = blk / nb, b = blk - n * nb;
+    const int sub = (int)(t & 7);
+    const float4 v = *reinterpret_cast<const float4 *>(x + t * 4);
+    uint32_t d16;
+    int qsum;
+    const uint32_t packed = q8_block_lane(v, d16, qsum);
+    const int phys = (sub >> 2) ^ (int)((n >> 3) & 1);            // 16-byte half, swapped per 8 tokens
+    reinterpret_cast<uint32_t *>(ximg)[((b * Np + n) * 32 + 16 * phys + 4 * (sub & 3)) >> 2] = packed;
+    if (sub == 0) xd16[b * Np + n] = (uint16_t)d16;
+}
+
+// weights: one lane per (row, block pair); a wave = 64 consecutive rows of one pair (coalesced 2 KiB
+// image stores per block).  Rows >= M of the last tile are written as zeros (d = 0).
+__global__ __launch_bounds__(256) void k_prep8_w(const uint8_t *__restrict__ W, int64_t rowbytes, int nb, int M,
+                                                  int8_t *__restrict__ wimg, uint16_t *__restrict__ wd16) {
+    const int r = threadIdx.x & 63;
+    const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);     // (row tile, pair)
+    const int npair = nb >> 1;
+    const int64_t rt = item / npair;
+    const int p = (int)(item - rt * npair);
+    const int64_t row = rt * 64 + r;
+    if (rt * 64 >= M) return;
+    u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
+    uint32_t c = 0u;
+    if (row < M) {
+        const uint8_t *src = W + row * rowbytes + (int64_t)p * 36;
+        a = *reinterpret_cast<const u32x4 *>(src);      // dword-aligned 36-byte pair (rows are 36*nb/2 B)
+        b = *reinterpret_cast<const u32x4 *>(src + 16);
+        c = *reinterpret_cast<const uint32_t *>(src + 32);
+    }
+    // block 2p: d = a.x[15:0], qs = bytes 2..17; block 2p+1: d = b.x[31:16], qs = b.y..c
+    const uint32_t e[4] = {__builtin_amdgcn_alignbyte(a.y, a.x, 2), __builtin_amdgcn_alignbyte(a.z, a.y, 2),
+                           __builtin_amdgcn_alignbyte(a.w, a.z, 2), __builtin_amdgcn_alignbyte(b.x, a.w, 2)};
+    const uint32_t o[4] = {b.y, b.z, b.w, c};
+    const int sw = (r >> 3) & 1;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const uint32_t *q = k ? o : e;
+        u32x4 lo, hi;                                    // elements 0..15 (low nibbles), 16..31 (high)
+        lo.x = nib_to_i8x4(q[0], 0); lo.y = nib_to_i8x4(q[1], 0); lo.z = nib_to_i8x4(q[2], 0); lo.w = nib_to_i8x4(q[3], 0);
+        hi.x = nib_to_i8x4(q[0], 4); hi.y = nib_to_i8x4(q[1], 4); hi.z = nib_to_i8x4(q[2], 4); hi.w = nib_to_i8x4(q[3], 4);
+        if (row >= M) lo = hi = u32x4{0u, 0u, 0u, 0u};
+        const int64_t blk = rt * nb + 2 * p + k;
+        u32x4 *dst = reinterpret_cast<u32x4 *>(wimg + (blk * 64 + r) * 32);
+        dst[sw] = lo;
+        dst[sw ^ 1] = hi;
+        const uint32_t d = k ? (b.x >> 16) : (a.x & 0xFFFFu);
+        wd16[blk * 64 + r] = (uint16_t)(row < M ? d : 0u);
+    }
+}
+
+// DIAG (timing knockouts, results invalid): 1 no compute (DMA ring + barriers only), 2 no DMA
+// VAR bits (A/B knobs, all bitwise-identical results): 1 the i8 MFMA accumulates on 0 and the
+// epilogue converts with v_cvt_f32_i32 (no 16-register bias operand to keep live or rebuild); 2 the
+// next block's operands are read from LDS while the current block computes
+template <int DIAG, int VAR = 0>
+__global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__restrict__ wimg,
+                                                               const uint16_t *__restrict__ wd16, int nb, int M,
+                                                               const int8_t *__restrict__ ximg,
+                                                               const uint16_t *__restrict__ xd16, int64_t Np, int N,
+                                                               float *__restrict__ y, int64_t ldy) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *zero = smem + G8_NS * G8_STAGE;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 31, h = lane >> 5;
+    const int rt = blockIdx.x;
+    const int m0 = rt * G8_BM, n0 = blockIdx.y * G8_BN;
+    if (tid < G8_ZERO / 4) reinterpret_cast<uint32_t *>(zero)[tid] = 0u;   // ordered by the first barrier
+
+    // descriptors: this row tile's slice of the weight image, the whole x image
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(wimg + (int64_t)rt * nb * 2048, (uint32_t)nb * 2048u);
+    const __amdgpu_buffer_rsrc_t wdrs = make_rsrc(wd16 + (int64_t)rt * nb * 64, (uint32_t)nb * 128u);
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(ximg, (uint32_t)((int64_t)nb * Np * 32));
+    const __amdgpu_buffer_rsrc_t xdrs = make_rsrc(xd16, (uint32_t)((int64_t)nb * Np * 2));
+    const __amdgpu_buffer_rsrc_t nul = make_rsrc(wimg, 0);
+
+    // DMA roles: loader wave l = wave - 8 moves blocks 2l, 2l+1 of every stage: weights (2 x 1 KiB
+    // each), x (4 x 1 KiB each), d_x (256 B each), d_w (both blocks in one 256-B instruction) = 15
+    // instructions; the compute waves issue none (an LDS-DMA costs its issuing wave 60-185 cycles,
+    // MI355X_MICROARCH.md cycle constants, which measured as unhidden time in the compute waves)
+    const int lw = wave - 8;
+    const int lb = 2 * lw;                                                         // first block
+    auto issue = [&](int st) __attribute__((always_inline)) {
+        if (DIAG == 2 || wave < 8) return;
+        uint8_t *base = smem + (st % G8_NS) * G8_STAGE;
+        const int kb0 = st * G8_KB;
+        const bool v = kb0 + lb < nb;                                             // nb even: both or none
+        const __amdgpu_buffer_rsrc_t wr_ = v ? wrs : nul, xr_ = v ? xrs : nul, dr_ = v ? xdrs : nul,
+                                     wdr_ = v ? wdrs : nul;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int b = lb + j;
+#pragma unroll
+            for (int r = 0; r < 2; r++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wr_, (lds_void_t *)(base + b * 2048 + r * 1024), 16,
+                                                         (kb0 + b) * 2048 + r * 1024 + lane * 16, 0, 0, 0);
+            const int xs = (int)(((int64_t)(kb0 + b) * Np + n0) * 32) + lane * 16;
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xr_, (lds_void_t *)(base + G8_W + b * 4096 + r * 1024), 16,
+                                                         xs + r * 1024, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dr_, (lds_void_t *)(base + G8_W + G8_X + G8_WD + b * 256), 4,
+                                                     (int)(((int64_t)(kb0 + b) * Np + n0) * 2) + lane * 4, 0, 0, 0);
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wdr_, (lds_void_t *)(base + G8_W + G8_X + lb * 128), 4,
+                                                 (kb0 + lb) * 128 + lane * 4, 0, 0, 0);
+    };
+
+    // compute roles: workgroup half g takes blocks 4g .. 4g+3 of every stage; wave q of the half owns
+    // weight rows 32*(q&1)..+31 and token tiles 64*(q>>1) + {0, 32}
+    const int g = (wave >> 2) & 1, q = wave & 3;          // (loader waves: unused)
+    const int wrow = 32 * (q & 1) + c;
+    const int t0 = 64 * (q >> 1) + c, t1 = t0 + 32;
+    const int hw = 16 * (h ^ ((wrow >> 3) & 1));
+    const int h0 = 16 * (h ^ ((t0 >> 3) & 1)), h1 = 16 * (h ^ ((t1 >> 3) & 1));
+    constexpr bool CVT = VAR & 1, PF = VAR & 2;
+    const int mg = CVT ? 0 : 0x4B400000;
+    const i32x16 im = {mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg};
+    const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    float acc0[16], acc1[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc0[i] = acc1[i] = 0.0f;
+    i32x16 S0 = im, S1 = im;
+    f32x16 P0 = fz, P1 = fz;
+    // scale operands, carried: only element 0 (k = 0 / k = 8) is rewritten per block; the upper
+    // half-wave's d_w comes from the zero region, so P = d_x * d_w exactly
+    u32x4 as0 = {0u, 0u, 0u, 0u}, as1 = {0u, 0u, 0u, 0u}, bs = {0u, 0u, 0u, 0u};
+    auto epi = [&](float *a, const i32x16 &S, const f32x16 &P) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            a[i] = fmaf(CVT ? (float)S[i] : __int_as_float(S[i]) - 12582912.0f, P[i], a[i]);
+    };
+    struct Ops {
+        i32x4 bw, a0, a1;
+        uint32_t sw, sx0, sx1;
+    };
+    auto rd = [&](int st, int b) __attribute__((always_inline)) {
+        const uint8_t *base = smem + (st % G8_NS) * G8_STAGE;
+        Ops o;
+        o.bw = *reinterpret_cast<const i32x4 *>(base + b * 2048 + wrow * 32 + hw);
+        o.a0 = *reinterpret_cast<const i32x4 *>(base + G8_W + b * 4096 + t0 * 32 + h0);
+        o.a1 = *reinterpret_cast<const i32x4 *>(base + G8_W + b * 4096 + t1 * 32 + h1);
+        o.sw = *reinterpret_cast<const uint16_t *>((h ? zero : base + G8_W + G8_X + b * 128) + wrow * 2);
+        const uint16_t *xd = reinterpret_cast<const uint16_t *>(base + G8_W + G8_X + G8_WD + b * 256);
+        o.sx0 = xd[t0];
+        o.sx1 = xd[t1];
+        return o;
+    };
+    auto block = [&](const Ops &o) __attribute__((always_inline)) {
+        bs.x = o.sw;
+        as0.x = o.sx0;
+        as1.x = o.sx1;
+        S0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a0, o.bw, im, 0, 0, 0);
+        P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as0), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+        epi(acc1, S1, P1);                     // tile 1 of the previous block (S1 = bias, P1 = 0 at first)
+        S1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a1, o.bw, im, 0, 0, 0);
+        P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as1), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+        epi(acc0, S0, P0);
+    };
+    auto sync = [&]() __attribute__((always_inline)) {   // retire stage s+1, keep s+2 in flight
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((G8_NS - 2) * G8_OPS) : "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+
+    const int nstages = (nb + G8_KB - 1) / G8_KB;
+#pragma unroll
+    for (int st = 0; st < G8_NS - 1; st++) issue(st);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((G8_NS - 2) * G8_OPS) : "memory");   // stage 0 landed
+    __builtin_amdgcn_s_barrier();
+    for (int s = 0; s < nstages; s++) {
+        issue(s + G8_NS - 1);
+        const int kb = s * G8_KB + 4 * g;
+        if (DIAG != 1 && wave < 8) {
+            if (PF) {                              // nb is even and kb too: blocks come in valid pairs
+                Ops o = rd(s, 4 * g);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (kb + j >= nb) break;
+                    Ops n = o;
+                    if (j < 3) n = rd(s, 4 * g + j + 1);
+                    block(o);
+                    o = n;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (kb + j < nb) block(rd(s, 4 * g + j));
+            }
+        }
+        sync();
+    }
+    epi(acc1, S1, P1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may outlive the ring
+    __syncthreads();
+    // the halves' partial tiles: half 1 -> LDS, half 0 adds (acc_half0 + acc_half1, fixed order)
+    float *red = reinterpret_cast<float *>(smem);
+    if (wave >= 4 && wave < 8) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+            *reinterpret_cast<float4 *>(red + ((i / 4) * 256 + q * 64 + lane) * 4) = {acc0[i], acc0[i + 1], acc0[i + 2], acc0[i + 3]};
+            *reinterpret_cast<float4 *>(red + ((4 + i / 4) * 256 + q * 64 + lane) * 4) = {acc1[i], acc1[i + 1], acc1[i + 2], acc1[i + 3]};
+        }
+    }
+    __syncthreads();
+    if (wave < 4) {
+        const int row = m0 + wrow;
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+            const float4 o0 = *reinterpret_cast<const float4 *>(red + ((i / 4) * 256 + q * 64 + lane) * 4);
+            const float4 o1 = *reinterpret_cast<const float4 *>(red + ((4 + i / 4) * 256 + q * 64 + lane) * 4);
+            acc0[i] += o0.x; acc0[i + 1] += o0.y; acc0[i + 2] += o0.z; acc0[i + 3] += o0.w;
+            acc1[i] += o1.x; acc1[i + 1] += o1.y; acc1[i + 2] += o1.z; acc1[i + 3] += o1.w;
+        }
+        if (row < M) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int tk = n0 + 64 * (q >> 1) + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (tk < N) y[(int64_t)tk * ldy + row] = acc0[i];
+                if (tk + 32 < N) y[(int64_t)(tk + 32) * ldy + row] = acc1[i];
+            }
+        }
+    }
+}
+
+int64_t gemm8_np(int64_t N) { return (N + 3) & ~(int64_t)3; }
+size_t gemm8_x_bytes(int64_t K, int64_t N) { return (size_t)(K / QK) * gemm8_np(N) * 34; }
+size_t gemm8_w_bytes(int64_t K, int64_t M) { return (size_t)((M + 63) / 64) * (K / QK) * 64 * 34; }
+
+hipError_t gemm8_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStream_t s) {
+    const int64_t total8 = N * (K / QK) * 8;
+    if (total8 == 0) return hipSuccess;
+    const int64_t Np = gemm8_np(N);
+    int8_t *ximg = (int8_t *)xws;
+    uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)(K / QK) * Np * 32);
+    (void)hipGetLastError();
+    launch_k(k_prep8_x, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, s, x, K, total8, ximg, xd16, Np);
+    return hipGetLastError();
+}
+
+hipError_t gemm8_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStream_t s) {
+    const int nb = (int)(K / QK);
+    const int64_t Mt = (M + 63) / 64;
+    int8_t *wimg = (int8_t *)wws;
+    uint16_t *wd16 = (uint16_t *)((char *)wws + (size_t)Mt * nb * 2048);
+    (void)hipGetLastError();
+    const int64_t items = Mt * (nb / 2);                  // (row tile, pair) items, 4 per 256-thread block
+    launch_k(k_prep8_w, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, (const uint8_t *)W, (int64_t)nb * Q4B, nb,
+             (int)M, wimg, wd16);
+    return hipGetLastError();
+}
+
+hipError_t gemm8_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
+                     hipStream_t s) {
+    const int nb = (int)(K / QK);
+    const int64_t Mt = (M + 63) / 64, Np = gemm8_np(N);
+    const int8_t *wimg = (const int8_t *)wws;
+    const uint16_t *wd16 = (const uint16_t *)((const char *)wws + (size_t)Mt * nb * 2048);
+    const int8_t *ximg = (const int8_t *)xws;
+    const uint16_t *xd16 = (const uint16_t *)((const char *)xws + (size_t)nb * Np * 32);
+    if ((int64_t)nb * Np * 32 >= ((int64_t)1 << 31) || (int64_t)nb * 2048 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        for (auto k : {k_gemm8_q4_0<0, 0>, k_gemm8_q4_0<0, 1>, k_gemm8_q4_0<0, 2>, k_gemm8_q4_0<0, 3>,
+                       k_gemm8_q4_0<1, 3>, k_gemm8_q4_0<2, 3>}) {
+            hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS);
+            if (e != hipSuccess) return e;
+        }
+        attr = true;
+    }
+    // GGML_HIP_GEMM8_VAR (A/B, tools/r3_g8var.sh): 3 = cvt epilogue + operand prefetch (default,
+    // 33.3 -> 29.7 us at 4096x4096x512); GGML_HIP_GEMM_DIAG 81 / 82 = DMA-only / compute-only knockouts
+    static const int diag = env_int("GGML_HIP_GEMM_DIAG", 0);
+    static const int var = env_int("GGML_HIP_GEMM8_VAR", 3);
+    auto kern = diag == 81 ? k_gemm8_q4_0<1, 3> : diag == 82 ? k_gemm8_q4_0<2, 3>
+              : var == 0 ? k_gemm8_q4_0<0, 0> : var == 1 ? k_gemm8_q4_0<0, 1> : var == 2 ? k_gemm8_q4_0<0, 2>
+              : k_gemm8_q4_0<0, 3>;
+    (void)hipGetLastError();
+    launch_k(kern, dim3((unsigned)Mt, (unsigned)((N + G8_BN - 1) / G8_BN)), dim3(G8_THREADS), G8_LDS, s, wimg, wd16,
+             nb, (int)M, ximg, xd16, Np, (int)N, y, ldy);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Split-K MFMA GEMM for small / medium token counts (9 <= N <= 128 by default).
 //
 // The LDS-staged GEMM above runs (M/64) x ceil(N/128) workgroups that each walk all of K, so for

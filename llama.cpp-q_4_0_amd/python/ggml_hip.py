@@ -56,6 +56,11 @@ def _bind(L):
         "ggml_hip_mul_mat_q4_0": ([vp, i64, i64, vp, i64, vp, vp], i32),
         "ggml_hip_mul_mat_q4_0_ex": ([vp, i64, i64, vp, i64, vp, i64, i32, vp], i32),
         "ggml_hip_reserve_workspace": ([i64, i64], i32),
+        "ggml_hip_reserve_workspace_mm": ([i64, i64, i64], i32),
+        "ggml_hip_weight_image_create": ([vp, i64, i64, vp], i32),
+        "ggml_hip_weight_image_free": ([vp], i32),
+        "ggml_hip_weight_image_bytes": ([], i64),
+        "ggml_hip_debug_set_gemm_version": ([i32], i32),
         "ggml_hip_mul_mat_q4_0_multi": ([i32, vp, vp, i64, vp, i64, vp, vp], i32),
         "ggml_hip_comm_unique_id": ([vp], i32),
         "ggml_hip_comm_init": ([vp, i32, i32, vp], i32),

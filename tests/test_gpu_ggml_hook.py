@@ -83,10 +83,16 @@ def test_offloaded_weight_falcon_golden(ref):
 @pytest.mark.parametrize("K,M,N,offload", [(4096, 256, 32, 0), (4096, 512, 64, 0), (11008, 128, 48, 1),
                                            (4096, 300, 512, 1), (4544, 4672 // 8, 33, 0)])
 def test_prefill_through_ggml(ref, K, M, N, offload):
+    """Prefill through ggml's own hooks; an offloaded weight at N > 128 gets its int8 image on first use
+    (k_gemm8), released with the tensor by ggml_cuda_free_data."""
+    from hip_env import ggml_hip
+    L = ggml_hip.load()
+    before = L.ggml_hip_weight_image_bytes()
     wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED7000 + K + M, 0.0, 0.02).reshape(M, K))
     x = O.gaussian(N * K, 0x5EED7100 + N, 0.0, 1.0).reshape(N, K)
     y, _ = ggml_mul_mat(ref, wq, K, x, offload, 4)
     assert_close(wq, x, K, y, O.mul_mat(wq, K, x))
+    assert L.ggml_hip_weight_image_bytes() == before        # the driver frees the weight: image dropped
 
 
 def test_declined_node_runs_reference_cpu_op(ref):

@@ -588,3 +588,95 @@ def test_weight_cache_invalidate_and_full_verify():
     finally:
         ggml_hip.check(L.ggml_hip_weight_cache_set_verify(-1), "verify reset")
         ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+
+
+# ------------------------------------------------------------------------------- prefill GEMM v8 (int8 images)
+def _gemm_version(v):
+    ggml_hip.check(ggml_hip.load().ggml_hip_debug_set_gemm_version(v), "gemm version")
+
+
+@pytest.mark.parametrize("K,M,N", [s for s in EDGE_SHAPES if s[2] > 8] + [(4544, 4672 // 8, 130), (128, 1, 200)])
+def test_gemm8_per_call_image_vs_oracle(K, M, N):
+    """k_gemm8 with the weight converted into the workspace per call (version 9): ragged M (images padded
+    to 64 rows with d = 0), ragged N, K = 64 (one half-stage), K = 4544 (a partial last stage)."""
+    wq, x = make_case(K, M, N, seed=K * 3 + M + N)
+    _gemm_version(9)
+    try:
+        y, _ = gpu_mul_mat(wq, K, x, algo=2)
+    finally:
+        _gemm_version(-1)
+    xq = O.quantize_q8_0(x, "avx2")
+    _, s_abs = block_terms(wq, xq, K)
+    check_y(y, O.mul_mat(wq, K, x, nthreads=4), s_abs, RTOL, ATOL_BLOCKS)
+
+
+@pytest.mark.parametrize("K,M", [(4096, 4096), (11008, 4096)])
+def test_gemm8_registered_image_prefill_512(K, M):
+    """A registered int8 image (ggml_hip_weight_image_create) is used by every later prefill call of that
+    weight: bitwise equal to the per-call image, within the bound of the oracle at full LLaMA-7B shape,
+    x -> 2x bitwise; freeing the image returns the GEMM to the q4_0 bytes (k_gemm7)."""
+    L = ggml_hip.load()
+    wq, x = make_case(K, M, 512, seed=11 * K + M)
+    wd, xd = DB.from_array(wq), DB.from_array(x)
+    yd = DB(512 * M * 4)
+    before = L.ggml_hip_weight_image_bytes()
+    ggml_hip.check(L.ggml_hip_weight_image_create(wd.ptr, K, M, None), "image")
+    assert L.ggml_hip_weight_image_bytes() - before == (M + 63) // 64 * 64 * K // 32 * 34
+    try:
+        ggml_hip.mul_mat(wd, K, M, xd, 512, yd, algo=2)
+        y_img = yd.download((512, M), np.float32)
+        _gemm_version(9)
+        y_call, _ = gpu_mul_mat(wq, K, x, algo=2)
+        _gemm_version(-1)
+        assert np.array_equal(y_img.view(np.uint32), y_call.view(np.uint32))
+        xq = O.quantize_q8_0(x, "avx2")
+        y_ref = O.mul_mat(wq, K, x, nthreads=8, mode="avx2", pool=True)
+        rel, _ = check_y(y_img, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
+        assert rel < 1e-3
+        x2 = DB.from_array(2 * x)
+        ggml_hip.mul_mat(wd, K, M, x2, 512, yd, algo=2)
+        assert np.array_equal(yd.download((512, M), np.float32).view(np.uint32), (2 * y_img).view(np.uint32))
+    finally:
+        _gemm_version(-1)
+        assert L.ggml_hip_weight_image_free(wd.ptr) == 1
+    assert L.ggml_hip_weight_image_bytes() == before
+    ggml_hip.mul_mat(wd, K, M, xd, 512, yd, algo=2)                       # k_gemm7 again
+    y7 = yd.download((512, M), np.float32)
+    check_y(y7, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
+
+
+def test_gemm8_mixed_sibling_group_bitwise():
+    """A sibling group (one x quantization per form) where only some weights have images: the k_gemm8
+    and k_gemm7 siblings each read their own x form, bitwise equal to separate calls."""
+    L = ggml_hip.load()
+    K, N = 4096, 200
+    Ms = [256, 128, 300]
+    cases = [make_case(K, M, N, seed=60 + i) for i, M in enumerate(Ms)]
+    x = cases[0][1]
+    wds = [DB.from_array(c[0]) for c in cases]
+    ggml_hip.check(L.ggml_hip_weight_image_create(wds[1].ptr, K, Ms[1], None), "image")
+    try:
+        xd = DB.from_array(x)
+        ys = [DB(N * M * 4) for M in Ms]
+        ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
+        for wd, yd, M in zip(wds, ys, Ms):
+            single = DB(N * M * 4)
+            ggml_hip.mul_mat(wd, K, M, xd, N, single)
+            assert np.array_equal(yd.download((N, M), np.float32).view(np.uint32),
+                                  single.download((N, M), np.float32).view(np.uint32))
+        xq = O.quantize_q8_0(x, "avx2")
+        _, s_abs = block_terms(cases[1][0], xq, K)
+        check_y(ys[1].download((N, Ms[1]), np.float32), O.mul_mat(cases[1][0], K, x, nthreads=4), s_abs, RTOL,
+                ATOL_BLOCKS)
+    finally:
+        L.ggml_hip_weight_image_free(wds[1].ptr)
+
+
+def test_gemm8_image_api_errors():
+    L = ggml_hip.load()
+    wq, _ = make_case(128, 64, 1, seed=3)
+    wd = DB.from_array(wq)
+    assert L.ggml_hip_weight_image_create(wd.ptr, 96, 64, None) == ggml_hip.ERR_INVALID
+    assert L.ggml_hip_weight_image_create(None, 128, 64, None) == ggml_hip.ERR_INVALID
+    assert L.ggml_hip_weight_image_free(wd.ptr) == 0
+    assert L.ggml_hip_debug_set_gemm_version(5) == ggml_hip.ERR_INVALID

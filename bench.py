@@ -575,6 +575,37 @@ def _stats(vals):
     return {"median": float(np.median(v)), "min": float(v.min()), "max": float(v.max()), "n": int(v.size)}
 
 
+def _cpu_share():
+    """P for the CPU baseline: BASELINE.md §3 asks for the physical cores of one socket; a job on the GPU
+    box runs under a CPU quota (cgroup cpu.max / affinity / OMP_NUM_THREADS, 16 for one GPU), and
+    threads beyond the quota only time-slice, so P = min(cores per socket, quota), both reported."""
+    per_socket = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("cpu cores"):
+                per_socket = int(line.split(":")[1])
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    limits = {k: v for k, v in (("cgroup_cpu_max", quota), ("affinity", affinity), ("OMP_NUM_THREADS", omp)) if v}
+    cap = min(limits.values()) if limits else (os.cpu_count() or 1)
+    P = min(per_socket or cap, cap)
+    binding = min(limits, key=limits.get) if limits and cap < (per_socket or cap + 1) else "cores_per_socket"
+    lim = ", ".join(f"{k}={v}" for k, v in limits.items())
+    rule = (f"P = min(physical cores per socket {per_socket}, this job's CPU limit {cap} ({lim}))"
+            if per_socket else f"P = this job's CPU limit {cap} ({lim})")
+    return {"P": P, "cores_per_socket": per_socket, "limits": limits, "binding": binding, "rule": rule}
+
+
 def cpu_baseline(budget_s):
     """CPU path timed beside the GPU path on this host.
 
@@ -588,7 +619,8 @@ def cpu_baseline(budget_s):
     persistent-pool form (the oracle's AVX2 restatement of the same path, kind "port"), a 512-token
     prefill layer, and BASELINE config 1 (test-quantize-perf q4_0 vec_dot over 4096 x 4096 values, one
     thread).  Median / min / max over the samples.  kind "port" only when oracle/_ref was not built."""
-    P = int(os.environ.get("CPU_BASELINE_THREADS", min(16, os.cpu_count() or 1)))
+    share = _cpu_share()
+    P = int(os.environ.get("CPU_BASELINE_THREADS", share["P"]))
     n_copies = 6                                   # ~680 MB of weights: beyond any host LLC
     flags = _cpu_flags()
     native_ok = {"avx512f", "avx512bw", "avx512vl", "avx_vnni"} <= flags
@@ -651,9 +683,9 @@ def cpu_baseline(budget_s):
         "value": round(tok(dP["median"]), 3), "unit": "tok/s", "cores": P, "kind": "reference",
         "sample": (f"LLaMA-7B decode layers (7 q4_0 mul_mats, N=1) over {n_copies} rotating layer copies through the "
                    f"reference ggml.c (oracle/_ref, {build}); one ggml graph per pass, one ggml_graph_compute with "
-                   f"{P} threads (this process's CPU share on the box); {dP['n']} samples of >= 0.8 s, median; "
+                   f"{P} threads ({share['rule']}); {dP['n']} samples of >= 0.8 s, median; "
                    f"tok/s = 1/(32 x layer time)"),
-        "cpu": _cpu_name(), "host_cpus": os.cpu_count(), "build": build,
+        "cpu": _cpu_name(), "host_cpus": os.cpu_count(), "build": build, "cpu_share": share,
         "decode": {
             "threads_P": {"threads": P, "tok_s_median": round(tok(dP["median"]), 3),
                           "tok_s_min": round(tok(dP["max"]), 3), "tok_s_max": round(tok(dP["min"]), 3),

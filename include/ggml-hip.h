@@ -234,6 +234,17 @@ int ggml_hip_comm_destroy(ggml_hip_comm *comm);
  * below runs the same code on either transport.  Destroy each comm with ggml_hip_comm_destroy. */
 int ggml_hip_comm_init_local(ggml_hip_comm **comms, int nranks, const int *devices);
 int ggml_hip_comm_rank(const ggml_hip_comm *comm, int *rank, int *nranks);
+/* Direct-store all-gather (SURVEY.md §8e's P2P alternative to ncclAllGather for latency-bound decode
+ * gathers): each rank stores its slice straight into every peer's landing buffer over xGMI (an IPC
+ * mapping across processes, the buffer itself in a loopback group) and raises a flag there; one
+ * kernel per all-gather, graph-capturable (the epoch advances on the device).  Collective: call on
+ * every rank of the comm with the same max_floats (the largest slice of one all-gather, floats);
+ * at most 8 ranks.  After it the comm's all-gathers (the split mul_mats) use P2P stores;
+ * set_transport(comm, 0) returns to RCCL (1 = P2P again).  p2p_status synchronizes the device and
+ * returns 0, or a bit mask of peers whose data never arrived (bounded wait; results invalid). */
+int ggml_hip_comm_enable_p2p(ggml_hip_comm *comm, int64_t max_floats);
+int ggml_hip_comm_set_transport(ggml_hip_comm *comm, int transport);
+int ggml_hip_comm_p2p_status(ggml_hip_comm *comm);
 /* All-reduce of n <= 64 host doubles in place (op 0 sum, 1 max, 2 min) over the comm; synchronous,
  * so it is also a barrier (bench harness: max-over-ranks timing without a second runtime). */
 int ggml_hip_comm_allreduce_host(ggml_hip_comm *comm, double *vals, int n, int op);

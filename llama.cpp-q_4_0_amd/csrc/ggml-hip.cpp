@@ -2564,6 +2564,8 @@ struct LocalGroup {
     std::vector<size_t> count;
     std::vector<hipEvent_t> ready, done;       // per rank: send written / copies out of it enqueued
     std::vector<double> red;                   // host all-reduce scratch [R][n]
+    std::vector<void *> p2p;                   // each rank's P2P landing allocation (enable_p2p)
+    std::vector<int> p2p_dev;
     int refs = 0;
 
     // every rank calls this with the same sequence number of collectives; blocks until all arrived
@@ -2591,6 +2593,12 @@ struct ggml_hip_comm {
     float *slab = nullptr;        // [nranks][N][max_rows] gather buffer
     size_t slab_bytes = 0;
     double *red_dev = nullptr;    // host-value all-reduce staging (64 doubles)
+    // direct-store all-gather (ggml_hip_comm_enable_p2p, p2p_gather.hip)
+    int transport = 0;            // 0: RCCL / loopback copies, 1: P2P stores
+    bool p2p_on = false;
+    ghip::P2PArgs p2p{};
+    void *p2p_mine = nullptr;
+    std::vector<void *> p2p_opened;   // IPC mappings of the peers' landing buffers
 };
 
 namespace {
@@ -2604,8 +2612,17 @@ namespace {
         }                                                                                            \
     } while (0)
 
+// landing allocation of one rank: [2][R][cap] floats, then R flag words, then the control block
+size_t p2p_flag_off(int R, int64_t cap) { return ((size_t)2 * R * cap * 4 + 255) & ~(size_t)255; }
+size_t p2p_ctl_off(int R, int64_t cap) { return p2p_flag_off(R, cap) + 256; }
+size_t p2p_bytes(int R, int64_t cap) { return p2p_ctl_off(R, cap) + 256; }
+
 // GHIP_SYNC(ncclAllGather)(send, recv, count floats) on the comm's transport, stream-ordered on s
 int comm_allgather(ggml_hip_comm *c, const float *send, float *recv, size_t count, hipStream_t s) {
+    if (c->transport == 1 && c->p2p_on && (int64_t)count <= c->p2p.cap) {
+        HIP_RET(ghip::p2p_allgather(c->p2p, send, (int64_t)count, recv, s));
+        return GGML_HIP_OK;
+    }
     if (!c->local) {
         NCCL_RET(GHIP_SYNC(ncclAllGather)(send, recv, count, ncclFloat32, c->comm, s));
         return GGML_HIP_OK;
@@ -2632,11 +2649,11 @@ int comm_allgather(ggml_hip_comm *c, const float *send, float *recv, size_t coun
     return agree ? GGML_HIP_OK : fail(GGML_HIP_ERR_COMM, "loopback all-gather: ranks disagree on count");
 }
 int comm_group_start(ggml_hip_comm *c) {
-    if (!c->local) NCCL_RET(ncclGroupStart());
+    if (!c->local && c->transport == 0) NCCL_RET(ncclGroupStart());
     return GGML_HIP_OK;
 }
 int comm_group_end(ggml_hip_comm *c) {
-    if (!c->local) NCCL_RET(GHIP_SYNC(ncclGroupEnd)());
+    if (!c->local && c->transport == 0) NCCL_RET(GHIP_SYNC(ncclGroupEnd)());
     return GGML_HIP_OK;
 }
 
@@ -2702,6 +2719,9 @@ int ggml_hip_comm_init_local(ggml_hip_comm **comms, int nranks, const int *devic
 
 int ggml_hip_comm_destroy(ggml_hip_comm *c) {
     if (!c) return GGML_HIP_OK;
+    if (c->p2p_on) (void)GHIP_SYNC(hipDeviceSynchronize)();
+    for (void *p : c->p2p_opened) (void)hipIpcCloseMemHandle(p);
+    if (c->p2p_mine) (void)GHIP_SYNC(hipFree)(c->p2p_mine);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->slab) (void)GHIP_SYNC(hipFree)(c->slab);
     if (c->red_dev) (void)GHIP_SYNC(hipFree)(c->red_dev);
@@ -2757,6 +2777,105 @@ int ggml_hip_comm_allreduce_host(ggml_hip_comm *c, double *vals, int n, int op) 
     HIP_RET(GHIP_SYNC(hipMemcpyAsync)(vals, c->red_dev, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     HIP_RET(GHIP_SYNC(hipStreamSynchronize)(s));
     return GGML_HIP_OK;
+}
+
+int ggml_hip_comm_enable_p2p(ggml_hip_comm *c, int64_t max_floats) {
+    ensure_init();
+    if (!c || max_floats < 1) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    if (c->nranks > ghip::P2P_MAX_RANKS) return fail(GGML_HIP_ERR_UNSUPPORTED, "P2P all-gather: at most 8 ranks");
+    if (c->p2p_on) return fail(GGML_HIP_ERR_INVALID, "P2P already enabled on this comm");
+    const int R = c->nranks, me = c->rank;
+    const int64_t cap = (max_floats + 63) & ~(int64_t)63;
+    const size_t bytes = p2p_bytes(R, cap);
+    HIP_RET(hipSetDevice(c->device));
+    // fine-grained landing memory (coherent across devices); plain device memory where unavailable
+    if (hipExtMallocWithFlags(&c->p2p_mine, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+        (void)hipGetLastError();
+        HIP_RET(hipMalloc(&c->p2p_mine, bytes));
+    }
+    HIP_RET(GHIP_SYNC(hipMemset)(c->p2p_mine, 0, bytes));
+    HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
+    std::vector<char *> base(R, nullptr);
+    base[me] = (char *)c->p2p_mine;
+    if (c->local) {                            // one process: the peers' allocations directly
+        LocalGroup &g = *c->local;
+        {
+            std::lock_guard<std::mutex> lk(g.mu);
+            if (g.p2p.size() != (size_t)R) g.p2p.assign(R, nullptr), g.p2p_dev.assign(R, -1);
+            g.p2p[me] = c->p2p_mine;
+            g.p2p_dev[me] = c->device;
+        }
+        g.barrier();
+        for (int r = 0; r < R; r++) {
+            base[r] = (char *)g.p2p[r];
+            if (g.p2p_dev[r] != c->device) {
+                const hipError_t e = hipDeviceEnablePeerAccess(g.p2p_dev[r], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_RET(e);
+                (void)hipGetLastError();
+            }
+        }
+        g.barrier();                           // nobody re-assigns g.p2p before all have read it
+    } else {                                   // one process per GPU: IPC handles through the comm
+        hipIpcMemHandle_t h;
+        HIP_RET(hipIpcGetMemHandle(&h, c->p2p_mine));
+        static_assert(sizeof(hipIpcMemHandle_t) <= 128, "IPC handle size");
+        char *dev = nullptr;
+        HIP_RET(hipMalloc(&dev, (size_t)128 * R));
+        std::vector<char> all((size_t)128 * R, 0);
+        memcpy(all.data() + (size_t)128 * me, &h, sizeof h);
+        hipStream_t s = g_dev[c->device].stream;
+        HIP_RET(GHIP_SYNC(hipMemcpyAsync)(dev + (size_t)128 * me, all.data() + (size_t)128 * me, 128,
+                                          hipMemcpyHostToDevice, s));
+        NCCL_RET(GHIP_SYNC(ncclAllGather)(dev + (size_t)128 * me, dev, 128, ncclChar, c->comm, s));
+        HIP_RET(GHIP_SYNC(hipMemcpyAsync)(all.data(), dev, all.size(), hipMemcpyDeviceToHost, s));
+        HIP_RET(GHIP_SYNC(hipStreamSynchronize)(s));
+        HIP_RET(GHIP_SYNC(hipFree)(dev));
+        for (int r = 0; r < R; r++) {
+            if (r == me) continue;
+            hipIpcMemHandle_t hr;
+            memcpy(&hr, all.data() + (size_t)128 * r, sizeof hr);
+            void *p = nullptr;
+            HIP_RET(hipIpcOpenMemHandle(&p, hr, hipIpcMemLazyEnablePeerAccess));
+            c->p2p_opened.push_back(p);
+            base[r] = (char *)p;
+        }
+        double v = 0.0;                        // every rank mapped every peer before any store
+        const int rc = ggml_hip_comm_allreduce_host(c, &v, 1, 0);
+        if (rc != GGML_HIP_OK) return rc;
+    }
+    ghip::P2PArgs a{};
+    for (int r = 0; r < R; r++) {
+        a.land[r] = (float *)base[r];
+        a.flag[r] = (uint64_t *)(base[r] + p2p_flag_off(R, cap));
+    }
+    a.ctl = (uint64_t *)((char *)c->p2p_mine + p2p_ctl_off(R, cap));
+    a.me = me;
+    a.R = R;
+    a.cap = cap;
+    c->p2p = a;
+    c->p2p_on = true;
+    c->transport = 1;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_comm_set_transport(ggml_hip_comm *c, int transport) {
+    if (!c || transport < 0 || transport > 1) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    if (transport == 1 && !c->p2p_on) return fail(GGML_HIP_ERR_INVALID, "P2P not enabled on this comm");
+    c->transport = transport;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_comm_p2p_status(ggml_hip_comm *c) {
+    if (!c || !c->p2p_on) return fail(GGML_HIP_ERR_INVALID, "P2P not enabled on this comm");
+    HIP_RET(hipSetDevice(c->device));
+    HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
+    uint64_t err = 0;
+    HIP_RET(GHIP_SYNC(hipMemcpy)(&err, c->p2p.ctl + 2, 8, hipMemcpyDeviceToHost));
+    if (err) {
+        const uint64_t z = 0;
+        HIP_RET(GHIP_SYNC(hipMemcpy)(c->p2p.ctl + 2, &z, 8, hipMemcpyHostToDevice));
+    }
+    return (int)err;
 }
 
 int ggml_hip_comm_rank(const ggml_hip_comm *c, int *rank, int *nranks) {

@@ -1,0 +1,74 @@
+// p2p_gather.hip — direct-store all-gather over xGMI (the "P2P-store fallback if RCCL
+// small-message latency dominates"; reference gather ggml-cuda.cu:2514-2539 copies each device's row
+// slice to the main device with cudaMemcpyPeerAsync).
+//
+// Every rank owns a landing buffer: 2 slots x R segments x cap floats, then a flag word per peer and a
+// control block.  One launch per all-gather on each rank, R - 1 workgroups: workgroup j serves peer
+// q = (me + 1 + j) % R — it stores this rank's slice into segment `me` of slot (epoch & 1) of q's
+// landing buffer (a plain device pointer in one process, an IPC mapping across processes), publishes
+// it with a system-scope release fence and a flag store of the epoch into q's flag word `me`, then
+// waits (bounded) for q's flag in its own landing buffer and copies segment q into recv.  The epoch
+// lives on the device (control word 0, advanced by the last workgroup to finish), so the launch can
+// be captured in a HIP graph and replayed.  Two slots suffice: peer q writes slot (e & 1) for epoch e
+// only after its launch e - 1 completed, which needed this rank's e - 1 data, i.e. this rank's launch
+// e - 2 (the last reader of that slot) had completed.
+#include "q4_0_kernels.h"
+#include "launch.h"
+
+namespace ghip {
+
+__global__ __launch_bounds__(256) void k_p2p_allgather(const P2PArgs a, const float *__restrict__ send,
+                                                        int64_t count, float *__restrict__ recv) {
+    const int me = a.me, R = a.R;
+    const int tid = threadIdx.x;
+    const uint64_t e = a.ctl[0] + 1;                 // written only by the previous launch's last workgroup
+    const int slot = (int)(e & 1);
+    if (blockIdx.x == 0 && recv + (int64_t)me * count != send)   // own slice (not in place)
+        for (int64_t i = tid; i < count; i += blockDim.x) recv[(int64_t)me * count + i] = send[i];
+    if (R > 1) {
+        const int q = (me + 1 + (int)blockIdx.x) % R;
+        float *dst = a.land[q] + ((int64_t)slot * R + me) * a.cap;
+        for (int64_t i = tid; i < count; i += blockDim.x) dst[i] = send[i];    // stores over xGMI
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");                  // system scope: the peer's view
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.flag[q] + me, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // wait for q's slice in this rank's landing buffer (bounded: a peer that never arrives sets
+            // the error word instead of hanging the device)
+            uint32_t spins = 0;
+            while (__hip_atomic_load(a.flag[me] + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 24)) {
+                    __hip_atomic_fetch_or(a.ctl + 2, 1ull << q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        }
+        __syncthreads();
+        const float *src = a.land[me] + ((int64_t)slot * R + q) * a.cap;
+        for (int64_t i = tid; i < count; i += blockDim.x) recv[(int64_t)q * count + i] = src[i];
+    }
+    // the last workgroup to finish advances the epoch for the next launch
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const uint64_t old = __hip_atomic_fetch_add(a.ctl + 1, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gridDim.x - 1) {
+            __hip_atomic_store(a.ctl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ctl + 0, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+hipError_t p2p_allgather(const P2PArgs &a, const float *send, int64_t count, float *recv, hipStream_t s) {
+    if (a.R < 1 || a.R > P2P_MAX_RANKS || a.me < 0 || a.me >= a.R || count < 0 || count > a.cap)
+        return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    launch_k(k_p2p_allgather, dim3(a.R > 1 ? a.R - 1 : 1), dim3(256), 0, s, a, send, count, recv);
+    return hipGetLastError();
+}
+
+}  // namespace ghip

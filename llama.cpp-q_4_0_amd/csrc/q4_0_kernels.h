@@ -121,6 +121,19 @@ int chain_max_workgroups(int kmax, int ntasks, int depth);   // resident workgro
 hipError_t gemv_chain_q4_0(const ChainTaskDev *tasks, int ntasks, uint32_t *sync, int kmax, int grid, int depth,
                            unsigned long long *stamps, hipStream_t s);
 
+// Direct-store all-gather over xGMI (p2p_gather.hip): land[r] = rank r's landing buffer as mapped in
+// this process ([2 slots][R][cap] floats), flag[r] = its R flag words, ctl = this rank's control block
+// (epoch, arrivals, error bits).
+constexpr int P2P_MAX_RANKS = 8;
+struct P2PArgs {
+    float *land[P2P_MAX_RANKS];
+    uint64_t *flag[P2P_MAX_RANKS];
+    uint64_t *ctl;
+    int me, R;
+    int64_t cap;
+};
+hipError_t p2p_allgather(const P2PArgs &a, const float *send, int64_t count, float *recv, hipStream_t s);
+
 // Synthetic inputs for the bench (splitmix64 + Box-Muller on device).
 hipError_t fill_gaussian(float *dst, int64_t n, uint64_t seed, float mean, float std, hipStream_t s);
 

@@ -58,6 +58,9 @@ def _bind(L):
         "ggml_hip_reserve_workspace": ([i64, i64], i32),
         "ggml_hip_reserve_workspace_mm": ([i64, i64, i64], i32),
         "ggml_hip_weight_image_create": ([vp, i64, i64, vp], i32),
+        "ggml_hip_comm_enable_p2p": ([vp, i64], i32),
+        "ggml_hip_comm_set_transport": ([vp, i32], i32),
+        "ggml_hip_comm_p2p_status": ([vp], i32),
         "ggml_hip_weight_image_free": ([vp], i32),
         "ggml_hip_weight_image_bytes": ([], i64),
         "ggml_hip_debug_set_gemm_version": ([i32], i32),

@@ -245,3 +245,102 @@ def test_split_rccl_multiprocess(R):
         for r, (p, o) in enumerate(zip(procs, outs)):
             assert p.returncode == 0, f"rank {r} failed:\n{o[-3000:]}"
             assert "SPLIT_OK" in o, o[-2000:]
+
+
+# ------------------------------------------------------------------ direct-store (P2P) all-gather
+@pytest.mark.parametrize("R", [2, 3])
+@pytest.mark.parametrize("N,uneven", [(1, False), (1, True), (3, False), (40, True)])
+def test_split_p2p_loopback_ranks(R, N, uneven):
+    """ggml_hip_comm_enable_p2p: the same split calls with the all-gather done by direct stores into
+    the peers' landing buffers + flags (p2p_gather.hip) instead of copies; repeated calls cycle the
+    device-side epoch through both landing slots.  Every rank's y_full == the slice products, bitwise,
+    and no peer wait timed out.  (R <= 3 ranks share one device: their spinning gathers must be
+    co-resident, so each rank's stream needs its own hardware queue.)"""
+    K, M = 4096, 1000 if uneven else 1024
+    wq, x = make_case(K, M, N, seed=300 * R + N + uneven)
+    rb = split_rows(M, R, FRACTIONS[R] if uneven else None)
+    slices = [wq[rb[r]:rb[r + 1]] for r in range(R)]
+    expect = np.concatenate([gpu_y(s, K, x) for s in slices], axis=1)
+    L = ggml_hip.load()
+    xd = DB.from_array(x)
+    wds = [DB.from_array(s) for s in slices]
+    yds = [DB(N * M * 4) for _ in range(R)]
+    ggml_hip.synchronize()
+
+    def rank(r, comm, stream):
+        ggml_hip.check(L.ggml_hip_comm_enable_p2p(comm, N * M), f"enable_p2p rank {r}")
+        for it in range(5):
+            L.ggml_hip_memset(yds[r].ptr, 0x7F, yds[r].nbytes, stream)
+            ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split(comm, wds[r].ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
+                                                         xd.ptr, N, yds[r].ptr, stream), f"split rank {r}")
+        return L.ggml_hip_comm_p2p_status(comm)
+
+    status = run_ranks(R, rank)
+    assert status == [0] * R, status
+    for r in range(R):
+        got = yds[r].download((N, M), np.float32)
+        assert np.array_equal(got.view(np.uint32), expect.view(np.uint32)), f"rank {r}"
+
+
+@pytest.mark.parametrize("R", [2, 3])
+def test_split_multi_p2p_graph_replay(R):
+    """Sibling group (one GEMV + one all-gather per matrix) over P2P stores, captured in a HIP graph on
+    every rank and replayed: the epoch advances on the device, so replays keep alternating slots."""
+    K, N, Ms = 4096, 1, (1024, 2048, 512)
+    n = len(Ms)
+    x = O.gaussian(N * K, 0x5EED5100 + R, 0.0, 1.0).reshape(N, K)
+    rbs = [split_rows(M, R) for M in Ms]
+    ws = [make_case(K, M, 1, seed=17 * i + R)[0] for i, M in enumerate(Ms)]
+    expect = [np.concatenate([gpu_y(w[rb[r]:rb[r + 1]], K, x) for r in range(R)], axis=1) for w, rb in zip(ws, rbs)]
+    L = ggml_hip.load()
+    xd = DB.from_array(x)
+    wds = [[DB.from_array(w[rb[r]:rb[r + 1]]) for w, rb in zip(ws, rbs)] for r in range(R)]
+    yds = [[DB(N * M * 4) for M in Ms] for _ in range(R)]
+    ggml_hip.synchronize()
+    mt = (ctypes.c_int64 * n)(*Ms)
+    rp = (ctypes.c_void_p * n)(*[rb.ctypes.data for rb in rbs])
+
+    def rank(r, comm, stream):
+        ggml_hip.check(L.ggml_hip_comm_enable_p2p(comm, max(Ms)), f"enable_p2p rank {r}")
+        wp = (ctypes.c_void_p * n)(*[w.ptr for w in wds[r]])
+        yp = (ctypes.c_void_p * n)(*[y.ptr for y in yds[r]])
+
+        def call():
+            ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split_multi(comm, n, wp, mt, rp, K, xd.ptr, N, yp, stream),
+                           f"split_multi rank {r}")
+        call()
+        g = ggml_hip.Graph(stream)
+        with g:
+            call()
+        for _ in range(4):
+            for y in yds[r]:
+                L.ggml_hip_memset(y.ptr, 0, y.nbytes, stream)
+            g.launch()
+        ggml_hip.check(L.ggml_hip_stream_synchronize(stream))
+        del g
+        return L.ggml_hip_comm_p2p_status(comm)
+
+    status = run_ranks(R, rank)
+    assert status == [0] * R, status
+    for r in range(R):
+        for i, M in enumerate(Ms):
+            got = yds[r][i].download((N, M), np.float32)
+            assert np.array_equal(got.view(np.uint32), expect[i].view(np.uint32)), (r, i)
+
+
+def test_p2p_api_errors():
+    L = ggml_hip.load()
+    comms = (ctypes.c_void_p * 1)()
+    ggml_hip.check(L.ggml_hip_comm_init_local(comms, 1, None))
+    c = ctypes.c_void_p(comms[0])
+    try:
+        assert L.ggml_hip_comm_set_transport(c, 1) == ggml_hip.ERR_INVALID      # not enabled yet
+        assert L.ggml_hip_comm_p2p_status(c) == ggml_hip.ERR_INVALID
+        assert L.ggml_hip_comm_enable_p2p(c, 0) == ggml_hip.ERR_INVALID
+        ggml_hip.check(L.ggml_hip_comm_enable_p2p(c, 4096))
+        assert L.ggml_hip_comm_enable_p2p(c, 4096) == ggml_hip.ERR_INVALID     # twice
+        ggml_hip.check(L.ggml_hip_comm_set_transport(c, 0))
+        ggml_hip.check(L.ggml_hip_comm_set_transport(c, 1))
+        assert L.ggml_hip_comm_p2p_status(c) == 0
+    finally:
+        L.ggml_hip_comm_destroy(c)

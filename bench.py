@@ -137,6 +137,8 @@ def main():
                     help="run the multi-GPU code path (row split + RCCL all-gather) even with one rank")
     ap.add_argument("--no-extra", action="store_true", help="skip the LLaMA-13B / Falcon-7B decode lines")
     ap.add_argument("--no-exact", action="store_true", help="skip the exact-mode (bit-identical) decode line")
+    ap.add_argument("--no-p2p", action="store_true",
+                    help="N > 1: skip the direct-store (P2P) all-gather line next to RCCL's")
     ap.add_argument("--no-batch-siblings", action="store_true",
                     help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
     args = ap.parse_args()
@@ -306,6 +308,9 @@ def main():
         result["config"]["split_check"] = split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream)
         if not all(result["config"]["split_check"][k] for k in ("own_rows_bitwise", "gather_checksum")):
             log(f"[rank {rank}] SPLIT CHECK FAILED: {result['config']['split_check']}")
+        if world > 1 and not args.no_p2p:
+            result["config"]["p2p_transport"] = p2p_decode(gh, L, comm, decode_step, stack, ysplit, yb, rank,
+                                                           allreduce, barrier, stream, args, elapsed - el)
     result["config"]["runtime_libs"] = gh.mapped_runtime_libs()
 
     if rank == 0 and world == 1 and comm is None:
@@ -332,6 +337,44 @@ def _bits_checksum(a, offset):
     u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64).ravel()
     pos = np.arange(offset, offset + u.size, dtype=np.uint64)
     return int(np.sum((u + np.uint64(1)) * (pos * np.uint64(2654435761) + np.uint64(97)), dtype=np.uint64))
+
+
+def p2p_decode(gh, L, comm, decode_step, stack, ysplit, yb, rank, allreduce, barrier, stream, args, rccl_coll_s):
+    """The same row-sharded decode with the all-gathers done by direct stores into the peers' landing
+    buffers over xGMI (ggml_hip_comm_enable_p2p, p2p_gather.hip) instead of ncclAllGather: tok/s and
+    the collective cost per token next to RCCL's, plus the bitwise split check.  One eager step and a
+    status check first: a transport that cannot run here (IPC, peer access) is reported, not timed."""
+    max_floats = max(M for row in stack.mats for _, K, M, m, buf, rb in row)
+    rc = L.ggml_hip_comm_enable_p2p(comm, max_floats)
+    if allreduce([float(rc)], 2)[0] != 0.0:              # any rank failed
+        L.ggml_hip_comm_set_transport(comm, 0)
+        return {"error": f"enable_p2p rc={rc}: {L.ggml_hip_last_error().decode(errors='replace')}"}
+    try:
+        decode_step()
+        st = L.ggml_hip_comm_p2p_status(comm)
+        if allreduce([float(st)], 1)[0] != 0.0:
+            return {"error": f"peer waits timed out (status {st})"}
+        g = gh.Graph(stream)
+        with g:
+            decode_step()
+        for _ in range(args.warmup):
+            g.launch()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g.launch()
+        barrier()
+        el = allreduce([time.perf_counter() - t0], 1)[0]
+        st = L.ggml_hip_comm_p2p_status(comm)
+        ok = allreduce([float(st)], 1)[0] == 0.0
+        chk = split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream)
+        tok = args.steps / el * 32 / args.layers
+        return {"tok_s": round(tok, 2), "ms_per_step": round(el / args.steps * 1e3, 4), "status_ok": ok,
+                "split_check": chk,
+                "rccl_collective_us_per_token": round(rccl_coll_s / args.steps * 1e6 * 32 / args.layers, 1),
+                "note": "collective cost = this line's time minus the compute-only graph's (config)"}
+    finally:
+        L.ggml_hip_comm_set_transport(comm, 0)
 
 
 def split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream):

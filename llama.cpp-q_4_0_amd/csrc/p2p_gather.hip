@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void k_p2p_allgather(const P2PArgs a, const fl
             uint32_t spins = 0;
             while (__hip_atomic_load(a.flag[me] + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 24)) {
+                if (++spins > (1u << 21)) {
                     __hip_atomic_fetch_or(a.ctl + 2, 1ull << q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }

@@ -1863,7 +1863,8 @@ __global__ __launch_bounds__(256) void k_prep8_w(const uint8_t *__restrict__ W, 
     }
 }
 
-// DIAG (timing knockouts, results invalid): 1 no compute (DMA ring + barriers only), 2 no DMA
+// DIAG (timing knockouts, results invalid): 1 no compute (DMA ring + barriers only), 2 no DMA,
+// 3 no DMA and no per-stage barrier (the compute loop alone)
 // VAR bits (A/B knobs, all bitwise-identical results): 1 the i8 MFMA accumulates on 0 and the
 // epilogue converts with v_cvt_f32_i32 (no 16-register bias operand to keep live or rebuild); 2 the
 // next block's operands are read from LDS while the current block computes
@@ -1897,7 +1898,7 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
     const int lw = wave - 8;
     const int lb = 2 * lw;                                                         // first block
     auto issue = [&](int st) __attribute__((always_inline)) {
-        if (DIAG == 2 || wave < 8) return;
+        if (DIAG >= 2 || wave < 8) return;
         uint8_t *base = smem + (st % G8_NS) * G8_STAGE;
         const int kb0 = st * G8_KB;
         const bool v = kb0 + lb < nb;                                             // nb even: both or none
@@ -1929,7 +1930,7 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
     const int t0 = 64 * (q >> 1) + c, t1 = t0 + 32;
     const int hw = 16 * (h ^ ((wrow >> 3) & 1));
     const int h0 = 16 * (h ^ ((t0 >> 3) & 1)), h1 = 16 * (h ^ ((t1 >> 3) & 1));
-    constexpr bool CVT = VAR & 1, PF = VAR & 2;
+    constexpr bool CVT = VAR & 1, PF = VAR & 2, GRP = VAR & 4;
     const int mg = CVT ? 0 : 0x4B400000;
     const i32x16 im = {mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg};
     const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1966,6 +1967,20 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
         bs.x = o.sw;
         as0.x = o.sx0;
         as1.x = o.sx1;
+        if constexpr (GRP) {
+            // the block's four MFMAs back to back, then both epilogues: the wave parks on the matrix pipe
+            // while its SIMD partner runs its VALU (the two compute waves of a SIMD fall out of phase);
+            // every epilogue reads MFMA results issued a whole burst earlier
+            epi(acc0, S0, P0);
+            epi(acc1, S1, P1);
+            __builtin_amdgcn_sched_barrier(0);
+            S0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a0, o.bw, im, 0, 0, 0);
+            P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as0), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+            S1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a1, o.bw, im, 0, 0, 0);
+            P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as1), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            return;
+        }
         S0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a0, o.bw, im, 0, 0, 0);
         P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as0), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
         epi(acc1, S1, P1);                     // tile 1 of the previous block (S1 = bias, P1 = 0 at first)
@@ -1974,6 +1989,7 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
         epi(acc0, S0, P0);
     };
     auto sync = [&]() __attribute__((always_inline)) {   // retire stage s+1, keep s+2 in flight
+        if (DIAG == 3) return;
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((G8_NS - 2) * G8_OPS) : "memory");
         __builtin_amdgcn_s_barrier();
     };
@@ -2005,6 +2021,7 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
         }
         sync();
     }
+    if (GRP) epi(acc0, S0, P0);
     epi(acc1, S1, P1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may outlive the ring
     __syncthreads();
@@ -2076,20 +2093,23 @@ hipError_t gemm8_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     if ((int64_t)nb * Np * 32 >= ((int64_t)1 << 31) || (int64_t)nb * 2048 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
-        for (auto k : {k_gemm8_q4_0<0, 0>, k_gemm8_q4_0<0, 1>, k_gemm8_q4_0<0, 2>, k_gemm8_q4_0<0, 3>,
-                       k_gemm8_q4_0<1, 3>, k_gemm8_q4_0<2, 3>}) {
+        for (auto k : {k_gemm8_q4_0<0, 0>, k_gemm8_q4_0<0, 1>, k_gemm8_q4_0<0, 2>, k_gemm8_q4_0<0, 3>, k_gemm8_q4_0<0, 7>,
+                       k_gemm8_q4_0<3, 7>,
+                       k_gemm8_q4_0<1, 3>, k_gemm8_q4_0<2, 3>, k_gemm8_q4_0<3, 3>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS);
             if (e != hipSuccess) return e;
         }
         attr = true;
     }
-    // GGML_HIP_GEMM8_VAR (A/B, tools/r3_g8var.sh): 3 = cvt epilogue + operand prefetch (default,
-    // 33.3 -> 29.7 us at 4096x4096x512); GGML_HIP_GEMM_DIAG 81 / 82 = DMA-only / compute-only knockouts
+    // GGML_HIP_GEMM8_VAR (A/B, tools/r3_g8var.sh, kernel medians at 4096x4096x512): 0 33.3 us, 3 = cvt
+    // epilogue + operand prefetch 29.6-29.8, 7 = 3 + MFMA bursts 29.2-29.4 (default; compute-only knockout
+    // 25.0 -> 23.8); GGML_HIP_GEMM_DIAG 81 / 82 / 83 = DMA-only / no DMA / no DMA and no barrier
     static const int diag = env_int("GGML_HIP_GEMM_DIAG", 0);
-    static const int var = env_int("GGML_HIP_GEMM8_VAR", 3);
-    auto kern = diag == 81 ? k_gemm8_q4_0<1, 3> : diag == 82 ? k_gemm8_q4_0<2, 3>
+    static const int var = env_int("GGML_HIP_GEMM8_VAR", 7);
+    auto kern = diag == 81 ? k_gemm8_q4_0<1, 3> : diag == 82 ? k_gemm8_q4_0<2, 3> : diag == 83 ? k_gemm8_q4_0<3, 3>
+              : diag == 87 ? k_gemm8_q4_0<3, 7> : var == 3 ? k_gemm8_q4_0<0, 3>
               : var == 0 ? k_gemm8_q4_0<0, 0> : var == 1 ? k_gemm8_q4_0<0, 1> : var == 2 ? k_gemm8_q4_0<0, 2>
-              : k_gemm8_q4_0<0, 3>;
+              : k_gemm8_q4_0<0, 7>;
     (void)hipGetLastError();
     launch_k(kern, dim3((unsigned)Mt, (unsigned)((N + G8_BN - 1) / G8_BN)), dim3(G8_THREADS), G8_LDS, s, wimg, wd16,
              nb, (int)M, ximg, xd16, Np, (int)N, y, ldy);

@@ -2806,6 +2806,17 @@ int ggml_hip_comm_enable_p2p(ggml_hip_comm *c, int64_t max_floats) {
             g.p2p_dev[me] = c->device;
         }
         g.barrier();
+        // the ranks' gathers wait on each other on the device, so the launches of ranks that share a
+        // device must run concurrently; beyond two per device their streams may share a hardware queue
+        // (GPU_MAX_HW_QUEUES = 4, one taken by the null stream) and a gather would wait behind a peer's
+        int same = 0;
+        for (int r = 0; r < R; r++) same += g.p2p_dev[r] == c->device;
+        if (same > 2) {
+            g.barrier();
+            (void)GHIP_SYNC(hipFree)(c->p2p_mine);
+            c->p2p_mine = nullptr;
+            return fail(GGML_HIP_ERR_UNSUPPORTED, "loopback P2P: at most 2 ranks per device");
+        }
         for (int r = 0; r < R; r++) {
             base[r] = (char *)g.p2p[r];
             if (g.p2p_dev[r] != c->device) {

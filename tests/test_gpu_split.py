@@ -248,14 +248,15 @@ def test_split_rccl_multiprocess(R):
 
 
 # ------------------------------------------------------------------ direct-store (P2P) all-gather
-@pytest.mark.parametrize("R", [2, 3])
+@pytest.mark.parametrize("R", [2])
 @pytest.mark.parametrize("N,uneven", [(1, False), (1, True), (3, False), (40, True)])
 def test_split_p2p_loopback_ranks(R, N, uneven):
     """ggml_hip_comm_enable_p2p: the same split calls with the all-gather done by direct stores into
     the peers' landing buffers + flags (p2p_gather.hip) instead of copies; repeated calls cycle the
     device-side epoch through both landing slots.  Every rank's y_full == the slice products, bitwise,
-    and no peer wait timed out.  (R <= 3 ranks share one device: their spinning gathers must be
-    co-resident, so each rank's stream needs its own hardware queue.)"""
+    and no peer wait timed out.  (The ranks share one device: their waiting gathers must run
+    concurrently, so each rank's stream needs its own hardware queue; the product allows at most 2
+    loopback ranks per device for P2P, test_p2p_api_errors.)"""
     K, M = 4096, 1000 if uneven else 1024
     wq, x = make_case(K, M, N, seed=300 * R + N + uneven)
     rb = split_rows(M, R, FRACTIONS[R] if uneven else None)
@@ -269,7 +270,7 @@ def test_split_p2p_loopback_ranks(R, N, uneven):
 
     def rank(r, comm, stream):
         ggml_hip.check(L.ggml_hip_comm_enable_p2p(comm, N * M), f"enable_p2p rank {r}")
-        for it in range(5):
+        for it in range(7):
             L.ggml_hip_memset(yds[r].ptr, 0x7F, yds[r].nbytes, stream)
             ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split(comm, wds[r].ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
                                                          xd.ptr, N, yds[r].ptr, stream), f"split rank {r}")
@@ -282,7 +283,7 @@ def test_split_p2p_loopback_ranks(R, N, uneven):
         assert np.array_equal(got.view(np.uint32), expect.view(np.uint32)), f"rank {r}"
 
 
-@pytest.mark.parametrize("R", [2, 3])
+@pytest.mark.parametrize("R", [2])
 def test_split_multi_p2p_graph_replay(R):
     """Sibling group (one GEMV + one all-gather per matrix) over P2P stores, captured in a HIP graph on
     every rank and replayed: the epoch advances on the device, so replays keep alternating slots."""
@@ -344,3 +345,6 @@ def test_p2p_api_errors():
         assert L.ggml_hip_comm_p2p_status(c) == 0
     finally:
         L.ggml_hip_comm_destroy(c)
+    # three loopback ranks on one device: refused (their gathers could queue behind each other)
+    status = run_ranks(3, lambda r, comm, stream: L.ggml_hip_comm_enable_p2p(comm, 1024))
+    assert status == [ggml_hip.ERR_UNSUPPORTED] * 3, status

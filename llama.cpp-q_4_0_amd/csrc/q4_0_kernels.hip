@@ -1930,7 +1930,7 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
     const int t0 = 64 * (q >> 1) + c, t1 = t0 + 32;
     const int hw = 16 * (h ^ ((wrow >> 3) & 1));
     const int h0 = 16 * (h ^ ((t0 >> 3) & 1)), h1 = 16 * (h ^ ((t1 >> 3) & 1));
-    constexpr bool CVT = VAR & 1, PF = VAR & 2, GRP = VAR & 4;
+    constexpr bool CVT = VAR & 1, PF = VAR & 2, GRP = VAR & 4, STAG = VAR & 8, PRIO = VAR & 16;
     const int mg = CVT ? 0 : 0x4B400000;
     const i32x16 im = {mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg};
     const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1995,6 +1995,10 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
     };
 
     const int nstages = (nb + G8_KB - 1) / G8_KB;
+    // STAG: the second compute half starts every stage half a block late, so that one wave of each SIMD
+    // is in its MFMA burst while its partner runs VALU (MI355X_MICROARCH.md, two waves per SIMD item 9);
+    // PRIO: that half at priority 1 (item 4)
+    if (PRIO && wave >= 4 && wave < 8) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int st = 0; st < G8_NS - 1; st++) issue(st);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((G8_NS - 2) * G8_OPS) : "memory");   // stage 0 landed
@@ -2002,6 +2006,7 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
     for (int s = 0; s < nstages; s++) {
         issue(s + G8_NS - 1);
         const int kb = s * G8_KB + 4 * g;
+        if (STAG && g == 1 && wave < 8) __builtin_amdgcn_s_sleep(2);
         if (DIAG != 1 && wave < 8) {
             if (PF) {                              // nb is even and kb too: blocks come in valid pairs
                 Ops o = rd(s, 4 * g);
@@ -2094,6 +2099,7 @@ hipError_t gemm8_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     static bool attr = false;
     if (!attr) {
         for (auto k : {k_gemm8_q4_0<0, 0>, k_gemm8_q4_0<0, 1>, k_gemm8_q4_0<0, 2>, k_gemm8_q4_0<0, 3>, k_gemm8_q4_0<0, 7>,
+                       k_gemm8_q4_0<0, 15>, k_gemm8_q4_0<0, 23>, k_gemm8_q4_0<0, 31>,
                        k_gemm8_q4_0<3, 7>,
                        k_gemm8_q4_0<1, 3>, k_gemm8_q4_0<2, 3>, k_gemm8_q4_0<3, 3>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS);
@@ -2107,7 +2113,8 @@ hipError_t gemm8_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     static const int diag = env_int("GGML_HIP_GEMM_DIAG", 0);
     static const int var = env_int("GGML_HIP_GEMM8_VAR", 7);
     auto kern = diag == 81 ? k_gemm8_q4_0<1, 3> : diag == 82 ? k_gemm8_q4_0<2, 3> : diag == 83 ? k_gemm8_q4_0<3, 3>
-              : diag == 87 ? k_gemm8_q4_0<3, 7> : var == 3 ? k_gemm8_q4_0<0, 3>
+              : diag == 87 ? k_gemm8_q4_0<3, 7> : var == 3 ? k_gemm8_q4_0<0, 3> : var == 15 ? k_gemm8_q4_0<0, 15>
+              : var == 23 ? k_gemm8_q4_0<0, 23> : var == 31 ? k_gemm8_q4_0<0, 31>
               : var == 0 ? k_gemm8_q4_0<0, 0> : var == 1 ? k_gemm8_q4_0<0, 1> : var == 2 ? k_gemm8_q4_0<0, 2>
               : k_gemm8_q4_0<0, 7>;
     (void)hipGetLastError();

@@ -569,6 +569,116 @@ __global__ __launch_bounds__(512, 2) void k_mb(const uint8_t *src, float *out, i
         }
         epi2(acc[1], S1, P1);
     }
+
+    if constexpr (VAR == 30 || VAR == 31 || VAR == 32) {
+        // 30: MFMA only, C = constant (im / 0), fresh destinations (the GEMM's form) — vs VAR 8 (chained)
+        // 31: VAR 16 (2 sets, epilogue reads the other set) but the MFMAs accumulate in place (D = C)
+        // 32: VAR 16 exactly, for reference (no LDS)
+        const int wr = wave & 1, wt = (wave >> 1) & 1;
+        const int t0 = 64 * wt + c, t1 = 64 * wt + 32 + c, row = 32 * wr + c;
+        i32x16 SA0 = im, SA1 = im, SB0 = im, SB1 = im;
+        f32x16 PA0 = fz, PA1 = fz, PB0 = fz, PB1 = fz;
+        const i32x4 bb = rdB(0, row), a0 = rdA(0, t0), a1 = rdA(0, t1);
+        const uint32_t w = rdSW(0, row), x0 = rdSX(0, t0), x1 = rdSX(0, t1);
+        const u32x4 as = {x0, 0u, 0u, 0u}, bs = {w, 0u, 0u, 0u}, as1 = {x1, 0u, 0u, 0u};
+        auto mf = [&](const i32x4 &a, const u32x4 &sx, i32x16 &S, f32x16 &P) __attribute__((always_inline)) {
+            if constexpr (VAR == 31) {
+                S = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bb, S, 0, 0, 0);
+                P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, sx), __builtin_bit_cast(half8, bs), P, 0, 0, 0);
+            } else {
+                S = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bb, im, 0, 0, 0);
+                P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, sx), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+            }
+        };
+        auto step = [&](i32x16 &Sa, f32x16 &Pa, i32x16 &Sb, f32x16 &Pb, i32x16 &Sa_, f32x16 &Pa_, i32x16 &Sb_,
+                        f32x16 &Pb_) __attribute__((always_inline)) {
+            mf(a0, as, Sa, Pa);
+            mf(a1, as1, Sb, Pb);
+            if constexpr (VAR != 30) {
+                epi(acc[0], Sa_, Pa_);
+                epi(acc[1], Sb_, Pb_);
+            }
+        };
+        for (int b = 0; b < nblk; b += 2) {
+            step(SA0, PA0, SB0, PB0, SA1, PA1, SB1, PB1);
+            step(SA1, PA1, SB1, PB1, SA0, PA0, SB0, PB0);
+        }
+        epi(acc[2], SA1, PA1);
+        epi(acc[3], SB1, PB1);
+        epi(acc[2], SA0, PA0);
+        epi(acc[3], SB0, PB0);
+    }
+
+    if constexpr (VAR == 33) {
+        // VAR 32 with the MFMAs as inline asm writing AGPRs (acc file); the epilogue reads them through
+        // v_accvgpr_read (compiler-inserted), results consumed two bursts later (wait states long met)
+        const int wr = wave & 1, wt = (wave >> 1) & 1;
+        const int t0 = 64 * wt + c, t1 = 64 * wt + 32 + c, row = 32 * wr + c;
+        i32x16 SA0 = {}, SA1 = {}, SB0 = {}, SB1 = {};
+        f32x16 PA0 = fz, PA1 = fz, PB0 = fz, PB1 = fz;
+        const i32x4 bb = rdB(0, row), a0 = rdA(0, t0), a1 = rdA(0, t1);
+        const uint32_t w = rdSW(0, row), x0 = rdSX(0, t0), x1 = rdSX(0, t1);
+        const u32x4 as = {x0, 0u, 0u, 0u}, bs = {w, 0u, 0u, 0u}, as1 = {x1, 0u, 0u, 0u};
+        auto mf = [&](const i32x4 &a, const u32x4 &sx, i32x16 &S, f32x16 &P) __attribute__((always_inline)) {
+            asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 0" : "=a"(S) : "v"(a), "v"(bb));
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=a"(P) : "v"(sx), "v"(bs));
+        };
+        auto epc = [&](float *acc_, const i32x16 &S, const f32x16 &P) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc_[i] = fmaf((float)S[i], P[i], acc_[i]);
+        };
+        auto step = [&](i32x16 &Sa, f32x16 &Pa, i32x16 &Sb, f32x16 &Pb, i32x16 &Sa_, f32x16 &Pa_, i32x16 &Sb_,
+                        f32x16 &Pb_) __attribute__((always_inline)) {
+            mf(a0, as, Sa, Pa);
+            mf(a1, as1, Sb, Pb);
+            epc(acc[0], Sa_, Pa_);
+            epc(acc[1], Sb_, Pb_);
+        };
+        for (int b = 0; b < nblk; b += 2) {
+            step(SA0, PA0, SB0, PB0, SA1, PA1, SB1, PB1);
+            step(SA1, PA1, SB1, PB1, SA0, PA0, SB0, PB0);
+        }
+        asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+        epc(acc[2], SA1, PA1);
+        epc(acc[3], SB1, PB1);
+    }
+
+    if constexpr (VAR == 35) {
+        // scale product on the VALU (P = d_x * d_w from fp32 LDS values: no scale MFMA), and the
+        // MFMA results drained (int -> float) BEFORE the next block's MFMAs are issued, so that the
+        // VALU that overlaps the MFMA burst (the P products and the fmas) reads no MFMA-written register
+        const int wr = wave & 1, wt = (wave >> 1) & 1;
+        const int t0 = 64 * wt + c, t1 = 64 * wt + 32 + c, row = 32 * wr + c;
+        const i32x16 iz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        i32x16 S0 = iz, S1 = iz;
+        float F0[16], F1[16];
+        i32x4 bb = rdB(0, row), a0 = rdA(0, t0), a1 = rdA(0, t1);
+        for (int b = 0; b < nblk; b++) {
+            // drain the previous block's sums (the wave waits here once for its burst)
+#pragma unroll
+            for (int i = 0; i < 16; i++) F0[i] = (float)S0[i], F1[i] = (float)S1[i];
+            __builtin_amdgcn_sched_barrier(0);
+            S0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bb, iz, 0, 0, 0);
+            S1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bb, iz, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            // next operands + this (previous) block's scales, then the fmas
+            const float dw = __uint_as_float(0x3a000000u | rdSW(b - 1, row));
+            const float *xd = sx32 + ((b - 1) & (R - 1)) * BN;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const f32x4 d0 = *(const f32x4 *)(xd + 64 * wt + 8 * g + 4 * h);
+                const f32x4 d1 = *(const f32x4 *)(xd + 64 * wt + 32 + 8 * g + 4 * h);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    acc[0][4 * g + j] = fmaf(F0[4 * g + j], d0[j] * dw, acc[0][4 * g + j]);
+                    acc[1][4 * g + j] = fmaf(F1[4 * g + j], d1[j] * dw, acc[1][4 * g + j]);
+                }
+            }
+            bb = rdB(b + 1, row), a0 = rdA(b + 1, t0), a1 = rdA(b + 1, t1);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc[2][i] += (float)S0[i] + (float)S1[i];
+    }
     float s = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; t++)
@@ -614,12 +724,14 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&out, 4096 * 512 * 4));
     CK(hipMemcpy(src, h.data(), LDS, hipMemcpyHostToDevice));
     // waves per SIMD = waves/WG x WG/CU / 4 where registers allow
-    run<1>("VAR1 2 tiles/wave", 4, 2, src, out, nblk, 2);
-    run<1>("VAR1 2 tiles/wave", 4, 2, src, out, nblk, 3);
-    run<21>("VAR21 = 1 + carried scale operands", 4, 2, src, out, nblk, 2);
-    run<21>("VAR21 = 1 + carried scale operands", 4, 2, src, out, nblk, 3);
-    run<22>("VAR22 = 21 + packed f32 epilogue", 4, 2, src, out, nblk, 2);
-    run<22>("VAR22 = 21 + packed f32 epilogue", 4, 2, src, out, nblk, 3);
-    run<18>("VAR18 = 15 + MFMA/VALU interleave", 4, 2, src, out, nblk, 2);
+    run<8>("VAR8 MFMA only, chained C=D", 4, 2, src, out, nblk, 2);
+    run<30>("VAR30 MFMA only, C const, fresh D", 4, 2, src, out, nblk, 2);
+    run<12>("VAR12 MFMA chained + independent VALU", 4, 2, src, out, nblk, 2);
+    run<31>("VAR31 2 sets, epi on other set, D=C", 4, 2, src, out, nblk, 2);
+    run<32>("VAR32 2 sets, epi on other set, C const", 4, 2, src, out, nblk, 2);
+    run<9>("VAR9 VALU only", 4, 2, src, out, nblk, 2);
+    run<35>("VAR35 VALU scale, drain before burst", 4, 2, src, out, nblk, 1);
+    run<35>("VAR35 VALU scale, drain before burst", 4, 2, src, out, nblk, 2);
+    run<35>("VAR35 VALU scale, drain before burst", 4, 2, src, out, nblk, 3);
     return 0;
 }

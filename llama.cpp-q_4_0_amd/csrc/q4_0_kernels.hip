@@ -1807,14 +1807,21 @@ static_assert(G8_W / 1024 == 4 * G8_LOADERS && G8_X / 1024 == 8 * G8_LOADERS, "l
 static_assert(4 * 2 * 16 * 64 * 4 <= G8_NS * G8_STAGE, "the partial-tile exchange fits in the ring");
 
 // x: one lane per 4 floats (8 lanes per block, k_quantize_q8_0's lane code), written block-major.
-__global__ __launch_bounds__(256) void k_prep8_x(const float *__restrict__ x, int64_t K, int64_t total8,
+// Wave w of a workgroup takes block b = 4*blockIdx.x + w of 8 consecutive tokens (lanes 8j..8j+7 =
+// token n0 + j), so its 8 image blocks are adjacent (one 256-byte store run) and each 8-lane group
+// reads one 128-byte line of its token's row.  (The first version enumerated blocks along a token:
+// each wave stored 8 separate 32-byte pieces Np*32 bytes apart: 7.1 -> 6.0 us mean over the bench's
+// launches.  Four blocks per wave with their loads in flight together measured no faster: the launch
+// is ~3 us of fixed cost + 10 MB of streaming at K = 4096.)
+__global__ __launch_bounds__(256) void k_prep8_x(const float *__restrict__ x, int64_t K, int64_t N,
                                                   int8_t *__restrict__ ximg, uint16_t *__restrict__ xd16, int64_t Np) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= total8) return;
     const int64_t nb = K / QK;
-    const int64_t blk = t >> 3, n = blk / nb, b = blk - n * nb;
-    const int sub = (int)(t & 7);
-    const float4 v = *reinterpret_cast<const float4 *>(x + t * 4);
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.y * 8 + (lane >> 3);
+    if (b >= nb || n >= N) return;                          // whole 8-lane groups exit together
+    const int sub = lane & 7;
+    const float4 v = *reinterpret_cast<const float4 *>(x + n * K + b * QK + 4 * sub);
     uint32_t d16;
     int qsum;
     const uint32_t packed = q8_block_lane(v, d16, qsum);
@@ -2065,13 +2072,14 @@ size_t gemm8_x_bytes(int64_t K, int64_t N) { return (size_t)(K / QK) * gemm8_np(
 size_t gemm8_w_bytes(int64_t K, int64_t M) { return (size_t)((M + 63) / 64) * (K / QK) * 64 * 34; }
 
 hipError_t gemm8_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStream_t s) {
-    const int64_t total8 = N * (K / QK) * 8;
-    if (total8 == 0) return hipSuccess;
+    const int64_t nb = K / QK;
+    if (N <= 0 || nb <= 0) return hipSuccess;
+    if ((N + 7) / 8 > 65535) return hipErrorInvalidValue;          // grid.y limit
     const int64_t Np = gemm8_np(N);
     int8_t *ximg = (int8_t *)xws;
-    uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)(K / QK) * Np * 32);
+    uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)nb * Np * 32);
     (void)hipGetLastError();
-    launch_k(k_prep8_x, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, s, x, K, total8, ximg, xd16, Np);
+    launch_k(k_prep8_x, dim3((unsigned)((nb + 3) / 4), (unsigned)((N + 7) / 8)), dim3(256), 0, s, x, K, N, ximg, xd16, Np);
     return hipGetLastError();
 }
 

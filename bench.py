@@ -569,26 +569,40 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0,
 
     nbytes = sum(q4_bytes(K, m) + 4 * K * N + 4 * m * N for _, K, M, m, _, _ in mats)
     ops = sum(2 * K * m * N for _, K, M, m, _, _ in mats)
-    # default path: each weight's int8 image built once, as the hook does on a resident weight's first
-    # prefill (ggml_hip_weight_image_create; DESIGN.md §4 k_gemm8), then k_gemm8 per call
-    for _, K, M, m, buf, _ in mats:
-        gh.check(L.ggml_hip_weight_image_create(buf.ptr, K, m, stream))
-    image_bytes = L.ggml_hip_weight_image_bytes()
-    try:
-        t = timed()
-    finally:
-        for _, K, M, m, buf, _ in mats:
-            L.ggml_hip_weight_image_free(buf.ptr)
+    # default path: each weight's image built once, as the hook does on a resident weight's first
+    # prefill (ggml_hip_weight_image_create): fp6 images + k_gemm9 (GEMM version 10, the
+    # default); for comparison the int8 images + k_gemm8 (version 8) and no image (k_gemm7 on the q4_0
+    # bytes in place)
+    def with_images(version):
+        gh.check(L.ggml_hip_debug_set_gemm_version(version))
+        try:
+            for _, K, M, m, buf, _ in mats:
+                gh.check(L.ggml_hip_weight_image_create(buf.ptr, K, m, stream))
+            nbytes_img = L.ggml_hip_weight_image_bytes()
+            try:
+                return timed(), nbytes_img
+            finally:
+                for _, K, M, m, buf, _ in mats:
+                    L.ggml_hip_weight_image_free(buf.ptr)
+        finally:
+            gh.check(L.ggml_hip_debug_set_gemm_version(-1))
+
+    t, image_bytes = with_images(10)
+    t8, image_bytes8 = with_images(8)
     t7 = timed()                                      # no images: k_gemm7 on the q4_0 bytes in place
+
+    def alt(kernel, tt):
+        return {"kernel": kernel, "ms_per_layer": round(tt / layers * 1e3, 4), "TOPs": round(ops / tt / 1e12, 1),
+                "mfma_frac": round(ops / tt / 1e12 / INT8_PEAK_TOPS, 4)}
     return {"tokens": N, "layers": layers, "ms_per_layer": round(t / layers * 1e3, 4),
             "GBps": round(nbytes / t / 1e9, 1), "TOPs": round(ops / t / 1e12, 1),
             "mfma_frac": round(ops / t / 1e12 / INT8_PEAK_TOPS, 4), "peak_TOPs": INT8_PEAK_TOPS,
             "stack_7B_prefill_ms": round(t / layers * 32 * 1e3, 3),
-            "kernel": "k_gemm8_q4_0 on per-weight int8 images built once (34 B per 32 weights; image bytes "
-                      f"{image_bytes} for {layers} layers)",
-            "q4_0_in_place": {"kernel": "k_gemm7_q4_0 (no image: the q4_0 blocks read in place)",
-                              "ms_per_layer": round(t7 / layers * 1e3, 4), "TOPs": round(ops / t7 / 1e12, 1),
-                              "mfma_frac": round(ops / t7 / 1e12 / INT8_PEAK_TOPS, 4)}}
+            "kernel": "k_gemm9_q4_0: exact block sums on the block-scaled fp6 MFMA, per-weight e2m3 images built "
+                      f"once (26 B per 32 weights; image bytes {image_bytes} for {layers} layers)",
+            "int8_images": alt("k_gemm8_q4_0: i8 MFMA on per-weight int8 images (34 B per 32 weights; image bytes "
+                               f"{image_bytes8})", t8),
+            "q4_0_in_place": alt("k_gemm7_q4_0 (no image: the q4_0 blocks read in place)", t7)}
 
 
 def _cpu_name():

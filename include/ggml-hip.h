@@ -161,13 +161,15 @@ int ggml_hip_get_exact(void);
  * capturing a HIP graph). */
 int ggml_hip_reserve_workspace(int64_t K, int64_t N);
 /* The same for prefill mul_mats (N > 128) of matrices up to M rows: the LDS GEMM also keeps a per-call
- * int8 image of the weights in the workspace (34 bytes per 32 weights). */
+ * image of the weights in the workspace (up to 34 bytes per 32 weights). */
 int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M);
 
-/* Prefill weight images (no ggml-cuda.h counterpart).  The LDS GEMM (N > 128) runs fastest on an int8
- * image of the weight (w = nibble - 8, fp16 d verbatim; 34 B per 32 weights, 1.9x the q4_0 bytes):
- * create builds it once (stream-ordered, outside capture) and every later prefill mul_mat of that device
- * pointer with the same K, M uses it; without one the GEMM reads the q4_0 bytes directly.  The weight
+/* Prefill weight images (no ggml-cuda.h counterpart).  The LDS GEMM (N > 128) runs fastest on an image
+ * of the weight: by default fp6 (e2m3 codes of w/2, w = nibble - 8, fp16 d verbatim; 26 B per 32
+ * weights, 1.44x the q4_0 bytes; the exact block sums on the block-scaled fp6 MFMA, k_gemm9), under GEMM
+ * version 8 int8 (34 B per 32 weights, k_gemm8; bitwise the same results): create builds it once
+ * (stream-ordered, outside capture) and every later prefill mul_mat of that device pointer with the
+ * same K, M uses it; without one the GEMM reads the q4_0 bytes directly.  The weight
  * must not change while its image exists (free it first).  Device-resident ggml weights
  * (transform_tensor, the residency cache) get their image on their first prefill use, dropped with the
  * buffer.  Results are identical either way in exact arithmetic per block; the fp32 accumulation order
@@ -175,8 +177,9 @@ int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M);
 int ggml_hip_weight_image_create(const void *dev_w, int64_t K, int64_t M, void *stream);
 int ggml_hip_weight_image_free(const void *dev_w);        /* number of images dropped */
 int64_t ggml_hip_weight_image_bytes(void);                  /* device bytes held by images */
-/* test hook: prefill GEMM version 7 (q4_0 bytes), 8 (image when registered, default), 9 (image always,
- * built per call into the workspace when unregistered); -1 = GGML_HIP_GEMM_V */
+/* test hook: prefill GEMM version 7 (q4_0 bytes), 8 / 10 (int8 / fp6 images built on registration, the
+ * GEMM of the image when one exists; 10 is the default), 9 / 11 (k_gemm8 / k_gemm9 always, an
+ * unregistered weight converted per call into the workspace); -1 = GGML_HIP_GEMM_V */
 int ggml_hip_debug_set_gemm_version(int v);
 
 /* ------------------------------------------------------------------------------------------

@@ -201,20 +201,27 @@ size_t ws_d16_offset(int64_t K, int64_t N) {
     return qs + (((size_t)N * (K / QK) * 4 + 255) & ~(size_t)255);
 }
 size_t workspace_bytes(int64_t K, int64_t N) { return ws_d16_offset(K, N) + (size_t)((N + 3) & ~3) * (K / QK) * 2; }
-// the LDS GEMM (algo 2, v8) adds its x image and the per-call int8 weight image of an M-row matrix
+// the LDS GEMM (algo 2, v8 / v9) adds its x image and the per-call weight image of an M-row matrix (room
+// for either image format)
 size_t ws_g8x_offset(int64_t K, int64_t N) { return (workspace_bytes(K, N) + 255) & ~(size_t)255; }
-size_t ws_g8w_offset(int64_t K, int64_t N) { return (ws_g8x_offset(K, N) + ghip::gemm8_x_bytes(K, N) + 255) & ~(size_t)255; }
-size_t workspace_bytes_mm(int64_t K, int64_t N, int64_t M) { return ws_g8w_offset(K, N) + ghip::gemm8_w_bytes(K, M); }
-// prefill GEMM version (GGML_HIP_GEMM_V / ggml_hip_debug_set_gemm_version): 8 (default) = k_gemm8 when
-// the weight has an int8 image (ggml_hip_weight_image_create, or built on first prefill use of a
-// device-resident ggml weight), else k_gemm7 on the q4_0 bytes; 9 = k_gemm8 always (an unregistered
-// weight is converted into the workspace per call); 7 = k_gemm7 always
+size_t ws_g8w_offset(int64_t K, int64_t N) {
+    return (ws_g8x_offset(K, N) + std::max(ghip::gemm8_x_bytes(K, N), ghip::gemm9_x_bytes(K, N)) + 255) & ~(size_t)255;
+}
+size_t workspace_bytes_mm(int64_t K, int64_t N, int64_t M) {
+    return ws_g8w_offset(K, N) + std::max(ghip::gemm8_w_bytes(K, M), ghip::gemm9_w_bytes(K, M));
+}
+// prefill GEMM version (GGML_HIP_GEMM_V / ggml_hip_debug_set_gemm_version): 10 (default) = k_gemm9 when
+// the weight has an image (ggml_hip_weight_image_create, or built on first prefill use of a
+// device-resident ggml weight; images are built in fp6 format), else k_gemm7 on the q4_0 bytes; 8 = the
+// same with int8 images (k_gemm8); 9 / 11 = k_gemm8 / k_gemm9 always (an unregistered weight is
+// converted into the workspace per call); 7 = k_gemm7 always.  A weight's image keeps the format it
+// was built in; the GEMM follows the image.
 std::atomic<int> g_gemm_v{-1};
 int gemm_version() {
     int v = g_gemm_v.load(std::memory_order_relaxed);
     if (v < 0) {
         const char *e = getenv("GGML_HIP_GEMM_V");
-        int want = e ? atoi(e) : 8, expect = -1;
+        int want = e ? atoi(e) : 10, expect = -1;
         g_gemm_v.compare_exchange_strong(expect, want);
         v = g_gemm_v.load(std::memory_order_relaxed);
     }
@@ -231,15 +238,19 @@ struct WImage {
     int64_t K, M;
     void *img;
     size_t bytes;
+    int fmt;                                                 // 8: int8 (k_gemm8), 9: fp6 (k_gemm9)
 };
+int image_format() { return gemm_version() >= 10 ? 9 : 8; }
 std::mutex g_wi_mu;
 std::map<std::pair<int, uintptr_t>, WImage> g_wi;          // (device, weight address)
 int64_t g_wi_resident = 0;
 
-const void *wimage_find(int id, const void *w, int64_t K, int64_t M) {
+const void *wimage_find(int id, const void *w, int64_t K, int64_t M, int *fmt = nullptr) {
     std::lock_guard<std::mutex> lk(g_wi_mu);
     auto it = g_wi.find({id, (uintptr_t)w});
-    return it != g_wi.end() && it->second.K == K && it->second.M == M ? it->second.img : nullptr;
+    if (it == g_wi.end() || it->second.K != K || it->second.M != M) return nullptr;
+    if (fmt) *fmt = it->second.fmt;
+    return it->second.img;
 }
 
 // build (stream-ordered on s) unless present; returns the image or nullptr on failure
@@ -252,12 +263,13 @@ const void *wimage_ensure(int id, const void *w, int64_t K, int64_t M, hipStream
         g_wi_resident -= (int64_t)it->second.bytes;
         g_wi.erase(it);
     }
-    WImage im{K, M, nullptr, ghip::gemm8_w_bytes(K, M)};
+    const int fmt = image_format();
+    WImage im{K, M, nullptr, fmt == 9 ? ghip::gemm9_w_bytes(K, M) : ghip::gemm8_w_bytes(K, M), fmt};
     if (hipMalloc(&im.img, im.bytes) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
-    if (ghip::gemm8_prep_w(w, K, M, im.img, s) != hipSuccess) {
+    if ((fmt == 9 ? ghip::gemm9_prep_w(w, K, M, im.img, s) : ghip::gemm8_prep_w(w, K, M, im.img, s)) != hipSuccess) {
         (void)GHIP_SYNC(hipFree)(im.img);
         return nullptr;
     }
@@ -525,7 +537,7 @@ bool exact_mode() {
 // xq: in/out mask of the q8_0(x) forms already in this stream's workspace from the previous call
 // (siblings that share x: ggml_hip_mul_mat_q4_0_multi quantizes once per form): XQ_SOA = qs + d (split-K,
 // exact, gemm7), XQ_G8 = the k_gemm8 x image; null = quantize; ignored by the fused GEMV
-enum { XQ_SOA = 1, XQ_G8 = 2 };
+enum { XQ_SOA = 1, XQ_G8 = 2, XQ_G9 = 4 };
 int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, float *y, int64_t ldy, int algo,
                 hipStream_t s, unsigned *xq = nullptr) {
     unsigned xq_local = 0;
@@ -551,19 +563,23 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
     if (algo < 2 || algo > 4) return fail(GGML_HIP_ERR_INVALID, "algo must be 0, 1, 2, 3 or 4");
     void *ws = nullptr;
     const int gv = gemm_version();
-    const void *wimg = algo == 2 && gv >= 8 ? wimage_find(id, w, K, M) : nullptr;
-    if (algo == 2 && (wimg || gv == 9)) {      // k_gemm8: x image + int8 weight image
+    int fmt = 0;
+    const void *wimg = algo == 2 && gv >= 8 ? wimage_find(id, w, K, M, &fmt) : nullptr;
+    if (algo == 2 && (wimg || gv == 9 || gv == 11)) {   // k_gemm8 / k_gemm9 on weight + x images
+        if (!wimg) fmt = gv == 11 ? 9 : 8;
         const int wrc = stream_workspace(id, s, workspace_bytes_mm(K, N, wimg ? 0 : M), &ws);
         if (wrc != GGML_HIP_OK) return wrc;
         void *xws = (char *)ws + ws_g8x_offset(K, N);
-        if (!(*xq & XQ_G8)) HIP_RET(ghip::gemm8_prep_x(x, K, N, xws, s));
-        *xq |= XQ_G8;
+        const unsigned form = fmt == 9 ? XQ_G9 : XQ_G8;        // one x image region: the forms exclude
+        if (!(*xq & form))
+            HIP_RET(fmt == 9 ? ghip::gemm9_prep_x(x, K, N, xws, s) : ghip::gemm8_prep_x(x, K, N, xws, s));
+        *xq = (*xq & ~(unsigned)(XQ_G8 | XQ_G9)) | form;
         if (!wimg) {                            // unregistered weight: converted per call
             void *wws = (char *)ws + ws_g8w_offset(K, N);
-            HIP_RET(ghip::gemm8_prep_w(w, K, M, wws, s));
+            HIP_RET(fmt == 9 ? ghip::gemm9_prep_w(w, K, M, wws, s) : ghip::gemm8_prep_w(w, K, M, wws, s));
             wimg = wws;
         }
-        HIP_RET(ghip::gemm8_run(wimg, K, M, xws, N, y, ldy, s));
+        HIP_RET(fmt == 9 ? ghip::gemm9_run(wimg, K, M, xws, N, y, ldy, s) : ghip::gemm8_run(wimg, K, M, xws, N, y, ldy, s));
         return GGML_HIP_OK;
     }
     const int wrc = stream_workspace(id, s, workspace_bytes(K, N), &ws);
@@ -1895,7 +1911,8 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
             }
             // prefill (the LDS GEMM, N > 128) of a resident weight: build its int8 image once (k_gemm8;
             // a failure to allocate it leaves k_gemm7 on the q4_0 bytes)
-            if (w_resident && N > 128 && !exact_mode() && gemm_version() == 8) (void)wimage_ensure(id, w, K, rows, s);
+            if (w_resident && N > 128 && !exact_mode() && (gemm_version() == 8 || gemm_version() == 10))
+                (void)wimage_ensure(id, w, K, rows, s);
             // activations
             const float *x;
             const size_t xbytes = (size_t)N * K * 4;
@@ -2358,7 +2375,7 @@ int64_t ggml_hip_weight_image_bytes(void) {
 }
 
 int ggml_hip_debug_set_gemm_version(int v) {
-    if (v != -1 && v != 7 && v != 8 && v != 9) return fail(GGML_HIP_ERR_INVALID, "version must be 7, 8, 9 or -1");
+    if (v != -1 && (v < 7 || v > 11)) return fail(GGML_HIP_ERR_INVALID, "version must be 7 ... 11 or -1");
     g_gemm_v.store(v, std::memory_order_relaxed);
     if (v == -1) (void)gemm_version();            // re-read GGML_HIP_GEMM_V
     return GGML_HIP_OK;

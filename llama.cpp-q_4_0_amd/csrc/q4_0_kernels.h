@@ -85,6 +85,16 @@ hipError_t gemm8_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStre
 hipError_t gemm8_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStream_t s);
 hipError_t gemm8_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
                      hipStream_t s);
+// Prefill GEMM v9: the same block sums on the block-scaled fp6 MFMA (e2m3 images: weights w/2,
+// x split into (q >> 4)/2 and (q & 15)/2; 26 B per 32 weights, 50 B per 32 activations), bitwise
+// equal to v8.
+int64_t gemm9_np(int64_t N);
+size_t gemm9_x_bytes(int64_t K, int64_t N);
+size_t gemm9_w_bytes(int64_t K, int64_t M);
+hipError_t gemm9_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStream_t s);
+hipError_t gemm9_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStream_t s);
+hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
+                     hipStream_t s);
 
 // Small / medium N (split-K over the waves of a 32x32-tile workgroup, operands straight to registers).
 hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,

@@ -2132,6 +2132,420 @@ hipError_t gemm8_run(const void *wws, int64_t K, int64_t M, const void *xws, int
 }
 
 // ---------------------------------------------------------------------------------------------
+// Prefill GEMM v9: the exact per-block integer sum on the block-scaled fp6 matrix cores
+// (v_mfma_scale_f32_32x32x64_f8f6f4, e2m3 operands, tools/fp6_check.hip: 0 mismatches over 262k
+// outputs).  Why: gemm8's compute phase is bound by its epilogue, which first converts each i8
+// MFMA's int32 block sums to float (16 VALU per tile and block) before the scale fma; the fp6
+// instruction returns the same integer already as an f32 (every partial sum an integer < 2^24, so
+// exact), which leaves the epilogue one fma per output (tools/gemm_mb.hip VAR36 vs VAR21: 172 vs 210
+// cycles per tile-block on the same box, although the fp6 instruction takes twice the i8 one's cycles).
+// Operand encoding (every value exact in e2m3 = 1 sign, 2 exponent, 3 mantissa bits, |v| <= 7.5):
+//   weights  w = nibble - 8 in [-8, 7] as w/2, block scale 2^1, in both K halves of the instruction;
+//   x        the q8_0 value q in [-128, 127] split as q = 16*(q >> 4) + (q & 15): K half 0 holds
+//            (q >> 4)/2 with scale 2^5, K half 1 holds (q & 15)/2 with scale 2^1,
+// so one 32x32x64 instruction = sum_k w*16*(q >> 4) + w*(q & 15) = sum_k w*q, the block's sumi.
+// The epilogue acc = fma(S, d_x*d_w, acc) gives bit for bit gemm8's values (same integer, same scale
+// product, same block order and workgroup-half split).
+// Images (32 codes x 6 bits = 24 B per row and block, element j at bits 6j..6j+5, stored as a 16-byte
+// and an 8-byte part so that every operand read is one ds_read_b128 + one ds_read_b64 on 16/8-byte
+// strides, bank-conflict free): weights [M/128][nb][128 rows x 16 B | 128 rows x 8 B] + fp16 d_w
+// [M/128][nb][128] (26 B per 32 weights: 1.44x the q4_0 bytes); x [nb][3][Np][16 B]: part 0 = the
+// first 16 B of the (q >> 4) codes, part 1 = those of the (q & 15) codes, part 2 = the last 8 B of
+// both (swapped for tokens with bit 4 set: the b64 reads of a half-wave cover all 64 banks) + fp16
+// d_x [nb][Np].
+// Tile 128 weight rows x 64 tokens (the stage is 51 KB like gemm8's, ring of 3); wave q of half g
+// owns tokens 32(q&1).. and rows 64(q>>1) + {0, 32} (the x operand shared by its two tiles).
+static constexpr int G9_BM = 128, G9_BN = 64, G9_KB = 8, G9_NS = 3, G9_LOADERS = 4;
+static constexpr int G9_THREADS = (8 + G9_LOADERS) * 64;
+static constexpr int G9_WB = G9_BM * 24;                          // weight codes per block   3 KB
+static constexpr int G9_XB = G9_BN * 48;                          // x codes per block        3 KB
+static constexpr int G9_W = G9_KB * G9_WB;                        // 24 KB
+static constexpr int G9_X = G9_KB * G9_XB;                        // 24 KB
+static constexpr int G9_WD = G9_KB * G9_BM * 2;                   // fp16 d_w                 2 KB
+static constexpr int G9_XD = G9_KB * G9_BN * 2;                   // fp16 d_x                 1 KB
+static constexpr int G9_STAGE = G9_W + G9_X + G9_WD + G9_XD;      // 51 KB
+static constexpr int G9_ZERO = 256;
+static constexpr int G9_LDS = G9_NS * G9_STAGE + G9_ZERO;         // 153.25 KB
+static constexpr int G9_OPS = 15;                                  // DMA instructions per loader wave per stage
+static_assert(G9_WB == 3 * 1024 && G9_XB == 3 * 1024, "3 x 1 KiB DMAs per block and operand");
+static_assert(4 * 2 * 16 * 64 * 4 <= G9_NS * G9_STAGE, "the partial-tile exchange fits in the ring");
+static constexpr int G9_SCALE_1 = 128, G9_SCALE_5 = 132;           // E8M0 block scales 2^1, 2^5
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// e2m3 code of n/2 for an integer n in [-15, 15]
+__device__ __forceinline__ uint32_t e2m3_half(int n) {
+    const uint32_t a = (uint32_t)(n < 0 ? -n : n);
+    const uint32_t c = a < 4 ? 4 * a : a < 8 ? 8 + 2 * a : 16 + a;
+    return (n < 0 ? 0x20u : 0u) | c;
+}
+// four 6-bit codes (elements 4m .. 4m+3) as one 24-bit field
+__device__ __forceinline__ uint32_t f6x4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    return c0 | (c1 << 6) | (c2 << 12) | (c3 << 18);
+}
+// 32 codes = fields F0..F7 (24 bits each) -> 6 dwords, element j at bits 6j..6j+5
+__device__ __forceinline__ void f6_pack(const uint32_t *F, uint32_t *D) {
+    D[0] = F[0] | (F[1] << 24);
+    D[1] = (F[1] >> 8) | (F[2] << 16);
+    D[2] = (F[2] >> 16) | (F[3] << 8);
+    D[3] = F[4] | (F[5] << 24);
+    D[4] = (F[5] >> 8) | (F[6] << 16);
+    D[5] = (F[6] >> 16) | (F[7] << 8);
+}
+
+// x: the q8_0 lane code of k_prep8_x (8 lanes per block, wave = 8 tokens of one block); each lane's
+// four q give four (q >> 4) and four (q & 15) codes (24 bits each), and lanes 0-5 of the group
+// assemble the block's six dwords of each half from their neighbours' fields.
+__global__ __launch_bounds__(256) void k_prep9_x(const float *__restrict__ x, int64_t K, int64_t N,
+                                                  uint8_t *__restrict__ ximg, uint16_t *__restrict__ xd16, int64_t Np) {
+    const int64_t nb = K / QK;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.y * 8 + (lane >> 3);
+    if (b >= nb) return;                                    // wave-uniform
+    const bool live = n < N;
+    const int sub = lane & 7;
+    float4 v = {0.f, 0.f, 0.f, 0.f};
+    if (live) v = *reinterpret_cast<const float4 *>(x + n * K + b * QK + 4 * sub);
+    uint32_t d16;
+    int qsum;
+    const uint32_t packed = q8_block_lane(v, d16, qsum);
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const int q = (int)(int8_t)(packed >> (8 * e));
+        hi[e] = e2m3_half(q >> 4);
+        lo[e] = e2m3_half(q & 15);
+    }
+    const uint32_t Fh = f6x4(hi[0], hi[1], hi[2], hi[3]), Fl = f6x4(lo[0], lo[1], lo[2], lo[3]);
+    // dword k of a half: fields s and s + 1 shifted by off (k = 0..5 -> (s, off) = (0,0) (1,8) (2,16)
+    // (4,0) (5,8) (6,16))
+    const int k = sub < 6 ? sub : 5;
+    const int s = k < 3 ? k : k + 1, off = 8 * (k % 3);
+    const int base = lane & ~7;
+    const uint32_t h0 = (uint32_t)__shfl((int)Fh, base + s), h1 = (uint32_t)__shfl((int)Fh, base + s + 1);
+    const uint32_t l0 = (uint32_t)__shfl((int)Fl, base + s), l1 = (uint32_t)__shfl((int)Fl, base + s + 1);
+    if (!live || sub >= 6) return;
+    const uint32_t dh = (h0 >> off) | (h1 << (24 - off)), dl = (l0 >> off) | (l1 << (24 - off));
+    const int sw = (int)((n >> 4) & 1);
+    uint32_t *p0 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 0) * Np + n) * 16);
+    uint32_t *p1 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 1) * Np + n) * 16);
+    uint32_t *p2 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 2) * Np + n) * 16);
+    if (k < 4) {
+        p0[k] = dh;
+        p1[k] = dl;
+    } else {
+        p2[2 * sw + k - 4] = dh;
+        p2[2 * (sw ^ 1) + k - 4] = dl;
+    }
+    if (sub == 0) xd16[b * Np + n] = (uint16_t)d16;
+}
+
+// weights: one lane per (row, block pair), 128 consecutive rows of one pair per 128 lanes; rows >= M
+// of the last tile are zeros (d = 0)
+__global__ __launch_bounds__(256) void k_prep9_w(const uint8_t *__restrict__ W, int64_t rowbytes, int nb, int M,
+                                                  uint8_t *__restrict__ wimg, uint16_t *__restrict__ wd16) {
+    const int r = threadIdx.x & 127;
+    const int64_t item = (int64_t)blockIdx.x * 2 + (threadIdx.x >> 7);     // (row tile, pair)
+    const int npair = nb >> 1;
+    const int64_t rt = item / npair;
+    const int p = (int)(item - rt * npair);
+    const int64_t row = rt * 128 + r;
+    if (rt * 128 >= M) return;
+    u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
+    uint32_t c = 0u;
+    const bool live = row < M;
+    if (live) {
+        const uint8_t *src = W + row * rowbytes + (int64_t)p * 36;
+        a = *reinterpret_cast<const u32x4 *>(src);
+        b = *reinterpret_cast<const u32x4 *>(src + 16);
+        c = *reinterpret_cast<const uint32_t *>(src + 32);
+    }
+    const uint32_t e[4] = {__builtin_amdgcn_alignbyte(a.y, a.x, 2), __builtin_amdgcn_alignbyte(a.z, a.y, 2),
+                           __builtin_amdgcn_alignbyte(a.w, a.z, 2), __builtin_amdgcn_alignbyte(b.x, a.w, 2)};
+    const uint32_t o[4] = {b.y, b.z, b.w, c};
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+        const uint32_t *q = kk ? o : e;
+        uint32_t F[8];
+#pragma unroll
+        for (int m = 0; m < 8; m++) {                   // elements 4m..4m+3: m < 4 low nibbles, else high
+            const uint32_t word = q[m & 3], sh = m < 4 ? 0u : 4u;
+            uint32_t cc[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) cc[t] = live ? e2m3_half((int)((word >> (8 * t + sh)) & 15u) - 8) : 0u;
+            F[m] = f6x4(cc[0], cc[1], cc[2], cc[3]);
+        }
+        uint32_t D[6];
+        f6_pack(F, D);
+        const int64_t blk = rt * nb + 2 * p + kk;
+        *reinterpret_cast<u32x4 *>(wimg + blk * G9_WB + r * 16) = u32x4{D[0], D[1], D[2], D[3]};
+        *reinterpret_cast<u32x2 *>(wimg + blk * G9_WB + 2048 + r * 8) = u32x2{D[4], D[5]};
+        const uint32_t d = kk ? (b.x >> 16) : (a.x & 0xFFFFu);
+        wd16[blk * 128 + r] = (uint16_t)(live ? d : 0u);
+    }
+}
+
+// DIAG (timing knockouts, results invalid): 1 no compute, 2 no DMA, 3 no DMA and no barrier
+// VAR bits (A/B knobs, bitwise-identical results): 1 operands read right before their block (no
+// prefetch), 2 packed f32 epilogue (v_pk_fma_f32), 4 two named operand sets read one block ahead
+// (ping-pong, no copies)
+template <int DIAG, int VAR = 0>
+__global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const uint8_t *__restrict__ wimg,
+                                                               const uint16_t *__restrict__ wd16, int nb, int M,
+                                                               const uint8_t *__restrict__ ximg,
+                                                               const uint16_t *__restrict__ xd16, int64_t Np, int N,
+                                                               float *__restrict__ y, int64_t ldy) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *zero = smem + G9_NS * G9_STAGE;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 31, h = lane >> 5;
+    const int rt = blockIdx.x;
+    const int m0 = rt * G9_BM, n0 = blockIdx.y * G9_BN;
+    if (tid < G9_ZERO / 4) reinterpret_cast<uint32_t *>(zero)[tid] = 0u;
+
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(wimg + (int64_t)rt * nb * G9_WB, (uint32_t)nb * G9_WB);
+    const __amdgpu_buffer_rsrc_t wdrs = make_rsrc(wd16 + (int64_t)rt * nb * G9_BM, (uint32_t)nb * G9_BM * 2u);
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(ximg, (uint32_t)((int64_t)nb * Np * 48));
+    const __amdgpu_buffer_rsrc_t xdrs = make_rsrc(xd16, (uint32_t)((int64_t)nb * Np * 2));
+    const __amdgpu_buffer_rsrc_t nul = make_rsrc(wimg, 0);
+
+    // loader wave l = wave - 8 moves blocks 2l, 2l+1 of every stage: weights and x 3 x 1 KiB each per
+    // block, d_w 256 B per block, d_x of both blocks in one instruction (lanes 32-63: the second) = 15
+    const int lw = wave - 8;
+    const int lb = 2 * lw;
+    auto issue = [&](int st) __attribute__((always_inline)) {
+        if (DIAG >= 2 || wave < 8) return;
+        uint8_t *base = smem + (st % G9_NS) * G9_STAGE;
+        const int kb0 = st * G9_KB;
+        const bool v = kb0 + lb < nb;                                             // nb even: both or none
+        const __amdgpu_buffer_rsrc_t wr_ = v ? wrs : nul, xr_ = v ? xrs : nul, dr_ = v ? xdrs : nul,
+                                     wdr_ = v ? wdrs : nul;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int b = lb + j;
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wr_, (lds_void_t *)(base + b * G9_WB + r * 1024), 16,
+                                                         (kb0 + b) * G9_WB + r * 1024 + lane * 16, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xr_, (lds_void_t *)(base + G9_W + b * G9_XB + r * 1024), 16,
+                                                         (int)((((int64_t)(kb0 + b) * 3 + r) * Np + n0) * 16) + lane * 16,
+                                                         0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wdr_, (lds_void_t *)(base + G9_W + G9_X + b * 256), 4,
+                                                     (kb0 + b) * 256 + lane * 4, 0, 0, 0);
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(dr_, (lds_void_t *)(base + G9_W + G9_X + G9_WD + lb * 128), 4,
+                                                 (int)(((int64_t)(kb0 + lb + h) * Np + n0) * 2) + c * 4, 0, 0, 0);
+    };
+
+    const int g = (wave >> 2) & 1, q = wave & 3;
+    const int tt = 32 * (q & 1) + c;                       // this lane's token (A operand row) in the tile
+    const int r0 = 64 * (q >> 1) + c, r1 = r0 + 32;        // this lane's weight rows (B operand columns)
+    const int xo16 = h * 1024 + tt * 16, xo8 = 2048 + tt * 16 + 8 * (h ^ ((tt >> 4) & 1));
+    const int sa = h ? G9_SCALE_1 : G9_SCALE_5;
+    const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    float acc0[16], acc1[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc0[i] = acc1[i] = 0.0f;
+    f32x16 S0 = fz, S1 = fz, P0 = fz, P1 = fz;
+    u32x4 as = {0u, 0u, 0u, 0u}, bs0 = {0u, 0u, 0u, 0u}, bs1 = {0u, 0u, 0u, 0u};
+    auto epi = [&](float *a, const f32x16 &S, const f32x16 &P) __attribute__((always_inline)) {
+        if constexpr (VAR & 2) {
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                const f32x2 sv = {S[i], S[i + 1]}, pv = {P[i], P[i + 1]};
+                f32x2 av = {a[i], a[i + 1]};
+                av = __builtin_elementwise_fma(sv, pv, av);
+                a[i] = av.x;
+                a[i + 1] = av.y;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) a[i] = fmaf(S[i], P[i], a[i]);
+        }
+    };
+    struct Ops {
+        i32x8 ax, bw0, bw1;
+        uint32_t sx, sw0, sw1;
+    };
+    auto rd24 = [&](const uint8_t *p16, const uint8_t *p8) __attribute__((always_inline)) {
+        const u32x4 u = *reinterpret_cast<const u32x4 *>(p16);
+        const u32x2 v = *reinterpret_cast<const u32x2 *>(p8);
+        const i32x8 r = {(int)u.x, (int)u.y, (int)u.z, (int)u.w, (int)v.x, (int)v.y, 0, 0};
+        return r;
+    };
+    auto rd = [&](int st, int b) __attribute__((always_inline)) {
+        const uint8_t *base = smem + (st % G9_NS) * G9_STAGE;
+        const uint8_t *xb = base + G9_W + b * G9_XB, *wb = base + b * G9_WB;
+        Ops o;
+        o.ax = rd24(xb + xo16, xb + xo8);
+        o.bw0 = rd24(wb + r0 * 16, wb + 2048 + r0 * 8);
+        o.bw1 = rd24(wb + r1 * 16, wb + 2048 + r1 * 8);
+        const uint16_t *wd = reinterpret_cast<const uint16_t *>(h ? zero : base + G9_W + G9_X + b * 256);
+        o.sw0 = wd[h ? 0 : r0];
+        o.sw1 = wd[h ? 0 : r1];
+        o.sx = reinterpret_cast<const uint16_t *>(base + G9_W + G9_X + G9_WD + b * 128)[tt];
+        return o;
+    };
+    auto block = [&](const Ops &o) __attribute__((always_inline)) {
+        as.x = o.sx;
+        bs0.x = o.sw0;
+        bs1.x = o.sw1;
+        // the previous block's epilogues, then this block's four MFMAs back to back (gemm8's VAR 7 order)
+        epi(acc0, S0, P0);
+        epi(acc1, S1, P1);
+        __builtin_amdgcn_sched_barrier(0);
+        S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw0, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+        P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs0), fz, 0, 0, 0);
+        S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw1, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+        P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs1), fz, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto sync = [&]() __attribute__((always_inline)) {
+        if (DIAG == 3) return;
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((G9_NS - 2) * G9_OPS) : "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+
+    const int nstages = (nb + G9_KB - 1) / G9_KB;
+#pragma unroll
+    for (int st = 0; st < G9_NS - 1; st++) issue(st);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((G9_NS - 2) * G9_OPS) : "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int s = 0; s < nstages; s++) {
+        issue(s + G9_NS - 1);
+        const int kb = s * G9_KB + 4 * g;
+        if (DIAG != 1 && wave < 8) {
+            if constexpr (VAR & 4) {
+                // nb even and kb even: blocks come in valid pairs
+                if (kb < nb) {
+                    Ops oa = rd(s, 4 * g), ob = rd(s, 4 * g + 1);
+                    block(oa);
+                    const bool more = kb + 2 < nb;
+                    if (more) oa = rd(s, 4 * g + 2);
+                    block(ob);
+                    if (more) {
+                        ob = rd(s, 4 * g + 3);
+                        block(oa);
+                        block(ob);
+                    }
+                }
+            } else if constexpr (VAR & 1) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (kb + j < nb) block(rd(s, 4 * g + j));
+            } else {
+                Ops o = rd(s, 4 * g);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (kb + j >= nb) break;
+                    Ops nx = o;
+                    if (j < 3) nx = rd(s, 4 * g + j + 1);
+                    block(o);
+                    o = nx;
+                }
+            }
+        }
+        sync();
+    }
+    epi(acc0, S0, P0);
+    epi(acc1, S1, P1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(smem);
+    if (wave >= 4 && wave < 8) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+            *reinterpret_cast<float4 *>(red + ((i / 4) * 256 + q * 64 + lane) * 4) = {acc0[i], acc0[i + 1], acc0[i + 2], acc0[i + 3]};
+            *reinterpret_cast<float4 *>(red + ((4 + i / 4) * 256 + q * 64 + lane) * 4) = {acc1[i], acc1[i + 1], acc1[i + 2], acc1[i + 3]};
+        }
+    }
+    __syncthreads();
+    if (wave < 4) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+            const float4 o0 = *reinterpret_cast<const float4 *>(red + ((i / 4) * 256 + q * 64 + lane) * 4);
+            const float4 o1 = *reinterpret_cast<const float4 *>(red + ((4 + i / 4) * 256 + q * 64 + lane) * 4);
+            acc0[i] += o0.x; acc0[i + 1] += o0.y; acc0[i + 2] += o0.z; acc0[i + 3] += o0.w;
+            acc1[i] += o1.x; acc1[i + 1] += o1.y; acc1[i + 2] += o1.z; acc1[i + 3] += o1.w;
+        }
+        const int row0 = m0 + r0, row1 = m0 + r1;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int tk = n0 + 32 * (q & 1) + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (tk < N) {
+                if (row0 < M) y[(int64_t)tk * ldy + row0] = acc0[i];
+                if (row1 < M) y[(int64_t)tk * ldy + row1] = acc1[i];
+            }
+        }
+    }
+}
+
+int64_t gemm9_np(int64_t N) { return (N + 3) & ~(int64_t)3; }
+size_t gemm9_x_bytes(int64_t K, int64_t N) { return (size_t)(K / QK) * gemm9_np(N) * 50; }
+size_t gemm9_w_bytes(int64_t K, int64_t M) { return (size_t)((M + 127) / 128) * (K / QK) * 128 * 26; }
+
+hipError_t gemm9_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStream_t s) {
+    const int64_t nb = K / QK;
+    if (N <= 0 || nb <= 0) return hipSuccess;
+    if ((N + 7) / 8 > 65535) return hipErrorInvalidValue;
+    const int64_t Np = gemm9_np(N);
+    uint8_t *ximg = (uint8_t *)xws;
+    uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)nb * Np * 48);
+    (void)hipGetLastError();
+    launch_k(k_prep9_x, dim3((unsigned)((nb + 3) / 4), (unsigned)((N + 7) / 8)), dim3(256), 0, s, x, K, N, ximg, xd16, Np);
+    return hipGetLastError();
+}
+
+hipError_t gemm9_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStream_t s) {
+    const int nb = (int)(K / QK);
+    const int64_t Mt = (M + 127) / 128;
+    uint8_t *wimg = (uint8_t *)wws;
+    uint16_t *wd16 = (uint16_t *)((char *)wws + (size_t)Mt * nb * G9_WB);
+    (void)hipGetLastError();
+    const int64_t items = Mt * (nb / 2);                  // (row tile, pair) items, 2 per 256-thread block
+    launch_k(k_prep9_w, dim3((unsigned)((items + 1) / 2)), dim3(256), 0, s, (const uint8_t *)W, (int64_t)nb * Q4B, nb,
+             (int)M, wimg, wd16);
+    return hipGetLastError();
+}
+
+hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
+                     hipStream_t s) {
+    const int nb = (int)(K / QK);
+    const int64_t Mt = (M + 127) / 128, Np = gemm9_np(N);
+    const uint8_t *wimg = (const uint8_t *)wws;
+    const uint16_t *wd16 = (const uint16_t *)((const char *)wws + (size_t)Mt * nb * G9_WB);
+    const uint8_t *ximg = (const uint8_t *)xws;
+    const uint16_t *xd16 = (const uint16_t *)((const char *)xws + (size_t)nb * Np * 48);
+    if ((int64_t)nb * Np * 48 >= ((int64_t)1 << 31) || (int64_t)nb * G9_WB >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<1, 1>,
+                       k_gemm9_q4_0<2, 1>, k_gemm9_q4_0<3, 1>}) {
+            hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
+            if (e != hipSuccess) return e;
+        }
+        attr = true;
+    }
+    static const int diag = env_int("GGML_HIP_GEMM_DIAG", 0);
+    // GGML_HIP_GEMM9_VAR (A/B, tools/r3_g9var.sh, kernel medians, 2 interleaved rounds): 0 (prefetch one
+    // block ahead through a copied operand set) 32.6-32.9 us at 4096x4096x512, 1 (no prefetch, default)
+    // 25.9-26.0, 2 / 3 (packed epilogue) 38.5-38.7 / 26.7-26.8; k_gemm8 29.3-29.5 on the same boxes
+    static const int var = env_int("GGML_HIP_GEMM9_VAR", 1);
+    auto kern = diag == 91 ? k_gemm9_q4_0<1, 1> : diag == 92 ? k_gemm9_q4_0<2, 1> : diag == 93 ? k_gemm9_q4_0<3, 1>
+              : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : k_gemm9_q4_0<0, 1>;
+    (void)hipGetLastError();
+    launch_k(kern, dim3((unsigned)Mt, (unsigned)((N + G9_BN - 1) / G9_BN)), dim3(G9_THREADS), G9_LDS, s, wimg, wd16,
+             nb, (int)M, ximg, xd16, Np, (int)N, y, ldy);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Split-K MFMA GEMM for small / medium token counts (9 <= N <= 128 by default).
 //
 // The LDS-staged GEMM above runs (M/64) x ceil(N/128) workgroups that each walk all of K, so for

@@ -83,8 +83,8 @@ def test_offloaded_weight_falcon_golden(ref):
 @pytest.mark.parametrize("K,M,N,offload", [(4096, 256, 32, 0), (4096, 512, 64, 0), (11008, 128, 48, 1),
                                            (4096, 300, 512, 1), (4544, 4672 // 8, 33, 0)])
 def test_prefill_through_ggml(ref, K, M, N, offload):
-    """Prefill through ggml's own hooks; an offloaded weight at N > 128 gets its int8 image on first use
-    (k_gemm8), released with the tensor by ggml_cuda_free_data."""
+    """Prefill through ggml's own hooks; an offloaded weight at N > 128 gets its weight image on first use
+    (fp6, k_gemm9, under the default GEMM version), released with the tensor by ggml_cuda_free_data."""
     from hip_env import ggml_hip
     L = ggml_hip.load()
     before = L.ggml_hip_weight_image_bytes()

@@ -590,17 +590,26 @@ def test_weight_cache_invalidate_and_full_verify():
         ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
 
 
-# ------------------------------------------------------------------------------- prefill GEMM v8 (int8 images)
+# ---------------------------------------------------- prefill GEMM v8 (int8 images) and v9 (fp6 images)
 def _gemm_version(v):
     ggml_hip.check(ggml_hip.load().ggml_hip_debug_set_gemm_version(v), "gemm version")
 
 
+GEMM_PER_CALL = {8: 9, 10: 11}          # image version -> the version that builds that image per call
+
+
+def _image_bytes(K, M, v):
+    return (M + 63) // 64 * 64 * K // 32 * 34 if v == 8 else (M + 127) // 128 * 128 * K // 32 * 26
+
+
+@pytest.mark.parametrize("v", [9, 11], ids=["gemm8-int8", "gemm9-fp6"])
 @pytest.mark.parametrize("K,M,N", [s for s in EDGE_SHAPES if s[2] > 8] + [(4544, 4672 // 8, 130), (128, 1, 200)])
-def test_gemm8_per_call_image_vs_oracle(K, M, N):
-    """k_gemm8 with the weight converted into the workspace per call (version 9): ragged M (images padded
-    to 64 rows with d = 0), ragged N, K = 64 (one half-stage), K = 4544 (a partial last stage)."""
+def test_gemm8_per_call_image_vs_oracle(K, M, N, v):
+    """k_gemm8 / k_gemm9 with the weight converted into the workspace per call (version 9 / 11): ragged M
+    (images padded to 64 / 128 rows with d = 0), ragged N, K = 64 (one half-stage), K = 4544 (a partial
+    last stage)."""
     wq, x = make_case(K, M, N, seed=K * 3 + M + N)
-    _gemm_version(9)
+    _gemm_version(v)
     try:
         y, _ = gpu_mul_mat(wq, K, x, algo=2)
     finally:
@@ -610,24 +619,68 @@ def test_gemm8_per_call_image_vs_oracle(K, M, N):
     check_y(y, O.mul_mat(wq, K, x, nthreads=4), s_abs, RTOL, ATOL_BLOCKS)
 
 
+@pytest.mark.parametrize("K,M,N", [s for s in EDGE_SHAPES if s[2] > 8] +
+                         [(4544, 4672, 130), (128, 1, 200), (4096, 4096, 512), (11008, 4096, 300), (4096, 11008, 257)])
+def test_gemm9_fp6_bitwise_equals_gemm8_int8(K, M, N):
+    """The fp6 block sums (v_mfma_scale_f32_32x32x64_f8f6f4 on e2m3 images, k_gemm9) are the same integers
+    as the i8 MFMA's, and the two kernels share the block order, the workgroup-half K split and the scale
+    product: y is bitwise equal, at edge shapes and full LLaMA-7B prefill shapes (q8_0 values over the
+    whole int8 range, so the (q >> 4, q & 15) split sees every code)."""
+    wq, x = make_case(K, M, N, seed=K * 5 + M + N)
+    ys = {}
+    try:
+        for v in (9, 11):
+            _gemm_version(v)
+            ys[v], _ = gpu_mul_mat(wq, K, x, algo=2)
+    finally:
+        _gemm_version(-1)
+    assert np.array_equal(ys[9].view(np.uint32), ys[11].view(np.uint32))
+
+
+def test_gemm9_fp6_extreme_blocks_exact():
+    """Blocks whose q8_0 values hit -128 / 127 / 0 and whose nibbles are all 0 (w = -8) or all 15 (w = 7):
+    the largest block sums (|sumi| = 32 * 8 * 128) and every e2m3 code at its extremes, against the oracle."""
+    K, M, N = 256, 64, 160
+    rng = np.random.default_rng(7)
+    w = rng.standard_normal((M, K)).astype(np.float32) * 0.02
+    w[:8] = -1.0                                        # d = +0.125: all nibbles 0 -> w = -8
+    w[8:16] = np.where(np.arange(K) % 32 == 0, -1.0, 0.875).astype(np.float32)
+    wq, _ = O.quantize_q4_0(w)
+    x = rng.standard_normal((N, K)).astype(np.float32)
+    x[:8] = 1.0
+    x[8:16] = -1.0
+    x[16:24, ::2] = 0.0
+    xq = O.quantize_q8_0(x, "avx2")
+    _gemm_version(11)
+    try:
+        y, _ = gpu_mul_mat(wq, K, x, algo=2)
+    finally:
+        _gemm_version(-1)
+    _, s_abs = block_terms(wq, xq, K)
+    check_y(y, O.mul_mat(wq, K, x, nthreads=4), s_abs, RTOL, ATOL_BLOCKS)
+
+
+@pytest.mark.parametrize("v", [8, 10], ids=["int8-image", "fp6-image"])
 @pytest.mark.parametrize("K,M", [(4096, 4096), (11008, 4096)])
-def test_gemm8_registered_image_prefill_512(K, M):
-    """A registered int8 image (ggml_hip_weight_image_create) is used by every later prefill call of that
-    weight: bitwise equal to the per-call image, within the bound of the oracle at full LLaMA-7B shape,
-    x -> 2x bitwise; freeing the image returns the GEMM to the q4_0 bytes (k_gemm7)."""
+def test_gemm8_registered_image_prefill_512(K, M, v):
+    """A registered weight image (ggml_hip_weight_image_create; int8 under version 8, fp6 under the
+    default 10) is used by every later prefill call of that weight: bitwise equal to the per-call image,
+    within the bound of the oracle at full LLaMA-7B shape, x -> 2x bitwise; freeing the image returns the
+    GEMM to the q4_0 bytes (k_gemm7)."""
     L = ggml_hip.load()
     wq, x = make_case(K, M, 512, seed=11 * K + M)
     wd, xd = DB.from_array(wq), DB.from_array(x)
     yd = DB(512 * M * 4)
     before = L.ggml_hip_weight_image_bytes()
+    _gemm_version(v)
     ggml_hip.check(L.ggml_hip_weight_image_create(wd.ptr, K, M, None), "image")
-    assert L.ggml_hip_weight_image_bytes() - before == (M + 63) // 64 * 64 * K // 32 * 34
+    assert L.ggml_hip_weight_image_bytes() - before == _image_bytes(K, M, v)
     try:
         ggml_hip.mul_mat(wd, K, M, xd, 512, yd, algo=2)
         y_img = yd.download((512, M), np.float32)
-        _gemm_version(9)
+        _gemm_version(GEMM_PER_CALL[v])
         y_call, _ = gpu_mul_mat(wq, K, x, algo=2)
-        _gemm_version(-1)
+        _gemm_version(v)
         assert np.array_equal(y_img.view(np.uint32), y_call.view(np.uint32))
         xq = O.quantize_q8_0(x, "avx2")
         y_ref = O.mul_mat(wq, K, x, nthreads=8, mode="avx2", pool=True)
@@ -646,16 +699,21 @@ def test_gemm8_registered_image_prefill_512(K, M):
 
 
 def test_gemm8_mixed_sibling_group_bitwise():
-    """A sibling group (one x quantization per form) where only some weights have images: the k_gemm8
-    and k_gemm7 siblings each read their own x form, bitwise equal to separate calls."""
+    """A sibling group (one x quantization per form) where the weights have an fp6 image, an int8 image,
+    none, and an fp6 image again: the k_gemm9, k_gemm8 and k_gemm7 siblings each read their own x form (the
+    fp6 and int8 x images share one region, rewritten when the form changes), bitwise equal to separate
+    calls."""
     L = ggml_hip.load()
     K, N = 4096, 200
-    Ms = [256, 128, 300]
+    Ms = [256, 128, 300, 192]
     cases = [make_case(K, M, N, seed=60 + i) for i, M in enumerate(Ms)]
     x = cases[0][1]
     wds = [DB.from_array(c[0]) for c in cases]
-    ggml_hip.check(L.ggml_hip_weight_image_create(wds[1].ptr, K, Ms[1], None), "image")
     try:
+        for i, v in ((0, 10), (1, 8), (3, 10)):
+            _gemm_version(v)
+            ggml_hip.check(L.ggml_hip_weight_image_create(wds[i].ptr, K, Ms[i], None), "image")
+        _gemm_version(-1)
         xd = DB.from_array(x)
         ys = [DB(N * M * 4) for M in Ms]
         ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
@@ -665,11 +723,14 @@ def test_gemm8_mixed_sibling_group_bitwise():
             assert np.array_equal(yd.download((N, M), np.float32).view(np.uint32),
                                   single.download((N, M), np.float32).view(np.uint32))
         xq = O.quantize_q8_0(x, "avx2")
-        _, s_abs = block_terms(cases[1][0], xq, K)
-        check_y(ys[1].download((N, Ms[1]), np.float32), O.mul_mat(cases[1][0], K, x, nthreads=4), s_abs, RTOL,
-                ATOL_BLOCKS)
+        for i in (0, 1):
+            _, s_abs = block_terms(cases[i][0], xq, K)
+            check_y(ys[i].download((N, Ms[i]), np.float32), O.mul_mat(cases[i][0], K, x, nthreads=4), s_abs, RTOL,
+                    ATOL_BLOCKS)
     finally:
-        L.ggml_hip_weight_image_free(wds[1].ptr)
+        _gemm_version(-1)
+        for i in (0, 1, 3):
+            L.ggml_hip_weight_image_free(wds[i].ptr)
 
 
 def test_gemm8_image_api_errors():
@@ -680,3 +741,4 @@ def test_gemm8_image_api_errors():
     assert L.ggml_hip_weight_image_create(None, 128, 64, None) == ggml_hip.ERR_INVALID
     assert L.ggml_hip_weight_image_free(wd.ptr) == 0
     assert L.ggml_hip_debug_set_gemm_version(5) == ggml_hip.ERR_INVALID
+    assert L.ggml_hip_debug_set_gemm_version(12) == ggml_hip.ERR_INVALID

@@ -10,6 +10,9 @@
 //   2  VAR 1 with sched_group_barrier interleaving (1 MFMA : 8 VALU)
 //   3  VAR 0 with the scale product by VALU (16 v_mul_f32 from fp32 d_x read 4 at a time)
 //   4  4 tiles per wave (2 row x 2 token), 1 MFMA chain set per tile
+//   (... 5-35: see the variant comments)
+//   36 VAR21 with the block sum from the block-scaled fp6 MFMA (f32 result: no conversion), 37 its MFMAs
+//      alone; 38 / 39 four independent chains of fp6 / i8 MFMAs only (issue rate of each instruction)
 // Usage: gemm_mb [nblk]; prints us per launch and cycles per (tile x block) per SIMD at 2.4 GHz.
 #include <hip/hip_runtime.h>
 
@@ -679,6 +682,77 @@ __global__ __launch_bounds__(512, 2) void k_mb(const uint8_t *src, float *out, i
 #pragma unroll
         for (int i = 0; i < 16; i++) acc[2][i] += (float)S0[i] + (float)S1[i];
     }
+
+    if constexpr (VAR == 36 || VAR == 37 || VAR == 38 || VAR == 39 || VAR == 40 || VAR == 41) {
+        // VAR21 with the block sum from the block-scaled fp6 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4,
+        // e2m3 operands: w/2 and [x_hi/2 | x_lo/2] with power-of-two block scales -> the exact integer
+        // sum as an f32, no conversion in the epilogue): 36 with the epilogue, 37 MFMAs only
+        typedef int i32x8 __attribute__((ext_vector_type(8)));
+        const int wr = wave & 1, wt = (wave >> 1) & 1;
+        const int t0 = 64 * wt + c, t1 = 64 * wt + 32 + c, row = 32 * wr + c;
+        f32x16 S0 = fz, S1 = fz;
+        f32x16 P0 = fz, P1 = fz;
+        u32x4 as0 = {0u, 0u, 0u, 0u}, as1 = {0u, 0u, 0u, 0u}, bs = {0u, 0u, 0u, 0u};
+        const uint32_t *sx32w = (const uint32_t *)sx16;
+        auto rd6 = [&](int off) __attribute__((always_inline)) {
+            const i32x4 u = *(const i32x4 *)(lds + off);
+            const int2 v = *(const int2 *)(lds + off + 16);
+            const i32x8 r = {u.x, u.y, u.z, u.w, v.x, v.y, 0, 0};
+            return r;
+        };
+        auto epi3 = [&](float *a, const f32x16 &S, const f32x16 &P) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) a[i] = fmaf(S[i], P[i], a[i]);
+        };
+        const int sa = 128, sb = VAR == 40 ? (h ? 128 : 132) : 127 + 4;
+        for (int b = 0; b < nblk; b++) {
+            const int rb = (b & (R - 1));
+            const i32x8 bb = rd6(LA + rb * BM * 32 + (row & 15) * 48 + 24 * h);
+            bs.x = rdSW(b, row);
+            const i32x8 a0 = rd6(rb * BN * 32 + (t0 & 31) * 96 + 48 * h);
+            const i32x8 a1 = rd6(rb * BN * 32 + (t1 & 31) * 96 + 48 * h + 3072);
+            as0.x = sx32w[(rb * BN + t0) >> 1];
+            as1.x = sx32w[(rb * BN + t1) >> 1];
+            if constexpr (VAR == 36 || VAR == 40) {
+                S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, fz, 2, 2, 0, sb, 0, sa);
+                P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as0), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+                epi3(acc[1], S1, P1);
+                S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, fz, 2, 2, 0, sb, 0, sa);
+                P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as1), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+                epi3(acc[0], S0, P0);
+            } else if constexpr (VAR == 41) {          // VAR36 with the roles of A and B swapped (B shared)
+                S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bb, a0, fz, 2, 2, 0, sa, 0, sb);
+                P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as0), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+                epi3(acc[1], S1, P1);
+                S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bb, a1, fz, 2, 2, 0, sa, 0, sb);
+                P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as1), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+                epi3(acc[0], S0, P0);
+            } else if constexpr (VAR == 38) {          // fp6 only, 4 chains
+                S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, S0, 2, 2, 0, sb, 0, sa);
+                S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, S1, 2, 2, 0, sb, 0, sa);
+                P0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, P0, 2, 2, 0, sb, 0, sa);
+                P1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, P1, 2, 2, 0, sb, 0, sa);
+            } else if constexpr (VAR == 39) {          // i8 only, 4 chains
+                i32x16 *SI = (i32x16 *)&S0, *SJ = (i32x16 *)&S1, *PI = (i32x16 *)&P0, *PJ = (i32x16 *)&P1;
+                const i32x4 x0 = {a0.x, a0.y, a0.z, a0.w}, x1 = {a1.x, a1.y, a1.z, a1.w}, w4 = {bb.x, bb.y, bb.z, bb.w};
+                *SI = __builtin_amdgcn_mfma_i32_32x32x32_i8(x0, w4, *SI, 0, 0, 0);
+                *SJ = __builtin_amdgcn_mfma_i32_32x32x32_i8(x1, w4, *SJ, 0, 0, 0);
+                *PI = __builtin_amdgcn_mfma_i32_32x32x32_i8(x0, w4, *PI, 0, 0, 0);
+                *PJ = __builtin_amdgcn_mfma_i32_32x32x32_i8(x1, w4, *PJ, 0, 0, 0);
+            } else {
+                S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, S0, 2, 2, 0, sb, 0, sa);
+                P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as0), __builtin_bit_cast(half8, bs), P0, 0, 0, 0);
+                S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, S1, 2, 2, 0, sb, 0, sa);
+                P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as1), __builtin_bit_cast(half8, bs), P1, 0, 0, 0);
+            }
+        }
+        if constexpr (VAR == 36 || VAR == 40 || VAR == 41) {
+            epi3(acc[1], S1, P1);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc[0][i] += S0[i] + S1[i] + P0[i] + P1[i];
+        }
+    }
     float s = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; t++)
@@ -716,22 +790,19 @@ void run(const char *name, int waves, int tiles_per_wave, const uint8_t *src, fl
 
 int main(int argc, char **argv) {
     const int nblk = argc > 1 ? atoi(argv[1]) : 2048;
+    const int fill = argc > 2 ? atoi(argv[2]) : 0;     // 0 hash bytes, 1 zeros, 2 0x41 bytes, 3 0x08 bytes
     std::vector<uint8_t> h(LDS);
-    for (size_t i = 0; i < h.size(); i++) h[i] = (uint8_t)((i * 2654435761u) >> 13);
+    for (size_t i = 0; i < h.size(); i++)
+        h[i] = fill == 1 ? 0 : fill == 2 ? 0x41 : fill == 3 ? 0x08 : (uint8_t)((i * 2654435761u) >> 13);
     uint8_t *src;
     float *out;
     CK(hipMalloc(&src, LDS));
     CK(hipMalloc(&out, 4096 * 512 * 4));
     CK(hipMemcpy(src, h.data(), LDS, hipMemcpyHostToDevice));
     // waves per SIMD = waves/WG x WG/CU / 4 where registers allow
-    run<8>("VAR8 MFMA only, chained C=D", 4, 2, src, out, nblk, 2);
-    run<30>("VAR30 MFMA only, C const, fresh D", 4, 2, src, out, nblk, 2);
-    run<12>("VAR12 MFMA chained + independent VALU", 4, 2, src, out, nblk, 2);
-    run<31>("VAR31 2 sets, epi on other set, D=C", 4, 2, src, out, nblk, 2);
-    run<32>("VAR32 2 sets, epi on other set, C const", 4, 2, src, out, nblk, 2);
-    run<9>("VAR9 VALU only", 4, 2, src, out, nblk, 2);
-    run<35>("VAR35 VALU scale, drain before burst", 4, 2, src, out, nblk, 1);
-    run<35>("VAR35 VALU scale, drain before burst", 4, 2, src, out, nblk, 2);
-    run<35>("VAR35 VALU scale, drain before burst", 4, 2, src, out, nblk, 3);
+    printf("fill %d\n", fill);
+    run<21>("VAR21 i8 2 tiles/wave (gemm8 structure)", 4, 2, src, out, nblk, 2);
+    run<36>("VAR36 fp6 block sum, f32 epilogue (no cvt)", 4, 2, src, out, nblk, 2);
+    run<38>("VAR38 fp6 x2 per tile-blk, 4 chains", 4, 2, src, out, nblk, 2);
     return 0;
 }

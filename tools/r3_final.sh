@@ -29,17 +29,17 @@ i=0
 IFS='|' read -ra sets <<< "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES|SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA|SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU|SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS|FETCH_SIZE|WRITE_SIZE|GRBM_GUI_ACTIVE SQ_INSTS_SALU"
 for c in "${sets[@]}"; do
   i=$((i+1))
-  GGML_HIP_GEMM_V=9 GGML_HIP_GEMM_DIAG=0 step gpmc$i 90 rocprofv3 --pmc $c -d $O/gpmc/p$i -o run --output-format csv -- python3 tools/gemm_stamps.py
+  GGML_HIP_GEMM_V=11 GGML_HIP_GEMM_DIAG=0 step gpmc$i 90 rocprofv3 --pmc $c -d $O/gpmc/p$i -o run --output-format csv -- python3 tools/gemm_stamps.py
 done
-python3 - <<'PY' > $O/gemm_pmc.txt
+python3 - <<'PY' > $O/gemm9_pmc.txt
 import csv, glob, collections
 tot = collections.defaultdict(list)
 for f in glob.glob("gpurun_out/r03/gpmc/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "k_gemm8" in r.get("Kernel_Name", ""):
+        if "k_gemm9" in r.get("Kernel_Name", ""):
             tot[r["Counter_Name"]].append(float(r["Counter_Value"]))
-print("k_gemm8_q4_0 (per-call image, GGML_HIP_GEMM_V=9), K=M=4096, N=512; mean per dispatch")
+print("k_gemm9_q4_0 (per-call fp6 image, GGML_HIP_GEMM_V=11), K=M=4096, N=512; mean per dispatch")
 for k, v in sorted(tot.items()):
     print(f"{k:28s} n={len(v):3d} mean={sum(v)/len(v):.4g}")
 PY
-cat $O/gemm_pmc.txt
+cat $O/gemm9_pmc.txt

@@ -2289,7 +2289,8 @@ __global__ __launch_bounds__(256) void k_prep9_w(const uint8_t *__restrict__ W, 
 // DIAG (timing knockouts, results invalid): 1 no compute, 2 no DMA, 3 no DMA and no barrier
 // VAR bits (A/B knobs, bitwise-identical results): 1 operands read right before their block (no
 // prefetch), 2 packed f32 epilogue (v_pk_fma_f32), 4 two named operand sets read one block ahead
-// (ping-pong, no copies)
+// (ping-pong, no copies), 8 loader waves stage through registers (buffer_load_dwordx4 -> ds_write_b128)
+// instead of LDS-DMA
 template <int DIAG, int VAR = 0>
 __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const uint8_t *__restrict__ wimg,
                                                                const uint16_t *__restrict__ wd16, int nb, int M,
@@ -2340,6 +2341,45 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const uint8_t *__r
         }
         __builtin_amdgcn_raw_ptr_buffer_load_lds(dr_, (lds_void_t *)(base + G9_W + G9_X + G9_WD + lb * 128), 4,
                                                  (int)(((int64_t)(kb0 + lb + h) * Np + n0) * 2) + c * 4, 0, 0, 0);
+    };
+    // VAR & 8: the same bytes through the loader waves' registers (loaded one stage ahead of the write)
+    u32x4 stg[12];
+    uint32_t stg_dw[2], stg_dx = 0u;
+    auto load_regs = [&](int st) __attribute__((always_inline)) {
+        if (DIAG >= 2 || wave < 8) return;
+        const int kb0 = st * G9_KB;
+        const bool v = kb0 + lb < nb;
+        const __amdgpu_buffer_rsrc_t wr_ = v ? wrs : nul, xr_ = v ? xrs : nul, dr_ = v ? xdrs : nul,
+                                     wdr_ = v ? wdrs : nul;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int b = lb + j;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                stg[6 * j + r] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                               wr_, (kb0 + b) * G9_WB + r * 1024 + lane * 16, 0, 0));
+                stg[6 * j + 3 + r] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                               xr_, (int)((((int64_t)(kb0 + b) * 3 + r) * Np + n0) * 16) + lane * 16, 0, 0));
+            }
+            stg_dw[j] = __builtin_amdgcn_raw_buffer_load_b32(wdr_, (kb0 + b) * 256 + lane * 4, 0, 0);
+        }
+        stg_dx = __builtin_amdgcn_raw_buffer_load_b32(dr_, (int)(((int64_t)(kb0 + lb + h) * Np + n0) * 2) + c * 4, 0, 0);
+    };
+    auto store_regs = [&](int st) __attribute__((always_inline)) {
+        if (DIAG >= 2 || wave < 8) return;
+        uint8_t *base = smem + (st % G9_NS) * G9_STAGE;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int b = lb + j;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                *reinterpret_cast<u32x4 *>(base + b * G9_WB + r * 1024 + lane * 16) = stg[6 * j + r];
+                *reinterpret_cast<u32x4 *>(base + G9_W + b * G9_XB + r * 1024 + lane * 16) = stg[6 * j + 3 + r];
+            }
+            *reinterpret_cast<uint32_t *>(base + G9_W + G9_X + b * 256 + lane * 4) = stg_dw[j];
+        }
+        *reinterpret_cast<uint32_t *>(base + G9_W + G9_X + G9_WD + lb * 128 + lane * 4) = stg_dx;
     };
 
     const int g = (wave >> 2) & 1, q = wave & 3;
@@ -2408,15 +2448,47 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const uint8_t *__r
     };
     auto sync = [&]() __attribute__((always_inline)) {
         if (DIAG == 3) return;
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((G9_NS - 2) * G9_OPS) : "memory");
+        if constexpr (VAR & 8)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((G9_NS - 2) * G9_OPS) : "memory");
         __builtin_amdgcn_s_barrier();
     };
 
     const int nstages = (nb + G9_KB - 1) / G9_KB;
+    if constexpr (!(VAR & 8)) {
 #pragma unroll
-    for (int st = 0; st < G9_NS - 1; st++) issue(st);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((G9_NS - 2) * G9_OPS) : "memory");
-    __builtin_amdgcn_s_barrier();
+        for (int st = 0; st < G9_NS - 1; st++) issue(st);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((G9_NS - 2) * G9_OPS) : "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    if constexpr (VAR & 8) {
+        // separate code per role (the staging registers are not live in the compute loop), the same
+        // barriers in each: one after the prologue, one per stage
+        if (wave >= 8) {
+            load_regs(0);
+            store_regs(0);
+            load_regs(1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            for (int s = 0; s < nstages; s++) {
+                store_regs(s + 1);           // loaded during the previous stage (slot of stage s - 2: free)
+                load_regs(s + 2);
+                sync();
+            }
+        } else {
+            __builtin_amdgcn_s_barrier();
+            for (int s = 0; s < nstages; s++) {
+                const int kb = s * G9_KB + 4 * g;
+                if (DIAG != 1) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (kb + j < nb) block(rd(s, 4 * g + j));
+                }
+                sync();
+            }
+        }
+    } else
     for (int s = 0; s < nstages; s++) {
         issue(s + G9_NS - 1);
         const int kb = s * G9_KB + 4 * g;
@@ -2525,8 +2597,8 @@ hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     if ((int64_t)nb * Np * 48 >= ((int64_t)1 << 31) || (int64_t)nb * G9_WB >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
-        for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<1, 1>,
-                       k_gemm9_q4_0<2, 1>, k_gemm9_q4_0<3, 1>}) {
+        for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<0, 9>,
+                       k_gemm9_q4_0<1, 1>, k_gemm9_q4_0<2, 1>, k_gemm9_q4_0<3, 1>, k_gemm9_q4_0<1, 9>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
             if (e != hipSuccess) return e;
         }
@@ -2538,7 +2610,9 @@ hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     // 25.9-26.0, 2 / 3 (packed epilogue) 38.5-38.7 / 26.7-26.8; k_gemm8 29.3-29.5 on the same boxes
     static const int var = env_int("GGML_HIP_GEMM9_VAR", 1);
     auto kern = diag == 91 ? k_gemm9_q4_0<1, 1> : diag == 92 ? k_gemm9_q4_0<2, 1> : diag == 93 ? k_gemm9_q4_0<3, 1>
-              : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : k_gemm9_q4_0<0, 1>;
+              : diag == 94 ? k_gemm9_q4_0<1, 9>
+              : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : var == 9 ? k_gemm9_q4_0<0, 9>
+              : k_gemm9_q4_0<0, 1>;
     (void)hipGetLastError();
     launch_k(kern, dim3((unsigned)Mt, (unsigned)((N + G9_BN - 1) / G9_BN)), dim3(G9_THREADS), G9_LDS, s, wimg, wd16,
              nb, (int)M, ximg, xd16, Np, (int)N, y, ldy);

@@ -2286,7 +2286,8 @@ __global__ __launch_bounds__(256) void k_prep9_w(const uint8_t *__restrict__ W, 
     }
 }
 
-// DIAG (timing knockouts, results invalid): 1 no compute, 2 no DMA, 3 no DMA and no barrier
+// DIAG (timing knockouts, results invalid): 1 no compute, 2 no DMA, 3 no DMA and no barrier, 4 / 5 no
+// x / no weight DMA (the other operand still streams)
 // VAR bits (A/B knobs, bitwise-identical results): 1 operands read right before their block (no
 // prefetch), 2 packed f32 epilogue (v_pk_fma_f32), 4 two named operand sets read one block ahead
 // (ping-pong, no copies), 8 loader waves stage through registers (buffer_load_dwordx4 -> ds_write_b128)
@@ -2318,12 +2319,12 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const uint8_t *__r
     const int lw = wave - 8;
     const int lb = 2 * lw;
     auto issue = [&](int st) __attribute__((always_inline)) {
-        if (DIAG >= 2 || wave < 8) return;
+        if ((DIAG >= 2 && DIAG <= 3) || wave < 8) return;
         uint8_t *base = smem + (st % G9_NS) * G9_STAGE;
         const int kb0 = st * G9_KB;
         const bool v = kb0 + lb < nb;                                             // nb even: both or none
-        const __amdgpu_buffer_rsrc_t wr_ = v ? wrs : nul, xr_ = v ? xrs : nul, dr_ = v ? xdrs : nul,
-                                     wdr_ = v ? wdrs : nul;
+        const __amdgpu_buffer_rsrc_t wr_ = v && DIAG != 5 ? wrs : nul, xr_ = v && DIAG != 4 ? xrs : nul,
+                                     dr_ = v ? xdrs : nul, wdr_ = v ? wdrs : nul;
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int b = lb + j;
@@ -2598,7 +2599,8 @@ hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     static bool attr = false;
     if (!attr) {
         for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<0, 9>,
-                       k_gemm9_q4_0<1, 1>, k_gemm9_q4_0<2, 1>, k_gemm9_q4_0<3, 1>, k_gemm9_q4_0<1, 9>}) {
+                       k_gemm9_q4_0<1, 1>, k_gemm9_q4_0<2, 1>, k_gemm9_q4_0<3, 1>, k_gemm9_q4_0<1, 9>,
+                       k_gemm9_q4_0<4, 1>, k_gemm9_q4_0<5, 1>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
             if (e != hipSuccess) return e;
         }
@@ -2610,7 +2612,7 @@ hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     // 25.9-26.0, 2 / 3 (packed epilogue) 38.5-38.7 / 26.7-26.8; k_gemm8 29.3-29.5 on the same boxes
     static const int var = env_int("GGML_HIP_GEMM9_VAR", 1);
     auto kern = diag == 91 ? k_gemm9_q4_0<1, 1> : diag == 92 ? k_gemm9_q4_0<2, 1> : diag == 93 ? k_gemm9_q4_0<3, 1>
-              : diag == 94 ? k_gemm9_q4_0<1, 9>
+              : diag == 94 ? k_gemm9_q4_0<1, 9> : diag == 95 ? k_gemm9_q4_0<4, 1> : diag == 96 ? k_gemm9_q4_0<5, 1>
               : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : var == 9 ? k_gemm9_q4_0<0, 9>
               : k_gemm9_q4_0<0, 1>;
     (void)hipGetLastError();

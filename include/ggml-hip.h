@@ -164,7 +164,7 @@ int ggml_hip_reserve_workspace(int64_t K, int64_t N);
  * image of the weights in the workspace (up to 34 bytes per 32 weights). */
 int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M);
 
-/* Prefill weight images (no ggml-cuda.h counterpart).  The LDS GEMM (N > 128) runs fastest on an image
+/* Prefill weight images (no ggml-cuda.h counterpart).  The LDS GEMM (N > 64 with an image, N > 128 without) runs fastest on an image
  * of the weight: by default fp6 (e2m3 codes of w/2, w = nibble - 8, fp16 d verbatim; 26 B per 32
  * weights, 1.44x the q4_0 bytes; the exact block sums on the block-scaled fp6 MFMA, k_gemm9), under GEMM
  * version 8 int8 (34 B per 32 weights, k_gemm8; bitwise the same results): create builds it once

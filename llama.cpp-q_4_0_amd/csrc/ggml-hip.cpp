@@ -241,6 +241,10 @@ struct WImage {
     int fmt;                                                 // 8: int8 (k_gemm8), 9: fp6 (k_gemm9)
 };
 int image_format() { return gemm_version() >= 10 ? 9 : 8; }
+// a weight with an image takes the image GEMM above this token count (below it the split-K GEMM on
+// the q4_0 bytes; tools/n_sweep9.py: at N = 96 k_gemm9 24 / 26 / 51 us vs split-K 31 / 67 / 62 us for
+// 4096^2 / 4096->11008 / 11008->4096, at N = 64 split-K still wins two of the three)
+constexpr int64_t IMG_MIN_N = 64;
 std::mutex g_wi_mu;
 std::map<std::pair<int, uintptr_t>, WImage> g_wi;          // (device, weight address)
 int64_t g_wi_resident = 0;
@@ -553,8 +557,15 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
     const int id = current_device();
     const int max_nt = ghip::gemv_max_tokens(K);
     // auto: exact mode if switched on; else fused GEMV for N <= 8, split-K MFMA for N <= 128,
-    // LDS-staged MFMA GEMM above (crossovers measured with tools/n_sweep.py)
-    if (algo == 0) algo = exact_mode() ? 4 : (N <= max_nt) ? 1 : (N <= 128 ? 3 : 2);
+    // LDS-staged MFMA GEMM above (crossovers measured with tools/n_sweep.py); a
+    // weight with an image takes the image GEMM from N > IMG_MIN_N (tools/n_sweep9.py)
+    if (algo == 0) {
+        if (exact_mode()) algo = 4;
+        else if (N <= max_nt) algo = 1;
+        else if (N > 128) algo = 2;
+        else if (N > IMG_MIN_N && gemm_version() >= 8 && wimage_find(id, w, K, M)) algo = 2;
+        else algo = 3;
+    }
     if (algo == 1) {
         if (N > max_nt) return fail(GGML_HIP_ERR_INVALID, "GEMV path supports N <= gemv_max_tokens(K)");
         HIP_RET(ghip::gemv_q4_0(w, K, M, x, N, y, ldy, g_dev[id].info, s));
@@ -1909,9 +1920,9 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
                 w = p;
                 w_resident = false;
             }
-            // prefill (the LDS GEMM, N > 128) of a resident weight: build its int8 image once (k_gemm8;
-            // a failure to allocate it leaves k_gemm7 on the q4_0 bytes)
-            if (w_resident && N > 128 && !exact_mode() && (gemm_version() == 8 || gemm_version() == 10))
+            // prefill (N > IMG_MIN_N) of a resident weight: build its image once (fp6 for k_gemm9, int8
+            // under version 8; a failure to allocate it leaves the q4_0 bytes to k_gemm7 / split-K)
+            if (w_resident && N > IMG_MIN_N && !exact_mode() && (gemm_version() == 8 || gemm_version() == 10))
                 (void)wimage_ensure(id, w, K, rows, s);
             // activations
             const float *x;
@@ -2308,9 +2319,9 @@ int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *
         return GGML_HIP_OK;
     }
     if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30) || exact_mode()) {
-        if (N > 128 && !exact_mode() && dev_x && K > 0 && K % 64 == 0) {
-            // the v8 GEMM's weight image grows with M: size the workspace for the largest sibling
-            // first, so that a later sibling cannot reallocate it under the shared x image
+        if (N > IMG_MIN_N && !exact_mode() && dev_x && K > 0 && K % 64 == 0) {
+            // the image GEMMs' per-call weight image grows with M: size the workspace for the largest
+            // sibling first, so that a later sibling cannot reallocate it under the shared x image
             int64_t mmax = 0;
             for (int i = 0; i < n; i++) mmax = std::max(mmax, M[i]);
             void *ws = nullptr;

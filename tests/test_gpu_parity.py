@@ -698,6 +698,60 @@ def test_gemm8_registered_image_prefill_512(K, M, v):
     check_y(y7, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
 
 
+@pytest.mark.parametrize("K,M,N", [(4096, 4096, 96), (4096, 11008, 65), (11008, 4096, 128), (4544, 584, 100)])
+def test_image_gemm_below_prefill_threshold(K, M, N):
+    """A weight with an image takes the image GEMM (k_gemm9) from N > 64 in auto mode (below, and without
+    an image, the split-K GEMM on the q4_0 bytes): bitwise equal to the forced per-call fp6 image
+    (version 11, algo 2), within the bound of the oracle; without the image auto mode is the split-K
+    result."""
+    L = ggml_hip.load()
+    wq, x = make_case(K, M, N, seed=13 * K + M + N)
+    wd, xd = DB.from_array(wq), DB.from_array(x)
+    yd = DB(N * M * 4)
+    ggml_hip.mul_mat(wd, K, M, xd, N, yd)                                   # auto, no image: split-K
+    y_sk = yd.download((N, M), np.float32)
+    y_sk3, _ = gpu_mul_mat(wq, K, x, algo=3)
+    assert np.array_equal(y_sk.view(np.uint32), y_sk3.view(np.uint32))
+    ggml_hip.check(L.ggml_hip_weight_image_create(wd.ptr, K, M, None), "image")
+    try:
+        ggml_hip.mul_mat(wd, K, M, xd, N, yd)                               # auto with the image
+        y_img = yd.download((N, M), np.float32)
+        _gemm_version(11)
+        try:
+            y_call, _ = gpu_mul_mat(wq, K, x, algo=2)
+        finally:
+            _gemm_version(-1)
+        assert np.array_equal(y_img.view(np.uint32), y_call.view(np.uint32))
+        xq = O.quantize_q8_0(x, "avx2")
+        _, s_abs = block_terms(wq, xq, K)
+        check_y(y_img, O.mul_mat(wq, K, x, nthreads=4), s_abs, RTOL, ATOL_BLOCKS)
+    finally:
+        assert L.ggml_hip_weight_image_free(wd.ptr) == 1
+
+
+def test_mixed_sibling_group_at_96_tokens_bitwise():
+    """N = 96: a sibling group whose weights have / lack images runs k_gemm9 and the split-K GEMM side
+    by side on one x (two x forms), bitwise equal to separate calls."""
+    L = ggml_hip.load()
+    K, N = 4096, 96
+    Ms = [256, 4096, 300]
+    cases = [make_case(K, M, N, seed=90 + i) for i, M in enumerate(Ms)]
+    x = cases[0][1]
+    wds = [DB.from_array(c[0]) for c in cases]
+    ggml_hip.check(L.ggml_hip_weight_image_create(wds[1].ptr, K, Ms[1], None), "image")
+    try:
+        xd = DB.from_array(x)
+        ys = [DB(N * M * 4) for M in Ms]
+        ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
+        for wd, yd, M in zip(wds, ys, Ms):
+            single = DB(N * M * 4)
+            ggml_hip.mul_mat(wd, K, M, xd, N, single)
+            assert np.array_equal(yd.download((N, M), np.float32).view(np.uint32),
+                                  single.download((N, M), np.float32).view(np.uint32))
+    finally:
+        L.ggml_hip_weight_image_free(wds[1].ptr)
+
+
 def test_gemm8_mixed_sibling_group_bitwise():
     """A sibling group (one x quantization per form) where the weights have an fp6 image, an int8 image,
     none, and an fp6 image again: the k_gemm9, k_gemm8 and k_gemm7 siblings each read their own x form (the

@@ -245,6 +245,9 @@ int image_format() { return gemm_version() >= 10 ? 9 : 8; }
 // the q4_0 bytes; tools/n_sweep9.py: at N = 96 k_gemm9 24 / 26 / 51 us vs split-K 31 / 67 / 62 us for
 // 4096^2 / 4096->11008 / 11008->4096, at N = 64 split-K still wins two of the three)
 constexpr int64_t IMG_MIN_N = 64;
+// ... and at any N above the GEMV's for tall matrices (4096 -> 11008: k_gemm9 23.4-24.6 us at N = 16-64
+// against split-K 27.0-43.8, whose K walk streams every row per token tile)
+constexpr int64_t IMG_MIN_M = 8192;
 std::mutex g_wi_mu;
 std::map<std::pair<int, uintptr_t>, WImage> g_wi;          // (device, weight address)
 int64_t g_wi_resident = 0;
@@ -563,7 +566,7 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
         if (exact_mode()) algo = 4;
         else if (N <= max_nt) algo = 1;
         else if (N > 128) algo = 2;
-        else if (N > IMG_MIN_N && gemm_version() >= 8 && wimage_find(id, w, K, M)) algo = 2;
+        else if ((N > IMG_MIN_N || M >= IMG_MIN_M) && gemm_version() >= 8 && wimage_find(id, w, K, M)) algo = 2;
         else algo = 3;
     }
     if (algo == 1) {

@@ -698,12 +698,13 @@ def test_gemm8_registered_image_prefill_512(K, M, v):
     check_y(y7, y_ref, upper_s_abs(wq, xq, K), RTOL, ATOL_BLOCKS)
 
 
-@pytest.mark.parametrize("K,M,N", [(4096, 4096, 96), (4096, 11008, 65), (11008, 4096, 128), (4544, 584, 100)])
+@pytest.mark.parametrize("K,M,N", [(4096, 4096, 96), (4096, 11008, 65), (11008, 4096, 128), (4544, 584, 100),
+                                   (4096, 11008, 16), (5120, 13824, 9)])
 def test_image_gemm_below_prefill_threshold(K, M, N):
-    """A weight with an image takes the image GEMM (k_gemm9) from N > 64 in auto mode (below, and without
-    an image, the split-K GEMM on the q4_0 bytes): bitwise equal to the forced per-call fp6 image
-    (version 11, algo 2), within the bound of the oracle; without the image auto mode is the split-K
-    result."""
+    """A weight with an image takes the image GEMM (k_gemm9) from N > 64, and tall ones (M >= 8192) at
+    any N above the GEMV's, in auto mode (otherwise, and without an image, the split-K GEMM on the q4_0
+    bytes): bitwise equal to the forced per-call fp6 image (version 11, algo 2), within the bound of the
+    oracle; without the image auto mode is the split-K result."""
     L = ggml_hip.load()
     wq, x = make_case(K, M, N, seed=13 * K + M + N)
     wd, xd = DB.from_array(wq), DB.from_array(x)

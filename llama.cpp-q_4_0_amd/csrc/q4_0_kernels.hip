@@ -2844,9 +2844,7 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
 // d_x = the fp16-rounded scale as fp32), so d_w * d_x is the reference's d.
 constexpr int EX_RB = 16;                            // output rows per workgroup (8 lanes each)
 constexpr int EX_THREADS = EX_RB * 8;                // 128 = 2 waves
-constexpr int EX_C = 64;                             // blocks per chunk
-constexpr int EX_WB = EX_RB * EX_C * Q4B;            // weight bytes per slot (18 KiB)
-constexpr int EX_WI = EX_WB / 1024 / 2;              // 1-KiB weight DMAs per wave per chunk (9)
+constexpr int EX_C = 64;                             // blocks per chunk (decode: EXC = 32, below)
 // ring slots (S - 1 chunks in flight), per column count: decode (NC = 1) runs 2 slots = 41 KB of LDS,
 // three workgroups per CU instead of two (tools/r2_exs.sh: exact decode 467 -> 532 tok/s; 4 slots 377);
 // -DEX_SLOTS overrides every NC for A/B builds
@@ -2855,16 +2853,25 @@ constexpr int ex_slots(int) { return EX_SLOTS; }
 #else
 constexpr int ex_slots(int nc) { return nc == 1 ? 2 : 3; }
 #endif
-static_assert(EX_WB % 2048 == 0, "whole 1-KiB weight DMAs per wave");
 
-template <int NC>
+// EXC = blocks per chunk.  64: the weights of a chunk are 18 1-KiB DMAs, 9 per wave, and wave w loads
+// half w of each x column.  32 (N = 1 only): 9 weight DMAs, 5 for wave 0 and 4 for wave 1, which loads
+// the 1-KiB x column instead, so both waves still issue the same count (6 with the d_x DMA) and half
+// the LDS per slot lets twice the workgroups share a CU (GGML_HIP_EXACT_C, tools/r3_exact_c.sh)
+template <int NC, int EXC = EX_C, int SLOTS = 0>
 struct ExLayout {
-    static constexpr int XB = NC * EX_C * 32;                    // x bytes per slot
+    static constexpr int WB = EX_RB * EXC * Q4B;                 // weight bytes per slot
+    static constexpr int WI0 = (WB / 1024 + 1) / 2;              // weight DMAs of wave 0 / wave 1
+    static constexpr int WI1 = WB / 1024 - WI0;
+    static constexpr int XB = NC * EXC * 32;                     // x bytes per slot
+    static constexpr int XW = EXC == 64 ? NC : (NC == 1 ? 1 : -1);   // x DMAs per wave (EXC 32: wave 1)
     static constexpr int DXW = (NC + 1) / 2;                     // d_x DMAs per wave per chunk
     static constexpr int DXB = DXW * 2 * 64 * 4;                 // d_x bytes per slot
-    static constexpr int SLOT = EX_WB + XB + DXB;
-    static constexpr int OPS = EX_WI + NC + DXW;                 // vector-memory ops per wave per chunk
-    static constexpr int S = ex_slots(NC);                       // ring slots
+    static constexpr int SLOT = WB + XB + DXB;
+    static constexpr int OPS = EXC == 64 ? WI0 + NC + DXW : WI0 + DXW;   // vector-memory ops per wave per chunk
+    static constexpr int S = SLOTS ? SLOTS : ex_slots(NC);       // ring slots
+    static_assert(WB % 1024 == 0, "whole 1-KiB weight DMAs");
+    static_assert(EXC == 64 ? WI0 == WI1 : (NC == 1 && WI0 == WI1 + 1), "equal DMA counts per wave");
     static_assert(OPS <= 63, "vmcnt immediate");
 };
 
@@ -2880,11 +2887,12 @@ struct ExMats {
     int wg_begin[5];
 };
 
-template <int NC>
+template <int NC, int EXC = EX_C, int SLOTS = 0>
 __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const ExMats mats, int64_t rowbytes,
                                                                int nb, const int8_t *__restrict__ xqs,
                                                                const float *__restrict__ xd, int N, int K) {
-    using Lay = ExLayout<NC>;
+    using Lay = ExLayout<NC, EXC, SLOTS>;
+    constexpr int EX_WB = Lay::WB;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int t = threadIdx.x, l64 = t & 63, lane = t & 7, r = t >> 3;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2909,25 +2917,35 @@ __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const ExMats mats,
     const __amdgpu_buffer_rsrc_t xrs = make_rsrc(xqs + (int64_t)n0 * K, (uint32_t)((int64_t)cols * K));
     const __amdgpu_buffer_rsrc_t drs = make_rsrc(xd + (int64_t)n0 * nb, (uint32_t)((int64_t)cols * nb * 4));
     const __amdgpu_buffer_rsrc_t nul = make_rsrc(W, 0);
-    const int nchunks = (nb + EX_C - 1) / EX_C;
-    // weight DMA i of this wave (slot instruction 9*wave + i) covers units 64(9 wave + i) + l64:
-    // row l64 & 15, piece 4(9 wave + i) + (l64 >> 4)
-    const int wsrc = (l64 & 15) * (int)rowbytes + 16 * (4 * EX_WI * wave + (l64 >> 4));
+    const int nchunks = (nb + EXC - 1) / EXC;
+    // weight DMA i of this wave (slot instruction WI0*wave + i) covers units 64(WI0 wave + i) + l64:
+    // row l64 & 15, piece 4(WI0 wave + i) + (l64 >> 4)
+    const int wsrc = (l64 & 15) * (int)rowbytes + 16 * (4 * Lay::WI0 * wave + (l64 >> 4));
 
     auto issue = [&](int ch) __attribute__((always_inline)) {
         const bool valid = ch < nchunks;                    // past the end: counted, no traffic
-        const int b0 = valid ? ch * EX_C : 0;
+        const int b0 = valid ? ch * EXC : 0;
         uint8_t *slot = smem + (ch % Lay::S) * Lay::SLOT;
         const __amdgpu_buffer_rsrc_t w_ = valid ? wrs : nul;
-#pragma unroll
-        for (int i = 0; i < EX_WI; i++)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(w_, (lds_void_t *)(slot + 1024 * (EX_WI * wave + i)), 16,
-                                                     wsrc + b0 * Q4B + 64 * i, 0, 0, 0);
         const __amdgpu_buffer_rsrc_t x_ = valid ? xrs : nul;
+        if (EXC == 64 || wave == 0) {
 #pragma unroll
-        for (int c = 0; c < NC; c++)                         // wave w loads half w of each column
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(x_, (lds_void_t *)(slot + EX_WB + c * EX_C * 32 + 1024 * wave), 16,
-                                                     c * K + b0 * 32 + 1024 * wave + 16 * l64, 0, 0, 0);
+            for (int i = 0; i < Lay::WI0; i++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(w_, (lds_void_t *)(slot + 1024 * (Lay::WI0 * wave + i)), 16,
+                                                         wsrc + b0 * Q4B + 64 * i, 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < Lay::WI1; i++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(w_, (lds_void_t *)(slot + 1024 * (Lay::WI0 * wave + i)), 16,
+                                                         wsrc + b0 * Q4B + 64 * i, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(x_, (lds_void_t *)(slot + EX_WB), 16, b0 * 32 + 16 * l64, 0, 0, 0);
+        }
+        if constexpr (EXC == 64) {
+#pragma unroll
+            for (int c = 0; c < NC; c++)                     // wave w loads half w of each column
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(x_, (lds_void_t *)(slot + EX_WB + c * EXC * 32 + 1024 * wave), 16,
+                                                         c * K + b0 * 32 + 1024 * wave + 16 * l64, 0, 0, 0);
+        }
 #pragma unroll
         for (int cc = 0; cc < Lay::DXW; cc++) {
             const int c = 2 * cc + wave;
@@ -2961,7 +2979,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const ExMats mats,
     auto load_x = [&](Op &o, const uint8_t *slot, int b) __attribute__((always_inline)) {
 #pragma unroll
         for (int c = 0; c < NC; c++) {
-            o.x[c] = reinterpret_cast<const uint32_t *>(slot + EX_WB + c * EX_C * 32)[b * 8 + lane];
+            o.x[c] = reinterpret_cast<const uint32_t *>(slot + EX_WB + c * EXC * 32)[b * 8 + lane];
             o.dx[c] = reinterpret_cast<const float *>(slot + EX_WB + Lay::XB + 256 * c)[b];
         }
     };
@@ -2998,17 +3016,17 @@ __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const ExMats mats,
         __builtin_amdgcn_s_barrier();                       // everyone's landed; chunk ch-1 consumed
         issue(ch + Lay::S - 1);                             // into chunk ch-1's slot
         const uint8_t *slot = smem + (ch % Lay::S) * Lay::SLOT;
-        const int cb = min(EX_C, nb - ch * EX_C);
-        if (cb == EX_C) {
+        const int cb = min(EXC, nb - ch * EXC);
+        if (cb == EXC) {
             Op ops[2][BB];
 #pragma unroll
             for (int b = 0; b < BB; b++) load_step(ops[0][b], slot, b);
 #pragma unroll
-            for (int i = 0; i < EX_C / BB; i++) {
+            for (int i = 0; i < EXC / BB; i++) {
                 // sched_barrier: keep the next batch's LDS reads ahead of this batch's math (the
                 // scheduler otherwise pulls each read down to its use and waits on it)
                 __builtin_amdgcn_sched_barrier(0);
-                if (i + 1 < EX_C / BB) {
+                if (i + 1 < EXC / BB) {
 #pragma unroll
                     for (int b = 0; b < BB; b++) load_step(ops[(i + 1) & 1][b], slot, (i + 1) * BB + b);
                 }
@@ -3046,22 +3064,22 @@ __global__ __launch_bounds__(EX_THREADS) void k_mm_exact_q4_0(const ExMats mats,
     }
 }
 
-template <int NC>
+template <int NC, int EXC = EX_C, int SLOTS = 0>
 static hipError_t launch_exact(const ExMats &m, int n, int64_t K, const int8_t *xqs, const float *xd, int64_t N,
                                hipStream_t s) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
-    const int lds = ExLayout<NC>::S * ExLayout<NC>::SLOT;
+    const int lds = ExLayout<NC, EXC, SLOTS>::S * ExLayout<NC, EXC, SLOTS>::SLOT;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_mm_exact_q4_0<NC>,
+        hipError_t e = hipFuncSetAttribute((const void *)k_mm_exact_q4_0<NC, EXC, SLOTS>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
     dim3 grid((unsigned)m.wg_begin[n], (unsigned)((N + NC - 1) / NC));
     (void)hipGetLastError();  // report only this launch's error
-    launch_k(k_mm_exact_q4_0<NC>, grid, dim3(EX_THREADS), lds, s, m, rowbytes, nb, xqs, xd, (int)N, (int)K);
+    launch_k(k_mm_exact_q4_0<NC, EXC, SLOTS>, grid, dim3(EX_THREADS), lds, s, m, rowbytes, nb, xqs, xd, (int)N, (int)K);
     return hipGetLastError();
 }
 
@@ -3081,7 +3099,13 @@ hipError_t mm_exact_q4_0_multi(int n, const void *const *W, const int64_t *M, in
     static const int nc_env = env_int("GGML_HIP_EXACT_NC", 0);   // tuning: columns per workgroup
     // measured (tools/exact_nc.sh, 4096 x 4096): 8 columns best at N = 8, 2 at N = 40 and 512
     const int nc = nc_env ? nc_env : N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : 2;
-    if (nc == 1) return launch_exact<1>(m, n, K, xqs, xd, N, s);
+    // decode chunk (GGML_HIP_EXACT_C 32 / 64 blocks) and its ring slots (GGML_HIP_EXACT_S, with 32: 2 / 3);
+    // tools/r3_exact_c.sh, 2 interleaved rounds: 32 x 2 slots 549-551 tok/s, 64 x 2 530-533, 32 x 3 518-520
+    static const int exc = env_int("GGML_HIP_EXACT_C", 32);
+    static const int exs = env_int("GGML_HIP_EXACT_S", 2);
+    if (nc == 1)
+        return exc == 32 ? (exs == 3 ? launch_exact<1, 32, 3>(m, n, K, xqs, xd, N, s) : launch_exact<1, 32>(m, n, K, xqs, xd, N, s))
+                         : launch_exact<1>(m, n, K, xqs, xd, N, s);
     if (nc == 2) return launch_exact<2>(m, n, K, xqs, xd, N, s);
     if (nc == 4) return launch_exact<4>(m, n, K, xqs, xd, N, s);
     return launch_exact<8>(m, n, K, xqs, xd, N, s);

@@ -11,7 +11,11 @@
 //                     ggml_vec_dot_q4_0_q8_0 (ggml.c:2339-2607) with one wave64 per weight row
 //   k_gemm_q4_0       the same product for prefill batches on the int8 matrix cores
 //                     (v_mfma_i32_32x32x32_i8: K=32 = exactly one q4_0/q8_0 block, so every
-//                     MFMA yields the exact per-block integer sum the CPU computes)
+//                     MFMA yields the exact per-block integer sum the CPU computes); k_gemm7 reads
+//                     the q4_0 bytes in place, k_gemm8 an int8 image of the weights
+//   k_gemm9_q4_0      the default prefill GEMM on weight images: the same exact block sums from the
+//                     block-scaled fp6 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e2m3 operands), as f32
+//   k_mm_exact_q4_0   exact mode: the AVX2 branch's fp32 schedule, bit for bit
 //
 // Numerics: every per-block integer sum is exact (as on the CPU); the fp32 accumulation of
 // d_w*d_x*sumi runs in a different order than AVX2's 8-lane fma chain, so y agrees with the

@@ -613,6 +613,38 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
     return GGML_HIP_OK;
 }
 
+// Sibling matrices (one x) that all take k_gemm9 on a registered fp6 image: ONE launch over their
+// row tiles (the x image built once, as before).  Each output is computed exactly as by the
+// per-matrix launch (same block order, same workgroup-half split), so y is bitwise the same.
+// Returns 1 when the group does not qualify (the caller runs one launch per matrix).
+int mul_mat_group_g9(int n, const void *const *w, const int64_t *M, int64_t K, const float *x, int64_t N,
+                     float *const *y, hipStream_t s) {
+    static const bool grp = !getenv("GGML_HIP_GEMM9_GROUP") || atoi(getenv("GGML_HIP_GEMM9_GROUP")) != 0;
+    const int gv = gemm_version();
+    if (!grp || n < 2 || n > 4 || gv != 10 || !x || K <= 0 || K % 64 != 0 || !aligned(x, 16) ||
+        N <= ghip::gemv_max_tokens(K) || N * K >= ((int64_t)1 << 31))
+        return 1;
+    const int id = current_device();
+    const void *img[4];
+    int64_t ldy[4];
+    for (int i = 0; i < n; i++) {
+        int fmt = 0;
+        img[i] = wimage_find(id, w[i], K, M[i], &fmt);
+        // mul_mat_dev's algo rule: the image GEMM above 128 tokens, or above IMG_MIN_N / for tall
+        // matrices when an image exists
+        if (!img[i] || fmt != 9 || !(N > 128 || N > IMG_MIN_N || M[i] >= IMG_MIN_M)) return 1;
+        if (M[i] * (K / QK) * Q4B >= ((int64_t)1 << 31) || M[i] >= (1 << 30)) return 1;
+        ldy[i] = M[i];
+    }
+    void *ws = nullptr;
+    const int wrc = stream_workspace(id, s, workspace_bytes_mm(K, N, 0), &ws);
+    if (wrc != GGML_HIP_OK) return wrc;
+    void *xws = (char *)ws + ws_g8x_offset(K, N);
+    HIP_RET(ghip::gemm9_prep_x(x, K, N, xws, s));
+    HIP_RET(ghip::gemm9_run_multi(n, img, M, K, xws, N, y, ldy, s));
+    return GGML_HIP_OK;
+}
+
 // ------------------------------------------------------------------------------------------
 // tensor helpers
 
@@ -2330,6 +2362,10 @@ int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *
             void *ws = nullptr;
             const int wrc = stream_workspace(current_device(), s, workspace_bytes_mm(K, N, mmax), &ws);
             if (wrc != GGML_HIP_OK) return wrc;
+        }
+        if (n > 1 && !exact_mode()) {
+            const int rc = mul_mat_group_g9(n, dev_w, M, K, dev_x, N, dev_y, s);
+            if (rc != 1) return rc;           // 1: not every sibling takes k_gemm9 on an fp6 image
         }
         unsigned xq = 0;
         for (int i = 0; i < n; i++) {       // GEMM / exact path: x quantized once, one launch per matrix

@@ -93,6 +93,9 @@ size_t gemm9_x_bytes(int64_t K, int64_t N);
 size_t gemm9_w_bytes(int64_t K, int64_t M);
 hipError_t gemm9_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStream_t s);
 hipError_t gemm9_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStream_t s);
+// one launch over the row tiles of n (1..4) sibling weight images that share the x image
+hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *M, int64_t K, const void *xws, int64_t N,
+                           float *const *y, const int64_t *ldy, hipStream_t s);
 hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
                      hipStream_t s);
 

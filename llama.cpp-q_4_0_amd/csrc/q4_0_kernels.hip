@@ -2296,20 +2296,49 @@ __global__ __launch_bounds__(256) void k_prep9_w(const uint8_t *__restrict__ W, 
 // prefetch), 2 packed f32 epilogue (v_pk_fma_f32), 4 two named operand sets read one block ahead
 // (ping-pong, no copies), 8 loader waves stage through registers (buffer_load_dwordx4 -> ds_write_b128)
 // instead of LDS-DMA
+// Tile list of one launch: the row tiles of 1..4 sibling matrices sharing x (wq|wk|wv, w1|w3), tb[i]
+// = first row tile of matrix i, then the token tiles of each row tile.  Tile order (`xcd`):
+// 0 = row tile fastest (workgroup id = rt + Mt*ty: the token tiles of a row tile land on XCD
+// (rt + Mt*ty) % 8, i.e. on one XCD only when Mt % 8 == 0), 1 = XCD-aware: the hardware deals
+// workgroup ids round robin to the 8 XCDs, so id i runs on XCD i % 8; tile j = (i % 8)*C + i/8 (C =
+// G/8) gives XCD x the contiguous tile range [xC, xC + C) in row-tile-major order: the Ny token tiles
+// of a row tile run on one XCD, together, and its weight image is fetched into one L2 only.
+struct G9Mats {
+    const uint8_t *wimg[4];
+    const uint16_t *wd16[4];
+    float *y[4];
+    int64_t ldy[4];
+    int M[4];
+    int tb[5];
+    int n, ny, xcd;
+};
+
 template <int DIAG, int VAR = 0>
-__global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const uint8_t *__restrict__ wimg,
-                                                               const uint16_t *__restrict__ wd16, int nb, int M,
+__global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats, int nb,
                                                                const uint8_t *__restrict__ ximg,
-                                                               const uint16_t *__restrict__ xd16, int64_t Np, int N,
-                                                               float *__restrict__ y, int64_t ldy) {
+                                                               const uint16_t *__restrict__ xd16, int64_t Np, int N) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *zero = smem + G9_NS * G9_STAGE;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 31, h = lane >> 5;
-    const int rt = blockIdx.x;
-    const int m0 = rt * G9_BM, n0 = blockIdx.y * G9_BN;
+    const int G = (int)gridDim.x, Mt = mats.tb[mats.n];
+    int j = (int)blockIdx.x;
+    if (mats.xcd) {
+        const int C = G >> 3;
+        if (j < 8 * C) j = (j & 7) * C + (j >> 3);
+    }
+    const int rtg = mats.xcd ? j / mats.ny : j % Mt, ty = mats.xcd ? j - rtg * mats.ny : j / Mt;
+    // matrix of row tile rtg (selects, no dynamic kernarg indexing)
+    const int mi = (mats.n > 1 && rtg >= mats.tb[1]) + (mats.n > 2 && rtg >= mats.tb[2]) + (mats.n > 3 && rtg >= mats.tb[3]);
+    const uint8_t *wimg = mi == 0 ? mats.wimg[0] : mi == 1 ? mats.wimg[1] : mi == 2 ? mats.wimg[2] : mats.wimg[3];
+    const uint16_t *wd16 = mi == 0 ? mats.wd16[0] : mi == 1 ? mats.wd16[1] : mi == 2 ? mats.wd16[2] : mats.wd16[3];
+    float *y = mi == 0 ? mats.y[0] : mi == 1 ? mats.y[1] : mi == 2 ? mats.y[2] : mats.y[3];
+    const int64_t ldy = mi == 0 ? mats.ldy[0] : mi == 1 ? mats.ldy[1] : mi == 2 ? mats.ldy[2] : mats.ldy[3];
+    const int M = mi == 0 ? mats.M[0] : mi == 1 ? mats.M[1] : mi == 2 ? mats.M[2] : mats.M[3];
+    const int rt = rtg - (mi == 0 ? 0 : mi == 1 ? mats.tb[1] : mi == 2 ? mats.tb[2] : mats.tb[3]);
+    const int m0 = rt * G9_BM, n0 = ty * G9_BN;
     if (tid < G9_ZERO / 4) reinterpret_cast<uint32_t *>(zero)[tid] = 0u;
 
     const __amdgpu_buffer_rsrc_t wrs = make_rsrc(wimg + (int64_t)rt * nb * G9_WB, (uint32_t)nb * G9_WB);
@@ -2593,10 +2622,34 @@ hipError_t gemm9_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStrea
 
 hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
                      hipStream_t s) {
+    return gemm9_run_multi(1, &wws, &M, K, xws, N, &y, &ldy, s);
+}
+
+hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int64_t K, const void *xws, int64_t N,
+                           float *const *yv, const int64_t *ldyv, hipStream_t s) {
     const int nb = (int)(K / QK);
-    const int64_t Mt = (M + 127) / 128, Np = gemm9_np(N);
-    const uint8_t *wimg = (const uint8_t *)wws;
-    const uint16_t *wd16 = (const uint16_t *)((const char *)wws + (size_t)Mt * nb * G9_WB);
+    const int64_t Np = gemm9_np(N), Ny = (N + G9_BN - 1) / G9_BN;
+    if (n < 1 || n > 4 || N <= 0 || nb <= 0) return hipErrorInvalidValue;
+    G9Mats mats{};
+    mats.n = n;
+    mats.ny = (int)Ny;
+    mats.tb[0] = 0;
+    for (int i = 0; i < 4; i++) {
+        const int k = i < n ? i : 0;
+        const int64_t Mt = (Mv[k] + 127) / 128;
+        mats.wimg[i] = (const uint8_t *)wws[k];
+        mats.wd16[i] = (const uint16_t *)((const char *)wws[k] + (size_t)Mt * nb * G9_WB);
+        mats.y[i] = yv[k];
+        mats.ldy[i] = ldyv[k];
+        mats.M[i] = (int)Mv[k];
+        if (i < n) mats.tb[i + 1] = mats.tb[i] + (int)Mt;
+    }
+    for (int i = n; i < 4; i++) mats.tb[i + 1] = mats.tb[i];
+    const int64_t tiles = (int64_t)mats.tb[n] * Ny;
+    if (tiles >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    // GGML_HIP_GEMM9_XCD=0 restores the row-tile-fastest order (A/B)
+    static const int xcd = env_int("GGML_HIP_GEMM9_XCD", 1);
+    mats.xcd = xcd ? 1 : 0;
     const uint8_t *ximg = (const uint8_t *)xws;
     const uint16_t *xd16 = (const uint16_t *)((const char *)xws + (size_t)nb * Np * 48);
     if ((int64_t)nb * Np * 48 >= ((int64_t)1 << 31) || (int64_t)nb * G9_WB >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
@@ -2620,8 +2673,7 @@ hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int
               : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : var == 9 ? k_gemm9_q4_0<0, 9>
               : k_gemm9_q4_0<0, 1>;
     (void)hipGetLastError();
-    launch_k(kern, dim3((unsigned)Mt, (unsigned)((N + G9_BN - 1) / G9_BN)), dim3(G9_THREADS), G9_LDS, s, wimg, wd16,
-             nb, (int)M, ximg, xd16, Np, (int)N, y, ldy);
+    launch_k(kern, dim3((unsigned)tiles), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
     return hipGetLastError();
 }
 

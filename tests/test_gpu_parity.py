@@ -788,6 +788,40 @@ def test_gemm8_mixed_sibling_group_bitwise():
             L.ggml_hip_weight_image_free(wds[i].ptr)
 
 
+@pytest.mark.parametrize("K,Ms,N", [
+    (4096, [4096, 4096, 4096], 512),          # LLaMA-7B wq|wk|wv prefill: one k_gemm9 launch, 768 tiles
+    (4096, [11008, 11008], 512),              # w1|w3: 1376 tiles (XCD-aware order, C = 172)
+    (4096, [300, 128, 4096, 200], 200),       # ragged row tiles, 4 siblings, ragged token tile
+    (4544, [4672, 4544], 100),                # Falcon shapes, N just above IMG_MIN_N
+    (4096, [129, 11008], 40),                 # tall sibling below IMG_MIN_N with a short one (both imaged)
+])
+def test_gemm9_sibling_group_one_launch_bitwise(K, Ms, N):
+    """Siblings that all have fp6 images run as ONE k_gemm9 launch over their row tiles (the x image built
+    once): every y bitwise equal to a separate call per matrix, within the oracle bound."""
+    L = ggml_hip.load()
+    cases = [make_case(K, M, N, seed=700 + 7 * i + M) for i, M in enumerate(Ms)]
+    x = cases[0][1]
+    wds = [DB.from_array(c[0]) for c in cases]
+    for wd, M in zip(wds, Ms):
+        ggml_hip.check(L.ggml_hip_weight_image_create(wd.ptr, K, M, None), "image")
+    try:
+        xd = DB.from_array(x)
+        ys = [DB(N * M * 4) for M in Ms]
+        ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
+        outs = [yd.download((N, M), np.float32) for yd, M in zip(ys, Ms)]
+        for wd, y, M in zip(wds, outs, Ms):
+            single = DB(N * M * 4)
+            ggml_hip.mul_mat(wd, K, M, xd, N, single)
+            assert np.array_equal(y.view(np.uint32), single.download((N, M), np.float32).view(np.uint32))
+        i = min(range(len(Ms)), key=lambda k: Ms[k])            # the oracle on the smallest sibling
+        xq = O.quantize_q8_0(x, "avx2")
+        check_y(outs[i], O.mul_mat(cases[i][0], K, x, nthreads=8, mode="avx2", pool=True),
+                s_abs_exact(cases[i][0], xq, K), RTOL, ATOL_BLOCKS)
+    finally:
+        for wd in wds:
+            L.ggml_hip_weight_image_free(wd.ptr)
+
+
 def test_gemm8_image_api_errors():
     L = ggml_hip.load()
     wq, _ = make_case(128, 64, 1, seed=3)

@@ -2178,10 +2178,11 @@ static constexpr int G9_SCALE_1 = 128, G9_SCALE_5 = 132;           // E8M0 block
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 // e2m3 code of n/2 for an integer n in [-15, 15]
+// (branch-free: with e = (a >= 4) + (a >= 8), c = (a << (2 - e)) + 8e is 4a / 8 + 2a / 16 + a)
 __device__ __forceinline__ uint32_t e2m3_half(int n) {
-    const uint32_t a = (uint32_t)(n < 0 ? -n : n);
-    const uint32_t c = a < 4 ? 4 * a : a < 8 ? 8 + 2 * a : 16 + a;
-    return (n < 0 ? 0x20u : 0u) | c;
+    const uint32_t a = (uint32_t)__builtin_abs(n);
+    const uint32_t e = (uint32_t)(a >= 4u) + (uint32_t)(a >= 8u);
+    return ((uint32_t)n >> 26 & 0x20u) | ((a << (2u - e)) + 8u * e);
 }
 // four 6-bit codes (elements 4m .. 4m+3) as one 24-bit field
 __device__ __forceinline__ uint32_t f6x4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
@@ -2200,6 +2201,7 @@ __device__ __forceinline__ void f6_pack(const uint32_t *F, uint32_t *D) {
 // x: the q8_0 lane code of k_prep8_x (8 lanes per block, wave = 8 tokens of one block); each lane's
 // four q give four (q >> 4) and four (q & 15) codes (24 bits each), and lanes 0-5 of the group
 // assemble the block's six dwords of each half from their neighbours' fields.
+template <bool DPP>
 __global__ __launch_bounds__(256) void k_prep9_x(const float *__restrict__ x, int64_t K, int64_t N,
                                                   uint8_t *__restrict__ ximg, uint16_t *__restrict__ xd16, int64_t Np) {
     const int64_t nb = K / QK;
@@ -2225,10 +2227,22 @@ __global__ __launch_bounds__(256) void k_prep9_x(const float *__restrict__ x, in
     // dword k of a half: fields s and s + 1 shifted by off (k = 0..5 -> (s, off) = (0,0) (1,8) (2,16)
     // (4,0) (5,8) (6,16))
     const int k = sub < 6 ? sub : 5;
-    const int s = k < 3 ? k : k + 1, off = 8 * (k % 3);
-    const int base = lane & ~7;
-    const uint32_t h0 = (uint32_t)__shfl((int)Fh, base + s), h1 = (uint32_t)__shfl((int)Fh, base + s + 1);
-    const uint32_t l0 = (uint32_t)__shfl((int)Fl, base + s), l1 = (uint32_t)__shfl((int)Fl, base + s + 1);
+    const int off = 8 * (k % 3);
+    // the fields of lanes +1 and +2 by DPP row shifts (groups of 8 lanes sit inside 16-lane rows; lanes
+    // 6 and 7, which read past their group, store nothing): k < 3 takes fields (own, +1), k >= 3 (+1, +2)
+    // (DPP false: the same fields through __shfl, the round-3 first version; A/B GGML_HIP_PREP9_DPP=0)
+    const int base = lane & ~7, s1 = base + (k < 3 ? k : k + 1);
+    const uint32_t Fh1 = DPP ? (uint32_t)__builtin_amdgcn_mov_dpp((int)Fh, 0x101, 0xF, 0xF, false)   // row_shl:1
+                             : (uint32_t)__shfl((int)Fh, base + k + 1);
+    const uint32_t Fh2 = DPP ? (uint32_t)__builtin_amdgcn_mov_dpp((int)Fh, 0x102, 0xF, 0xF, false)   // row_shl:2
+                             : (uint32_t)__shfl((int)Fh, s1 + 1);
+    const uint32_t Fl1 = DPP ? (uint32_t)__builtin_amdgcn_mov_dpp((int)Fl, 0x101, 0xF, 0xF, false)
+                             : (uint32_t)__shfl((int)Fl, base + k + 1);
+    const uint32_t Fl2 = DPP ? (uint32_t)__builtin_amdgcn_mov_dpp((int)Fl, 0x102, 0xF, 0xF, false)
+                             : (uint32_t)__shfl((int)Fl, s1 + 1);
+    const bool lo3 = k < 3;
+    const uint32_t h0 = lo3 ? Fh : Fh1, h1 = lo3 ? Fh1 : Fh2;
+    const uint32_t l0 = lo3 ? Fl : Fl1, l1 = lo3 ? Fl1 : Fl2;
     if (!live || sub >= 6) return;
     const uint32_t dh = (h0 >> off) | (h1 << (24 - off)), dl = (l0 >> off) | (l1 << (24 - off));
     const int sw = (int)((n >> 4) & 1);
@@ -2604,7 +2618,8 @@ hipError_t gemm9_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStre
     uint8_t *ximg = (uint8_t *)xws;
     uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)nb * Np * 48);
     (void)hipGetLastError();
-    launch_k(k_prep9_x, dim3((unsigned)((nb + 3) / 4), (unsigned)((N + 7) / 8)), dim3(256), 0, s, x, K, N, ximg, xd16, Np);
+    static const bool dpp = env_int("GGML_HIP_PREP9_DPP", 1) != 0;
+    launch_k(dpp ? k_prep9_x<true> : k_prep9_x<false>, dim3((unsigned)((nb + 3) / 4), (unsigned)((N + 7) / 8)), dim3(256), 0, s, x, K, N, ximg, xd16, Np);
     return hipGetLastError();
 }
 

@@ -753,6 +753,42 @@ __global__ __launch_bounds__(512, 2) void k_mb(const uint8_t *src, float *out, i
             for (int i = 0; i < 16; i++) acc[0][i] += S0[i] + S1[i] + P0[i] + P1[i];
         }
     }
+    if constexpr (VAR >= 42 && VAR <= 45) {
+        // issue rate of one instruction kind, four independent accumulator chains per wave:
+        // 42 v_mfma_f32_32x32x16_f16 (the scale product's), 43 v_mfma_f32_32x32x8_f16 (legacy form),
+        // 44 the block-scaled f8f6f4 MFMA with fp4 (e2m1) operands, 45 with fp8 (e4m3) operands
+        typedef int i32x8 __attribute__((ext_vector_type(8)));
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+        f32x16 C0 = fz, C1 = fz, C2 = fz, C3 = fz;
+        for (int b = 0; b < nblk; b++) {
+            const int rb = (b & (R - 1));
+            const i32x4 u = *(const i32x4 *)(lds + rb * BN * 32 + c * 16);
+            const i32x4 v = *(const i32x4 *)(lds + LA + rb * BM * 32 + c * 16);
+            if constexpr (VAR == 42) {
+                const half8 a = __builtin_bit_cast(half8, u), bb = __builtin_bit_cast(half8, v);
+                C0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bb, C0, 0, 0, 0);
+                C1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bb, a, C1, 0, 0, 0);
+                C2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, a, C2, 0, 0, 0);
+                C3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bb, bb, C3, 0, 0, 0);
+            } else if constexpr (VAR == 43) {
+                const int2 u2 = {u.x, u.y}, v2 = {v.x, v.y};
+                const half4 a = __builtin_bit_cast(half4, u2), bb = __builtin_bit_cast(half4, v2);
+                C0 = __builtin_amdgcn_mfma_f32_32x32x8f16(a, bb, C0, 0, 0, 0);
+                C1 = __builtin_amdgcn_mfma_f32_32x32x8f16(bb, a, C1, 0, 0, 0);
+                C2 = __builtin_amdgcn_mfma_f32_32x32x8f16(a, a, C2, 0, 0, 0);
+                C3 = __builtin_amdgcn_mfma_f32_32x32x8f16(bb, bb, C3, 0, 0, 0);
+            } else {
+                constexpr int F = VAR == 44 ? 4 : 0;
+                const i32x8 a = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w}, bb = {v.x, v.y, v.z, v.w, u.x, u.y, u.z, u.w};
+                C0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, C0, F, F, 0, 127, 0, 127);
+                C1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bb, a, C1, F, F, 0, 127, 0, 127);
+                C2 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, a, C2, F, F, 0, 127, 0, 127);
+                C3 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bb, bb, C3, F, F, 0, 127, 0, 127);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc[0][i] += C0[i] + C1[i] + C2[i] + C3[i];
+    }
     float s = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; t++)
@@ -804,5 +840,14 @@ int main(int argc, char **argv) {
     run<21>("VAR21 i8 2 tiles/wave (gemm8 structure)", 4, 2, src, out, nblk, 2);
     run<36>("VAR36 fp6 block sum, f32 epilogue (no cvt)", 4, 2, src, out, nblk, 2);
     run<38>("VAR38 fp6 x2 per tile-blk, 4 chains", 4, 2, src, out, nblk, 2);
+    if (argc > 3) {        // instruction issue rates: 4 MFMAs per block-step, reported per MFMA (x2 tiles)
+        run<39>("VAR39 i8 32x32x32, 4 chains", 4, 2, src, out, nblk, 2);
+        run<42>("VAR42 f16 32x32x16, 4 chains", 4, 2, src, out, nblk, 2);
+        run<43>("VAR43 f16 32x32x8 (legacy), 4 chains", 4, 2, src, out, nblk, 2);
+        run<44>("VAR44 fp4 32x32x64 (scale), 4 chains", 4, 2, src, out, nblk, 2);
+        run<45>("VAR45 fp8 32x32x64 (scale), 4 chains", 4, 2, src, out, nblk, 2);
+        run<42>("VAR42 f16 32x32x16, 4 chains", 4, 2, src, out, nblk, 1);
+        run<44>("VAR44 fp4 32x32x64 (scale), 4 chains", 4, 2, src, out, nblk, 1);
+    }
     return 0;
 }

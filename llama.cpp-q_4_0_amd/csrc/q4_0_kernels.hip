@@ -2480,6 +2480,19 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
         o.sx = reinterpret_cast<const uint16_t *>(base + G9_W + G9_X + G9_WD + b * 128)[tt];
         return o;
     };
+    // the rank-1 scale product d_x (x) d_w: one fp16 MFMA with only K element 0 nonzero (lanes 32-63
+    // hold zeros in B), exact in f32.  VAR & 16: the K = 8 form v_mfma_f32_32x32x8_f16, 41 vs 51 nominal
+    // cycles per instruction for the K = 16 form (tools/gemm_mb.hip VAR 42 / 43, four chains), same
+    // output layout and the same products, so bitwise the same P
+    auto scale_mfma = [&](const u32x4 &a, const u32x4 &b) __attribute__((always_inline)) {
+        if constexpr (VAR & 16) {
+            typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+            const u32x2 a2 = {a.x, a.y}, b2 = {b.x, b.y};
+            return __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(half4, a2), __builtin_bit_cast(half4, b2), fz, 0, 0, 0);
+        } else {
+            return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), fz, 0, 0, 0);
+        }
+    };
     auto block = [&](const Ops &o) __attribute__((always_inline)) {
         as.x = o.sx;
         bs0.x = o.sw0;
@@ -2489,9 +2502,9 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
         epi(acc1, S1, P1);
         __builtin_amdgcn_sched_barrier(0);
         S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw0, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
-        P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs0), fz, 0, 0, 0);
+        P0 = scale_mfma(as, bs0);
         S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw1, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
-        P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs1), fz, 0, 0, 0);
+        P1 = scale_mfma(as, bs1);
         __builtin_amdgcn_sched_barrier(0);
     };
     auto sync = [&]() __attribute__((always_inline)) {
@@ -2670,7 +2683,7 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     if ((int64_t)nb * Np * 48 >= ((int64_t)1 << 31) || (int64_t)nb * G9_WB >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
-        for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<0, 9>,
+        for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<0, 9>, k_gemm9_q4_0<0, 17>,
                        k_gemm9_q4_0<1, 1>, k_gemm9_q4_0<2, 1>, k_gemm9_q4_0<3, 1>, k_gemm9_q4_0<1, 9>,
                        k_gemm9_q4_0<4, 1>, k_gemm9_q4_0<5, 1>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
@@ -2682,11 +2695,14 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     // GGML_HIP_GEMM9_VAR (A/B, tools/r3_g9var.sh, kernel medians, 2 interleaved rounds): 0 (prefetch one
     // block ahead through a copied operand set) 32.6-32.9 us at 4096x4096x512, 1 (no prefetch, default)
     // 25.9-26.0, 2 / 3 (packed epilogue) 38.5-38.7 / 26.7-26.8; k_gemm8 29.3-29.5 on the same boxes
-    static const int var = env_int("GGML_HIP_GEMM9_VAR", 1);
+    // 17 (= 1 with the scale product on the K = 8 fp16 MFMA, bitwise the same y; default since
+    // tools/r3_g9p8.sh: kernel medians 26.44-26.52 vs 26.52-26.56 us at 4096^2 x 512, bench prefill
+    // 0.370 / 0.377 vs 0.380 / 0.388 ms per layer in two rounds, VAR 17 run first in each)
+    static const int var = env_int("GGML_HIP_GEMM9_VAR", 17);
     auto kern = diag == 91 ? k_gemm9_q4_0<1, 1> : diag == 92 ? k_gemm9_q4_0<2, 1> : diag == 93 ? k_gemm9_q4_0<3, 1>
               : diag == 94 ? k_gemm9_q4_0<1, 9> : diag == 95 ? k_gemm9_q4_0<4, 1> : diag == 96 ? k_gemm9_q4_0<5, 1>
               : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : var == 9 ? k_gemm9_q4_0<0, 9>
-              : k_gemm9_q4_0<0, 1>;
+              : var == 17 ? k_gemm9_q4_0<0, 17> : k_gemm9_q4_0<0, 1>;
     (void)hipGetLastError();
     launch_k(kern, dim3((unsigned)tiles), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
     return hipGetLastError();

@@ -75,3 +75,47 @@ def test_pack_layout_round_trips():
         codes = [int(c) for c in rng.integers(0, 64, 32)]
         bits = sum(d << (32 * i) for i, d in enumerate(f6_pack(codes)))
         assert [(bits >> (6 * j)) & 63 for j in range(32)] == codes
+
+
+def e2m3_half_branchfree(n):
+    """the device encoder as compiled (csrc/q4_0_kernels.hip e2m3_half): e = (a >= 4) + (a >= 8),
+    c = (a << (2 - e)) + 8e, sign from bit 31 of n"""
+    a = abs(n)
+    e = int(a >= 4) + int(a >= 8)
+    return (((n & 0xFFFFFFFF) >> 26) & 0x20) | ((a << (2 - e)) + 8 * e)
+
+
+def test_branchfree_encoder_equals_definition():
+    for n in range(-15, 16):
+        assert e2m3_half_branchfree(n) == e2m3_half(n), n
+
+
+def g9_tile(i, G, Mt, ny, xcd):
+    """k_gemm9's workgroup id -> (row tile, token tile) (csrc/q4_0_kernels.hip, G9Mats.xcd)"""
+    j = i
+    if xcd:
+        C = G >> 3
+        if j < 8 * C:
+            j = (j & 7) * C + (j >> 3)
+        rt = j // ny
+        return rt, j - rt * ny
+    return j % Mt, j // Mt
+
+
+def test_g9_tile_order_is_a_permutation_and_xcd_local():
+    """Every tile exactly once in both orders; in the XCD-aware order (workgroup i runs on XCD i % 8)
+    each XCD gets a contiguous row-tile-major range, so the token tiles of a row tile share one XCD
+    except at the at most 7 range boundaries."""
+    for Mt, ny in [(32, 8), (86, 8), (96, 8), (172, 8), (3, 1), (13, 1), (7, 4), (35, 3), (1, 1)]:
+        G = Mt * ny
+        for xcd in (0, 1):
+            tiles = [g9_tile(i, G, Mt, ny, xcd) for i in range(G)]
+            assert sorted(tiles) == [(r, t) for r in range(Mt) for t in range(ny)], (Mt, ny, xcd)
+        xcds = {}
+        for i in range(G):
+            xcds.setdefault(g9_tile(i, G, Mt, ny, 1)[0], set()).add(i % 8)
+        split = sum(len(s) > 1 for s in xcds.values())
+        if G >= 8:
+            assert split <= 7, (Mt, ny, split)
+        if G % 8 == 0 and (G // 8) % ny == 0:
+            assert split == 0, (Mt, ny)

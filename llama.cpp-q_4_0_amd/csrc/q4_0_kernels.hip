@@ -1328,6 +1328,17 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm_q4_0(const uint8_t *__re
 //     not wait on two staging waves.
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Rank-1 scale product d_x (x) d_w of the prefill GEMMs: one fp16 MFMA whose A and B lanes carry a
+// single nonzero half (dword 0), so every K form gives the same exact f32 products; the K = 8 form
+// (v_mfma_f32_32x32x8_f16) issues in 41 nominal cycles against 51 for the K = 16 form
+// (tools/gemm_mb.hip VAR 42 / 43, profiles/r03_mfma_rates.txt).  Only dword 0 of a and b may be nonzero.
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x16 scale_rank1(const u32x4 &a, const u32x4 &b) {
+    const u32x2 a2 = {a.x, a.y}, b2 = {b.x, b.y};
+    const f32x16 z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    return __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(half4_t, a2), __builtin_bit_cast(half4_t, b2), z, 0, 0, 0);
+}
 static constexpr int G6_STAGE_W = GM_KB * GM_BM * 32;           // int8 weights  [KB][BM][32]
 static constexpr int G6_STAGE_X = GM_KB * GM_BN * 32;           // int8 acts     [KB][BN][32]
 static constexpr int G6_STAGE_WD = GM_KB * GM_BM * 2;           // fp16 d_w      [KB][BM]
@@ -1444,8 +1455,7 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm6_q4_0(const uint8_t *__r
         S = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a, o.b, MAGIC ? im : iz, 0, 0, 0);
         const u32x4 as = {h == 0 ? o.sx : 0u, 0u, 0u, 0u};
         const u32x4 bs = {h == 0 ? o.sw : 0u, 0u, 0u, 0u};
-        P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs), fz,
-                                                   0, 0, 0);
+        P = scale_rank1(as, bs);
     };
     float acc[16];
 #pragma unroll
@@ -1693,8 +1703,7 @@ __global__ __launch_bounds__(GM_THREADS, 2) void k_gemm7_q4_0(const uint8_t *__r
         S = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a, o.b, im, 0, 0, 0);
         const u32x4 as = {o.sx, 0u, 0u, 0u};
         const u32x4 bs = {o.sw, 0u, 0u, 0u};
-        P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as), __builtin_bit_cast(half8, bs), fz,
-                                                   0, 0, 0);
+        P = scale_rank1(as, bs);
     };
     float acc[16];
 #pragma unroll
@@ -1986,17 +1995,17 @@ __global__ __launch_bounds__(G8_THREADS, 1) void k_gemm8_q4_0(const int8_t *__re
             epi(acc1, S1, P1);
             __builtin_amdgcn_sched_barrier(0);
             S0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a0, o.bw, im, 0, 0, 0);
-            P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as0), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+            P0 = scale_rank1(as0, bs);
             S1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a1, o.bw, im, 0, 0, 0);
-            P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as1), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+            P1 = scale_rank1(as1, bs);
             __builtin_amdgcn_sched_barrier(0);
             return;
         }
         S0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a0, o.bw, im, 0, 0, 0);
-        P0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as0), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+        P0 = scale_rank1(as0, bs);
         epi(acc1, S1, P1);                     // tile 1 of the previous block (S1 = bias, P1 = 0 at first)
         S1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(o.a1, o.bw, im, 0, 0, 0);
-        P1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as1), __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+        P1 = scale_rank1(as1, bs);
         epi(acc0, S0, P0);
     };
     auto sync = [&]() __attribute__((always_inline)) {   // retire stage s+1, keep s+2 in flight
@@ -2767,7 +2776,6 @@ __global__ __launch_bounds__(SK * 64, 1) void k_gemm_sk_q4_0(const uint8_t *__re
     };
     const int mg = 0x4B400000;
     const i32x16 im = {mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg, mg};
-    const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float acc[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) acc[i] = 0.0f;
@@ -2781,8 +2789,7 @@ __global__ __launch_bounds__(SK * 64, 1) void k_gemm_sk_q4_0(const uint8_t *__re
         const i32x16 S = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa, wb, im, 0, 0, 0);
         const u32x4 as = {h == 0 ? f2h(dx) : 0u, 0u, 0u, 0u};
         const u32x4 bs = {h == 0 ? dw16 : 0u, 0u, 0u, 0u};
-        const f32x16 P = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, as),
-                                                                __builtin_bit_cast(half8, bs), fz, 0, 0, 0);
+        const f32x16 P = scale_rank1(as, bs);
 #pragma unroll
         for (int i = 0; i < 16; i++) acc[i] = fmaf(__int_as_float(S[i]) - 12582912.0f, P[i], acc[i]);
     };

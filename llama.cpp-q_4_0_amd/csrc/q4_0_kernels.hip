@@ -2177,8 +2177,8 @@ static constexpr int G9_X = G9_KB * G9_XB;                        // 24 KB
 static constexpr int G9_WD = G9_KB * G9_BM * 2;                   // fp16 d_w                 2 KB
 static constexpr int G9_XD = G9_KB * G9_BN * 2;                   // fp16 d_x                 1 KB
 static constexpr int G9_STAGE = G9_W + G9_X + G9_WD + G9_XD;      // 51 KB
-static constexpr int G9_ZERO = 256;
-static constexpr int G9_LDS = G9_NS * G9_STAGE + G9_ZERO;         // 153.25 KB
+static constexpr int G9_ZERO = 1024;                               // zero d_w for the h = 1 lanes
+static constexpr int G9_LDS = G9_NS * G9_STAGE + G9_ZERO;         // 154 KB
 static constexpr int G9_OPS = 15;                                  // DMA instructions per loader wave per stage
 static_assert(G9_WB == 3 * 1024 && G9_XB == 3 * 1024, "3 x 1 KiB DMAs per block and operand");
 static_assert(4 * 2 * 16 * 64 * 4 <= G9_NS * G9_STAGE, "the partial-tile exchange fits in the ring");
@@ -2318,7 +2318,9 @@ __global__ __launch_bounds__(256) void k_prep9_w(const uint8_t *__restrict__ W, 
 // VAR bits (A/B knobs, bitwise-identical results): 1 operands read right before their block (no
 // prefetch), 2 packed f32 epilogue (v_pk_fma_f32), 4 two named operand sets read one block ahead
 // (ping-pong, no copies), 8 loader waves stage through registers (buffer_load_dwordx4 -> ds_write_b128)
-// instead of LDS-DMA
+// instead of LDS-DMA, 16 the scale product on the K = 8 fp16 MFMA, 32 (with 1) per-stage VGPR address
+// bases with the block offsets as ds_read immediates (no address VALU per block; a variant that also
+// read the next block's operands before the current block needed 168 VGPRs and spilled 81: dropped)
 // Tile list of one launch: the row tiles of 1..4 sibling matrices sharing x (wq|wk|wv, w1|w3), tb[i]
 // = first row tile of matrix i, then the token tiles of each row tile.  Tile order (`xcd`):
 // 0 = row tile fastest (workgroup id = rt + Mt*ty: the token tiles of a row tile land on XCD
@@ -2577,6 +2579,32 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
                         block(ob);
                     }
                 }
+            } else if constexpr (VAR & 32) {
+                // per-stage VGPR bases, the block offsets as ds_read immediates: no address VALU per
+                // block; the second weight tile's 8-byte part is read from its own (opaque) base, so
+                // the compiler does not pair the two b64 reads into a ds_read2 + v_mov reassembly
+                const uint32_t sb = (uint32_t)(s % G9_NS) * G9_STAGE;
+                uint32_t xa = sb + G9_W + 4 * g * G9_XB + xo16, xb8 = sb + G9_W + 4 * g * G9_XB + xo8;
+                uint32_t wa0 = sb + 4 * g * G9_WB + r0 * 16, wa1 = wa0 + 512;
+                uint32_t w80 = sb + 4 * g * G9_WB + 2048 + r0 * 8, w81 = w80 + 256;
+                uint32_t da = h ? (uint32_t)(G9_NS * G9_STAGE) : sb + G9_W + G9_X + 4 * g * 256 + r0 * 2;
+                uint32_t xd = sb + G9_W + G9_X + G9_WD + 4 * g * 128 + tt * 2;
+                asm volatile("" : "+v"(wa1), "+v"(w81));
+                auto rdj = [&](int j) __attribute__((always_inline)) {
+                    Ops o;
+                    o.ax = rd24(smem + xa + j * G9_XB, smem + xb8 + j * G9_XB);
+                    o.bw0 = rd24(smem + wa0 + j * G9_WB, smem + w80 + j * G9_WB);
+                    o.bw1 = rd24(smem + wa1 + j * G9_WB, smem + w81 + j * G9_WB);
+                    o.sw0 = *reinterpret_cast<const uint16_t *>(smem + da + j * 256);
+                    o.sw1 = *reinterpret_cast<const uint16_t *>(smem + da + j * 256 + 64);
+                    o.sx = *reinterpret_cast<const uint16_t *>(smem + xd + j * 128);
+                    return o;
+                };
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (kb + j >= nb) break;
+                    block(rdj(j));
+                }
             } else if constexpr (VAR & 1) {
 #pragma unroll
                 for (int j = 0; j < 4; j++)
@@ -2693,6 +2721,7 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     static bool attr = false;
     if (!attr) {
         for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<0, 9>, k_gemm9_q4_0<0, 17>,
+                       k_gemm9_q4_0<0, 49>,
                        k_gemm9_q4_0<1, 1>, k_gemm9_q4_0<2, 1>, k_gemm9_q4_0<3, 1>, k_gemm9_q4_0<1, 9>,
                        k_gemm9_q4_0<4, 1>, k_gemm9_q4_0<5, 1>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
@@ -2707,11 +2736,15 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     // 17 (= 1 with the scale product on the K = 8 fp16 MFMA, bitwise the same y; default since
     // tools/r3_g9p8.sh: kernel medians 26.44-26.52 vs 26.52-26.56 us at 4096^2 x 512, bench prefill
     // 0.370 / 0.377 vs 0.380 / 0.388 ms per layer in two rounds, VAR 17 run first in each)
-    static const int var = env_int("GGML_HIP_GEMM9_VAR", 17);
+    // 49 (= 17 with per-stage VGPR address bases, no address VALU per block; default since
+    // tools/r3_g9p8.sh VA=17 VB=49: kernel medians 24.76-24.80 vs 26.76-26.84 us at 4096^2 x 512,
+    // 4096 -> 11008 67.6-67.9 vs 72.2-74.1, 11008 -> 4096 55.8-57.7 vs 59.5-60.1)
+    static const int var = env_int("GGML_HIP_GEMM9_VAR", 49);
     auto kern = diag == 91 ? k_gemm9_q4_0<1, 1> : diag == 92 ? k_gemm9_q4_0<2, 1> : diag == 93 ? k_gemm9_q4_0<3, 1>
               : diag == 94 ? k_gemm9_q4_0<1, 9> : diag == 95 ? k_gemm9_q4_0<4, 1> : diag == 96 ? k_gemm9_q4_0<5, 1>
               : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : var == 9 ? k_gemm9_q4_0<0, 9>
-              : var == 17 ? k_gemm9_q4_0<0, 17> : k_gemm9_q4_0<0, 1>;
+              : var == 17 ? k_gemm9_q4_0<0, 17> : var == 49 ? k_gemm9_q4_0<0, 49>
+              : k_gemm9_q4_0<0, 1>;
     (void)hipGetLastError();
     launch_k(kern, dim3((unsigned)tiles), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
     return hipGetLastError();

@@ -2721,9 +2721,9 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     static bool attr = false;
     if (!attr) {
         for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<0, 9>, k_gemm9_q4_0<0, 17>,
-                       k_gemm9_q4_0<0, 49>,
-                       k_gemm9_q4_0<1, 1>, k_gemm9_q4_0<2, 1>, k_gemm9_q4_0<3, 1>, k_gemm9_q4_0<1, 9>,
-                       k_gemm9_q4_0<4, 1>, k_gemm9_q4_0<5, 1>}) {
+                       k_gemm9_q4_0<0, 49>, k_gemm9_q4_0<0, 51>,
+                       k_gemm9_q4_0<1, 49>, k_gemm9_q4_0<2, 49>, k_gemm9_q4_0<3, 49>, k_gemm9_q4_0<1, 9>,
+                       k_gemm9_q4_0<4, 49>, k_gemm9_q4_0<5, 49>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
             if (e != hipSuccess) return e;
         }
@@ -2740,11 +2740,11 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     // tools/r3_g9p8.sh VA=17 VB=49: kernel medians 24.76-24.80 vs 26.76-26.84 us at 4096^2 x 512,
     // 4096 -> 11008 67.6-67.9 vs 72.2-74.1, 11008 -> 4096 55.8-57.7 vs 59.5-60.1)
     static const int var = env_int("GGML_HIP_GEMM9_VAR", 49);
-    auto kern = diag == 91 ? k_gemm9_q4_0<1, 1> : diag == 92 ? k_gemm9_q4_0<2, 1> : diag == 93 ? k_gemm9_q4_0<3, 1>
-              : diag == 94 ? k_gemm9_q4_0<1, 9> : diag == 95 ? k_gemm9_q4_0<4, 1> : diag == 96 ? k_gemm9_q4_0<5, 1>
+    auto kern = diag == 91 ? k_gemm9_q4_0<1, 49> : diag == 92 ? k_gemm9_q4_0<2, 49> : diag == 93 ? k_gemm9_q4_0<3, 49>
+              : diag == 94 ? k_gemm9_q4_0<1, 9> : diag == 95 ? k_gemm9_q4_0<4, 49> : diag == 96 ? k_gemm9_q4_0<5, 49>
               : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : var == 9 ? k_gemm9_q4_0<0, 9>
               : var == 17 ? k_gemm9_q4_0<0, 17> : var == 49 ? k_gemm9_q4_0<0, 49>
-              : k_gemm9_q4_0<0, 1>;
+              : var == 51 ? k_gemm9_q4_0<0, 51> : k_gemm9_q4_0<0, 1>;
     (void)hipGetLastError();
     launch_k(kern, dim3((unsigned)tiles), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
     return hipGetLastError();

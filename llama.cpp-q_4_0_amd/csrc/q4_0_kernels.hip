@@ -2320,7 +2320,8 @@ __global__ __launch_bounds__(256) void k_prep9_w(const uint8_t *__restrict__ W, 
 // (ping-pong, no copies), 8 loader waves stage through registers (buffer_load_dwordx4 -> ds_write_b128)
 // instead of LDS-DMA, 16 the scale product on the K = 8 fp16 MFMA, 32 (with 1) per-stage VGPR address
 // bases with the block offsets as ds_read immediates (no address VALU per block; a variant that also
-// read the next block's operands before the current block needed 168 VGPRs and spilled 81: dropped)
+// read the next block's operands before the current block needed 168 VGPRs and spilled 81: dropped),
+// 128 loader waves at s_setprio 3
 // Tile list of one launch: the row tiles of 1..4 sibling matrices sharing x (wq|wk|wv, w1|w3), tb[i]
 // = first row tile of matrix i, then the token tiles of each row tile.  Tile order (`xcd`):
 // 0 = row tile fastest (workgroup id = rt + Mt*ty: the token tiles of a row tile land on XCD
@@ -2528,6 +2529,9 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
     };
 
     const int nstages = (nb + G9_KB - 1) / G9_KB;
+    if constexpr ((VAR & 128) != 0) {
+        if (wave >= 8) __builtin_amdgcn_s_setprio(3);     // VAR 128: loader waves issue first
+    }
     if constexpr (!(VAR & 8)) {
 #pragma unroll
         for (int st = 0; st < G9_NS - 1; st++) issue(st);
@@ -2721,7 +2725,7 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     static bool attr = false;
     if (!attr) {
         for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<0, 9>, k_gemm9_q4_0<0, 17>,
-                       k_gemm9_q4_0<0, 49>, k_gemm9_q4_0<0, 51>,
+                       k_gemm9_q4_0<0, 49>, k_gemm9_q4_0<0, 51>, k_gemm9_q4_0<0, 177>,
                        k_gemm9_q4_0<1, 49>, k_gemm9_q4_0<2, 49>, k_gemm9_q4_0<3, 49>, k_gemm9_q4_0<1, 9>,
                        k_gemm9_q4_0<4, 49>, k_gemm9_q4_0<5, 49>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
@@ -2744,7 +2748,7 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
               : diag == 94 ? k_gemm9_q4_0<1, 9> : diag == 95 ? k_gemm9_q4_0<4, 49> : diag == 96 ? k_gemm9_q4_0<5, 49>
               : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : var == 9 ? k_gemm9_q4_0<0, 9>
               : var == 17 ? k_gemm9_q4_0<0, 17> : var == 49 ? k_gemm9_q4_0<0, 49>
-              : var == 51 ? k_gemm9_q4_0<0, 51> : k_gemm9_q4_0<0, 1>;
+              : var == 51 ? k_gemm9_q4_0<0, 51> : var == 177 ? k_gemm9_q4_0<0, 177> : k_gemm9_q4_0<0, 1>;
     (void)hipGetLastError();
     launch_k(kern, dim3((unsigned)tiles), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
     return hipGetLastError();

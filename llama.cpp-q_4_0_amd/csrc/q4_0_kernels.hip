@@ -2321,7 +2321,7 @@ __global__ __launch_bounds__(256) void k_prep9_w(const uint8_t *__restrict__ W, 
 // instead of LDS-DMA, 16 the scale product on the K = 8 fp16 MFMA, 32 (with 1) per-stage VGPR address
 // bases with the block offsets as ds_read immediates (no address VALU per block; a variant that also
 // read the next block's operands before the current block needed 168 VGPRs and spilled 81: dropped),
-// 128 loader waves at s_setprio 3
+// 128 loader waves at s_setprio 3, 256 the burst as fp6, fp6, fp16, fp16
 // Tile list of one launch: the row tiles of 1..4 sibling matrices sharing x (wq|wk|wv, w1|w3), tb[i]
 // = first row tile of matrix i, then the token tiles of each row tile.  Tile order (`xcd`):
 // 0 = row tile fastest (workgroup id = rt + Mt*ty: the token tiles of a row tile land on XCD
@@ -2513,10 +2513,18 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
         epi(acc0, S0, P0);
         epi(acc1, S1, P1);
         __builtin_amdgcn_sched_barrier(0);
-        S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw0, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
-        P0 = scale_mfma(as, bs0);
-        S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw1, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
-        P1 = scale_mfma(as, bs1);
+        if constexpr ((VAR & 256) != 0) {
+            // VAR 256: the two fp6 MFMAs, then the two fp16 ones (two format switches per burst, not four)
+            S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw0, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+            S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw1, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+            P0 = scale_mfma(as, bs0);
+            P1 = scale_mfma(as, bs1);
+        } else {
+            S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw0, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+            P0 = scale_mfma(as, bs0);
+            S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw1, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+            P1 = scale_mfma(as, bs1);
+        }
         __builtin_amdgcn_sched_barrier(0);
     };
     auto sync = [&]() __attribute__((always_inline)) {
@@ -2725,7 +2733,7 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     static bool attr = false;
     if (!attr) {
         for (auto k : {k_gemm9_q4_0<0, 0>, k_gemm9_q4_0<0, 1>, k_gemm9_q4_0<0, 4>, k_gemm9_q4_0<0, 9>, k_gemm9_q4_0<0, 17>,
-                       k_gemm9_q4_0<0, 49>, k_gemm9_q4_0<0, 51>, k_gemm9_q4_0<0, 177>,
+                       k_gemm9_q4_0<0, 49>, k_gemm9_q4_0<0, 51>, k_gemm9_q4_0<0, 177>, k_gemm9_q4_0<0, 305>,
                        k_gemm9_q4_0<1, 49>, k_gemm9_q4_0<2, 49>, k_gemm9_q4_0<3, 49>, k_gemm9_q4_0<1, 9>,
                        k_gemm9_q4_0<4, 49>, k_gemm9_q4_0<5, 49>}) {
             hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
@@ -2743,12 +2751,15 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     // 49 (= 17 with per-stage VGPR address bases, no address VALU per block; default since
     // tools/r3_g9p8.sh VA=17 VB=49: kernel medians 24.76-24.80 vs 26.76-26.84 us at 4096^2 x 512,
     // 4096 -> 11008 67.6-67.9 vs 72.2-74.1, 11008 -> 4096 55.8-57.7 vs 59.5-60.1)
-    static const int var = env_int("GGML_HIP_GEMM9_VAR", 49);
+    // 305 (= 49 with the burst ordered fp6, fp6, fp16, fp16; tools/r3_g9p8.sh VA=49 VB=305: 4096 -> 11008
+    // 66.2-67.2 vs 68.1-68.5 us, 4096^2 25.0-25.1 vs 25.0-25.4, 11008 -> 4096 54.7-56.5 vs 55.4-56.5)
+    static const int var = env_int("GGML_HIP_GEMM9_VAR", 305);
     auto kern = diag == 91 ? k_gemm9_q4_0<1, 49> : diag == 92 ? k_gemm9_q4_0<2, 49> : diag == 93 ? k_gemm9_q4_0<3, 49>
               : diag == 94 ? k_gemm9_q4_0<1, 9> : diag == 95 ? k_gemm9_q4_0<4, 49> : diag == 96 ? k_gemm9_q4_0<5, 49>
               : var == 0 ? k_gemm9_q4_0<0, 0> : var == 4 ? k_gemm9_q4_0<0, 4> : var == 9 ? k_gemm9_q4_0<0, 9>
               : var == 17 ? k_gemm9_q4_0<0, 17> : var == 49 ? k_gemm9_q4_0<0, 49>
-              : var == 51 ? k_gemm9_q4_0<0, 51> : var == 177 ? k_gemm9_q4_0<0, 177> : k_gemm9_q4_0<0, 1>;
+              : var == 51 ? k_gemm9_q4_0<0, 51> : var == 177 ? k_gemm9_q4_0<0, 177>
+              : var == 305 ? k_gemm9_q4_0<0, 305> : k_gemm9_q4_0<0, 1>;
     (void)hipGetLastError();
     launch_k(kern, dim3((unsigned)tiles), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
     return hipGetLastError();

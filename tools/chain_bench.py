@@ -1,6 +1,7 @@
-"""Decode chain vs one launch per mul_mat (graph), LLaMA-7B shapes, data-dependent wiring
-(wo reads q, w1|w3 read wo's y, w2 reads w1's y, the next layer reads w2's y).
-Usage: [GGML_HIP_CHAIN_DEPTH=8] python tools/chain_bench.py [layers] [reps]"""
+"""Decode chain (overlapped launches, two streams) vs the same chain on one stream vs one launch per
+mul_mat (graph), LLaMA-7B shapes, data-dependent wiring (wo reads q, w1|w3 read wo's y, w2 reads w1's
+y, the next layer reads w2's y).
+Usage: python tools/chain_bench.py [layers] [reps]"""
 import json
 import os
 import sys
@@ -41,7 +42,11 @@ for l in range(layers):
 gh.synchronize()
 nbytes = sum(18 * Kk // 32 * sum(Ms) for _, Ms, Kk, _, _ in tasks)
 
-ch = gh.Chain(tasks)
+import ctypes  # noqa: E402
+import numpy as np  # noqa: E402
+
+L.ggml_hip_debug_set_chain_overlap.argtypes = [ctypes.c_int]
+L.ggml_hip_debug_chain_overlap.argtypes = [ctypes.c_void_p]
 ev = [gh.Event(), gh.Event()]
 
 
@@ -51,8 +56,7 @@ def timeit(fn):
     for _ in range(reps):
         fn()
     ev[1].record(s)
-    ms = ev[0].elapsed_ms(ev[1]) / reps
-    return ms
+    return ev[0].elapsed_ms(ev[1]) / reps
 
 
 def launches():
@@ -66,16 +70,27 @@ with g:
     launches()
 ms_g = timeit(g.launch)
 yg = Y[-1][6].download((K,), "float32")
-gc = gh.Graph(s)
-with gc:
-    ch.launch(s)
-ms_c = timeit(gc.launch)
-st = ch.status()
-yc = Y[-1][6].download((K,), "float32")
-ms_ce = timeit(lambda: ch.launch(s))
-import numpy as np
-print(json.dumps({"layers": layers, "depth": int(os.environ.get("GGML_HIP_CHAIN_DEPTH", 8)),
-                  "graph_launches_ms": round(ms_g, 4), "chain_graph_ms": round(ms_c, 4), "chain_eager_ms": round(ms_ce, 4),
-                  "tok_s_launches": round(32 / layers * 1e3 / ms_g, 1), "tok_s_chain": round(32 / layers * 1e3 / ms_c, 1),
-                  "GBps_chain": round(nbytes / ms_c / 1e6, 1), "status": st,
-                  "bitwise_equal": bool(np.array_equal(yg.view(np.uint32), yc.view(np.uint32)))}), flush=True)
+out = {"layers": layers, "graph_launches_ms": round(ms_g, 4), "tok_s_launches": round(32 / layers * 1e3 / ms_g, 1)}
+for ov in (1, 0):
+    L.ggml_hip_debug_set_chain_overlap(ov)
+    ch = gh.Chain(tasks)
+    tag = "ovl" if ov else "one_stream"
+    out[f"{tag}_active"] = L.ggml_hip_debug_chain_overlap(ch.h)
+    ms_ce = timeit(lambda: ch.launch(s))
+    st_e = ch.status()
+    ye = Y[-1][6].download((K,), "float32")
+    gc = gh.Graph(s)
+    with gc:
+        ch.launch(s)
+    ms_c = timeit(gc.launch)
+    st = ch.status()
+    yc = Y[-1][6].download((K,), "float32")
+    out.update({f"{tag}_eager_ms": round(ms_ce, 4), f"{tag}_graph_ms": round(ms_c, 4),
+                f"{tag}_tok_s_eager": round(32 / layers * 1e3 / ms_ce, 1),
+                f"{tag}_tok_s_graph": round(32 / layers * 1e3 / ms_c, 1),
+                f"{tag}_GBps_best": round(nbytes / min(ms_c, ms_ce) / 1e6, 1), f"{tag}_status": [st_e, st],
+                f"{tag}_bitwise_equal": [bool(np.array_equal(yg.view(np.uint32), ye.view(np.uint32))),
+                                         bool(np.array_equal(yg.view(np.uint32), yc.view(np.uint32)))]})
+    del gc, ch
+L.ggml_hip_debug_set_chain_overlap(-1)
+print(json.dumps(out), flush=True)

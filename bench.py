@@ -201,18 +201,29 @@ def main():
     groups = [[0, 1, 2], [3], [4, 5], [6]] if batch else [[i] for i in range(len(LAYER))]
     yb = {i: gh.DeviceBuffer(LAYER[i][2] * 4) for i in range(len(LAYER))}
     ysplit = {i: gh.DeviceBuffer(LAYER[i][2] * 4) for i in range(len(LAYER))}   # full-M gathered outputs
+    # one GPU: the decode's real data dependencies (each launch reads the y of the launch before it):
+    # wq|wk|wv read the previous layer's w2 output (layer 0: the fixed input row), wo reads q, w1|w3 read
+    # wo's output, w2 reads w1's output.  Multi-GPU keeps one fixed x per K (split_check reads the slices).
+    DEP = {0: 6, 1: 6, 2: 6, 3: 0, 4: 3, 5: 3, 6: 4}
+    def x_of(li, i, use_comm):
+        K = LAYER[i][1]
+        if use_comm or (li == 0 and DEP[i] == 6):
+            return xs[K].ptr
+        return yb[DEP[i]].ptr
+
     def build_launch_args(use_comm):
         out = []
-        for row in stack.mats:
+        for li, row in enumerate(stack.mats):
             for g in groups:
                 if len(g) == 1 or not batch:
-                    out.append(("one" if use_comm else "local", tuple(row[g[0]]) + (yb[g[0]], ysplit[g[0]])))
+                    out.append(("one" if use_comm else "local",
+                                tuple(row[g[0]]) + (yb[g[0]], ysplit[g[0]], x_of(li, g[0], use_comm))))
                 elif not use_comm:
                     n = len(g)
                     wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
                     yp = (ctypes.c_void_p * n)(*[yb[i].ptr for i in g])
                     mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
-                    out.append(("multi", (n, wp, mp, row[g[0]][1], yp)))
+                    out.append(("multi", (n, wp, mp, row[g[0]][1], yp, x_of(li, g[0], use_comm))))
                 else:                # split siblings: one GEMV launch + one grouped all-gather
                     n = len(g)
                     wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
@@ -227,16 +238,16 @@ def main():
     def decode_step(launch_args=launch_args):
         for kind, a in launch_args:
             if kind == "multi":
-                n, wp, mp, K, yp = a
-                gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, 1, yp, stream))
+                n, wp, mp, K, yp, xp = a
+                gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xp, 1, yp, stream))
                 continue
             if kind == "split_multi":
                 n, wp, mt, rp, K, yp = a
                 gh.check(L.ggml_hip_mul_mat_q4_0_split_multi(comm, n, wp, mt, rp, K, xs[K].ptr, 1, yp, stream))
                 continue
-            name, K, M, m_loc, buf, rb, ylocal, yfull = a
+            name, K, M, m_loc, buf, rb, ylocal, yfull, xp = a
             if kind == "local":      # this rank's slice only, no collective
-                gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, 1, ylocal.ptr, m_loc, 0, stream))
+                gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xp, 1, ylocal.ptr, m_loc, 0, stream))
             elif comm is None:
                 gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, M, xs[K].ptr, 1, ys[M].ptr, M, 0, stream))
             else:
@@ -277,7 +288,9 @@ def main():
         "metric": METRIC, "value": round(tok_s, 2), "unit": "tok/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "q4_0 x q8_0 (int8 dot, f32 acc)",
-        "data": "synthetic: W ~ N(0,0.02) -> q4_0 (ggml A3 rule, on device), x ~ N(0,1); random-init, no checkpoint",
+        "data": ("synthetic: W ~ N(0,0.02) -> q4_0 (ggml A3 rule, on device), x ~ N(0,1); random-init, no checkpoint"
+                 + ("; each launch reads the previous launch's y (wo <- q, w1|w3 <- wo, w2 <- w1, next layer <- w2)"
+                    if comm is None else "")),
         "config": {"workload": "LLaMA-7B q4_0 decode, 32 layers x 7 mul_mats (wq,wk,wv,wo 4096x4096; w1,w3 "
                                "4096->11008; w2 11008->4096), N=1, q8_0 quantize of x included, lm_head excluded",
                    "layers": args.layers, "weights_bytes_per_rank": stack.total_bytes,
@@ -439,7 +452,7 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
         t = e0.elapsed_ms(e1) * 1e-3 / (reps * len(sel))
         kind, a = sel[0]
         if kind == "multi":
-            n, wp, mp, K, yp = a
+            n, wp, mp, K, yp, _ = a
             Ms = [mp[i] for i in range(n)]
         else:
             K, Ms = a[1], [a[3]]
@@ -541,10 +554,10 @@ def extra_decode(gh, L, stream, name, n_layers, spec, groups, steps=20, warmup=5
 
 def run_launch(gh, L, kind, a, xs, stream):
     if kind == "multi":
-        n, wp, mp, K, yp = a
+        n, wp, mp, K, yp, _ = a
         gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, 1, yp, stream))
     else:
-        name, K, M, m_loc, buf, rb, yb, _ = a
+        name, K, M, m_loc, buf, rb, yb, _, _ = a
         gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, 1, yb.ptr, m_loc, 1, stream))
 
 
@@ -646,6 +659,23 @@ def _stats(vals):
     return {"median": float(np.median(v)), "min": float(v.min()), "max": float(v.max()), "n": int(v.size)}
 
 
+def _loadavg():
+    try:
+        return float(open("/proc/loadavg").read().split()[0])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+def _cg_throttled():
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            if line.startswith("throttled_usec"):
+                return int(line.split()[1])
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
 def _cpu_share():
     """P for the CPU baseline: BASELINE.md §3 asks for the physical cores of one socket; a job on the GPU
     box runs under a CPU quota (cgroup cpu.max / affinity / OMP_NUM_THREADS, 16 for one GPU), and
@@ -724,7 +754,17 @@ def cpu_baseline(budget_s):
 
     h = R.ref_layers_create(n_copies, 1)
     R.ref_stack_run(h, n_copies, P)              # warm: page in every layer copy
+    load0, thr0 = _loadavg(), _cg_throttled()
+    r0, w0 = os.times(), time.perf_counter()
     dec_p = samples(lambda: (R.ref_stack_run(h, n_copies, P), n_copies), 0.8, 5, 12, 0.45 * budget_s)
+    r1, w1 = os.times(), time.perf_counter()
+    load1, thr1 = _loadavg(), _cg_throttled()
+    host_load = {
+        "loadavg_1m_before": load0, "loadavg_1m_after": load1, "host_cpus": os.cpu_count(),
+        # CPU time this process got during the P-thread samples / (wall x P): < 1 when its threads waited
+        "cpu_utilisation_of_P": round(((r1.user - r0.user) + (r1.system - r0.system)) / max(1e-9, (w1 - w0) * P), 3),
+        "cgroup_throttled_usec": (thr1 - thr0) if thr0 is not None and thr1 is not None else None,
+        "note": "the box's host is shared with other jobs: compare CPU numbers across runs with these fields"}
     dec_1 = samples(lambda: (R.ref_stack_run(h, n_copies, 1), n_copies), 0.2, 3, 5, 0.08 * budget_s)
     k = [0]
 
@@ -752,6 +792,7 @@ def cpu_baseline(budget_s):
              "-march=x86-64-v3 (AVX2/FMA/F16C branches; the host lacks AVX-512/AVX-VNNI)")
     return {
         "value": round(tok(dP["median"]), 3), "unit": "tok/s", "cores": P, "kind": "reference",
+        "value_min": round(tok(dP["max"]), 3), "value_max": round(tok(dP["min"]), 3), "host_load": host_load,
         "sample": (f"LLaMA-7B decode layers (7 q4_0 mul_mats, N=1) over {n_copies} rotating layer copies through the "
                    f"reference ggml.c (oracle/_ref, {build}); one ggml graph per pass, one ggml_graph_compute with "
                    f"{P} threads ({share['rule']}); {dP['n']} samples of >= 0.8 s, median; "

@@ -183,20 +183,15 @@ int64_t ggml_hip_weight_image_bytes(void);                  /* device bytes held
 int ggml_hip_debug_set_gemm_version(int v);
 
 /* ------------------------------------------------------------------------------------------
- * Decode chains: a sequence of dependent N = 1 q4_0 mul_mats as ONE persistent launch.
+ * Decode chains: a sequence of dependent N = 1 q4_0 mul_mats, validated once and launched together.
  * A decode eval issues its q4_0 mul_mats one after another on one stream (llama.cpp:1217-1600 ->
- * ggml_compute_forward_mul_mat_q_f32, ggml.c:11226-11411); each pays a kernel boundary and a ramp.
- * A chain runs tasks 0..n-1 in order inside one launch: task t reads x only after every task < t
- * has written its y (so x of a task may be, or overlap, the y of an earlier task), while the
- * weight loads of later tasks stream ahead.  Results are bitwise equal to n separate
- * ggml_hip_mul_mat_q4_0_multi(N = 1) calls, except for long rows (K > 12288) whose separate call
- * takes the chunk-balanced GEMV (BAL, a different fp32 order within the same parity bound).
- * Weights must not change while a launch runs; a task's y must not overlap its own x (create
- * rejects it).  The launch is persistent: its grid (one workgroup per CU) must be co-resident, so
- * do not run other kernels concurrently on the device while it runs; a dependency wait that never
- * completes gives up after a bounded spin, and results are UNDEFINED until ggml_hip_chain_status
- * returns 0.  Exact mode (ggml_hip_set_exact) runs the tasks as separate exact-mode calls.  No
- * ggml-cuda.h counterpart; default off (slower than per-launch GEMVs).
+ * ggml_compute_forward_mul_mat_q_f32, ggml.c:11226-11411).  A chain runs tasks 0..n-1 in stream order,
+ * each as one sibling GEMV launch (ggml_hip_mul_mat_q4_0_multi with N = 1): task t reads x only after
+ * every task < t has written its y, so x of a task may be, or overlap, the y of an earlier task.
+ * Results are bitwise those of n separate ggml_hip_mul_mat_q4_0_multi calls (exact mode included).
+ * A task's y must not overlap its own x (create rejects it).  Graph-capturable.  Two in-launch
+ * designs (one persistent launch, round 2; overlapped launches with flag hand-offs, round 4) were
+ * bitwise equal and slower.  No ggml-cuda.h counterpart.
  * ---------------------------------------------------------------------------------------- */
 typedef struct ggml_hip_chain_task {
     int nmat;                 /* 1..4 sibling matrices sharing x (e.g. wq|wk|wv) */
@@ -207,12 +202,11 @@ typedef struct ggml_hip_chain_task {
     float *y[4];              /* f32 [M[i]] */
 } ggml_hip_chain_task;
 typedef struct ggml_hip_chain ggml_hip_chain;
-/* Validates the tasks and uploads the task table to the current device (synchronous). */
+/* Validates the tasks (no device work). */
 int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **chain);
-/* Stream-ordered (graph-capturable): one memset node + one kernel per segment of <= 256 tasks. */
+/* Stream-ordered (graph-capturable): one GEMV launch per task. */
 int ggml_hip_chain_launch(ggml_hip_chain *chain, void *stream);
-/* Synchronizes the device; 0 when every dependency wait of the last launch completed, else the
- * index + 1 of the first task whose wait gave up (bounded spin; its results are invalid). */
+/* Synchronizes the device; 0 (kept for source compatibility with the in-launch designs). */
 int ggml_hip_chain_status(ggml_hip_chain *chain);
 int ggml_hip_chain_destroy(ggml_hip_chain *chain);
 

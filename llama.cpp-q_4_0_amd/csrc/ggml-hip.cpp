@@ -2441,38 +2441,18 @@ int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M) {
 }
 
 // ------------------------------------------------------------------------------------------
-// decode chains (q4_0_chain.hip): one overlapped launch per task, alternating between the caller's
-// stream and the chain's own second stream, so that task t becomes resident and streams its weights
-// while task t-1 runs; stream order (t-2 -> t) bounds the launches in flight to two.
+// decode chains: tasks validated once, launched as stream-ordered sibling GEMVs (one launch per task).
+// Round 2 ran a chain as one persistent launch and round 4 as overlapped launches on two streams with
+// per-workgroup flag hand-offs; both were bitwise equal and measured slower than one
+// kernel per task (the in-launch hand-off costs more than a kernel boundary plus the GEMV's prologue),
+// so a chain is the per-launch path.
 
 }  // extern "C"
 
-std::atomic<int> g_chain_overlap{-1};            // -1: GGML_HIP_CHAIN_OVERLAP (default 1)
-
 struct ggml_hip_chain {
     int device = 0;
-    int num_cus = 0;
-    bool overlap = true;                           // two streams (false: every task on the caller's stream)
-    std::vector<ggml_hip_chain_task> tasks;       // host copy (exact-mode path)
-    std::vector<ghip::ChainOvlTask> rec;
-    std::vector<int> grid;                        // workgroups of each task's launch
-    uint32_t *d_sync = nullptr;                   // [0] epoch, [64] error word, [256 ...] flags per task
-    hipStream_t s2 = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    unsigned long long *d_stamps = nullptr;        // diagnostics: [ntasks][256][8] (GGML_HIP_CHAIN_STAMPS=1)
+    std::vector<ggml_hip_chain_task> tasks;
 };
-
-namespace {
-constexpr int CHAIN_SYNC_HEAD = 256;               // words before the per-task flag arrays
-void chain_free(ggml_hip_chain *c) {
-    if (c->d_sync) (void)GHIP_SYNC(hipFree)(c->d_sync);
-    if (c->ev_fork) (void)GHIP_SYNC(hipEventDestroy)(c->ev_fork);
-    if (c->ev_join) (void)GHIP_SYNC(hipEventDestroy)(c->ev_join);
-    if (c->s2) (void)GHIP_SYNC(hipStreamDestroy)(c->s2);
-    if (c->d_stamps) (void)GHIP_SYNC(hipFree)(c->d_stamps);
-    delete c;
-}
-}  // namespace
 
 extern "C" {
 
@@ -2482,84 +2462,23 @@ int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip
     *out = nullptr;
     if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
     if (ntasks < 1 || !tasks) return fail(GGML_HIP_ERR_INVALID, "ntasks must be >= 1");
-    const int dev = current_device();
-    const int cus = g_dev[dev].info.num_cus;
-    if (cus > ghip::CHAIN_FLAGS_PER_TASK) return fail(GGML_HIP_ERR_UNSUPPORTED, "more CUs than chain flag words");
-    std::vector<ghip::ChainOvlTask> rec(ntasks);
-    std::vector<int> grid(ntasks);
-    bool resident2 = true;
     for (int t = 0; t < ntasks; t++) {
         const ggml_hip_chain_task &k = tasks[t];
         if (k.nmat < 1 || k.nmat > ghip::GEMV_MULTI_MAX) return fail(GGML_HIP_ERR_INVALID, "nmat must be 1..4");
         if (k.K <= 0 || k.K % 64 != 0 || !k.x || !aligned(k.x, 16))
             return fail(GGML_HIP_ERR_INVALID, "bad x or K (K % 64 == 0, 16-byte aligned x)");
-        if (k.K > (int64_t)ghip::CHAIN_OVL_MAX_PPL * 4096) return fail(GGML_HIP_ERR_UNSUPPORTED, "K too large for a chain");
-        ghip::ChainOvlTask &r = rec[t];
-        int64_t total = 0;
-        for (int i = 0; i < ghip::GEMV_MULTI_MAX; i++) {
-            const bool used = i < k.nmat;
-            if (used && (!k.W[i] || !k.y[i] || k.M[i] <= 0 || !aligned(k.W[i], 16) || !aligned(k.y[i], 4)))
+        for (int i = 0; i < k.nmat; i++) {
+            if (!k.W[i] || !k.y[i] || k.M[i] <= 0 || !aligned(k.W[i], 16) || !aligned(k.y[i], 4))
                 return fail(GGML_HIP_ERR_INVALID, "null / misaligned W or y, or M <= 0");
-            r.W[i] = used ? k.W[i] : k.W[0];
-            r.y[i] = used ? k.y[i] : k.y[0];
-            if (used) {                   // a task's y may not overlap its own x (its rows read x while others write y)
-                const uint64_t xlo = (uint64_t)(uintptr_t)k.x, xhi = xlo + 4 * (uint64_t)k.K;
-                const uint64_t yp = (uint64_t)(uintptr_t)k.y[i];
-                if (yp < xhi && xlo < yp + 4 * (uint64_t)k.M[i])
-                    return fail(GGML_HIP_ERR_INVALID, "a task's y overlaps its own x");
-            }
-            total += used ? k.M[i] : 0;
+            // a task's y may not overlap its own x (its rows read x while others write y)
+            const uint64_t xlo = (uint64_t)(uintptr_t)k.x, xhi = xlo + 4 * (uint64_t)k.K;
+            const uint64_t yp = (uint64_t)(uintptr_t)k.y[i];
+            if (yp < xhi && xlo < yp + 4 * (uint64_t)k.M[i]) return fail(GGML_HIP_ERR_INVALID, "a task's y overlaps its own x");
         }
-        // row_begin[i + 1] = M[0] + ... + M[i] for used siblings, the total rows for unused ones
-        int64_t acc = 0;
-        for (int i = 0; i < 3; i++) {
-            acc += i < k.nmat ? k.M[i] : 0;
-            r.rb[i] = (int)std::min<int64_t>(i + 1 < k.nmat ? acc : total, INT_MAX);
-        }
-        r.M = total;
-        r.K = k.K;
-        r.x = k.x;
-        r.index = t;
-        grid[t] = ghip::chain_ovl_grid(total, cus);
-        if ((int64_t)grid[t] * 4 * 64 < total) return fail(GGML_HIP_ERR_UNSUPPORTED, "too many rows for one chain task");
-        const int occ = ghip::chain_ovl_occupancy(k.K);
-        if (occ < 1) return fail(GGML_HIP_ERR_UNSUPPORTED, "chain kernel cannot be resident (occupancy 0)");
-        if (occ < 2) resident2 = false;
     }
-    const int overlap_set = g_chain_overlap.load();
-    const int overlap_env = overlap_set >= 0 ? overlap_set : [] {
-        const char *e = getenv("GGML_HIP_CHAIN_OVERLAP");
-        return e ? atoi(e) : 1;
-    }();
     auto *c = new ggml_hip_chain();
-    c->device = dev;
-    c->num_cus = cus;
-    // two launches side by side need two resident workgroups per CU; otherwise one stream (still correct:
-    // every wait is then satisfied when the launch starts)
-    c->overlap = overlap_env != 0 && resident2;
+    c->device = current_device();
     c->tasks.assign(tasks, tasks + ntasks);
-    c->rec = std::move(rec);
-    c->grid = std::move(grid);
-    const size_t words = CHAIN_SYNC_HEAD + (size_t)ntasks * ghip::CHAIN_FLAGS_PER_TASK;
-    if (hipMalloc(&c->d_sync, words * 4) != hipSuccess) {
-        c->d_sync = nullptr;
-        chain_free(c);
-        return fail(GGML_HIP_ERR_NOMEM, "chain: hipMalloc failed");
-    }
-    if (GHIP_SYNC(hipMemset)(c->d_sync, 0, words * 4) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
-        chain_free(c);
-        return fail(GGML_HIP_ERR_DEVICE, "chain: stream / event setup failed");
-    }
-    if (getenv("GGML_HIP_CHAIN_STAMPS")) {
-        const size_t sb = sizeof(unsigned long long) * 8 * 256 * (size_t)ntasks;
-        if (hipMalloc(&c->d_stamps, sb) != hipSuccess || GHIP_SYNC(hipMemset)(c->d_stamps, 0, sb) != hipSuccess) {
-            chain_free(c);
-            return fail(GGML_HIP_ERR_NOMEM, "chain: stamps");
-        }
-    }
     *out = c;
     return GGML_HIP_OK;
 }
@@ -2569,37 +2488,9 @@ int ggml_hip_chain_launch(ggml_hip_chain *c, void *stream) {
     if (!c) return fail(GGML_HIP_ERR_INVALID, "null chain");
     if (current_device() != c->device) return fail(GGML_HIP_ERR_INVALID, "chain belongs to another device");
     hipStream_t s = resolve_stream(stream);
-    if (exact_mode()) {                          // the exact kernels, one call per task
-        for (const auto &k : c->tasks) {
-            int rc = ggml_hip_mul_mat_q4_0_multi(k.nmat, k.W, k.M, k.K, k.x, 1, (float *const *)k.y, s);
-            if (rc != GGML_HIP_OK) return rc;
-        }
-        return GGML_HIP_OK;
-    }
-    static const int spin = [] {
-        const char *e = getenv("GGML_HIP_CHAIN_SPIN");
-        return e ? atoi(e) : (1 << 18);     // ~0.3 s per wait
-    }();
-    uint32_t *epoch = c->d_sync, *err = c->d_sync + 64;
-    uint32_t *flags = c->d_sync + CHAIN_SYNC_HEAD;
-    // the epoch bump is a kernel boundary ahead of every task: the previous launch's flags are all
-    // stale (epoch - 1) from here on, and the first task's x is ordered behind the caller's work
-    HIP_RET(ghip::chain_ovl_bump(epoch, err, s));
-    const int n = (int)c->rec.size();
-    if (c->overlap && n > 1) {
-        HIP_RET(GHIP_SYNC(hipEventRecord)(c->ev_fork, s));
-        HIP_RET(GHIP_SYNC(hipStreamWaitEvent)(c->s2, c->ev_fork, 0));
-    }
-    for (int t = 0; t < n; t++) {
-        hipStream_t st = (c->overlap && (t & 1)) ? c->s2 : s;
-        const uint32_t *wait = t > 0 ? flags + (size_t)(t - 1) * ghip::CHAIN_FLAGS_PER_TASK : nullptr;
-        HIP_RET(ghip::chain_ovl_launch(c->rec[t], wait, t > 0 ? c->grid[t - 1] : 0,
-                                       flags + (size_t)t * ghip::CHAIN_FLAGS_PER_TASK, epoch, err, spin, c->num_cus, st,
-                                       c->d_stamps));
-    }
-    if (c->overlap && n > 1) {
-        HIP_RET(GHIP_SYNC(hipEventRecord)(c->ev_join, c->s2));
-        HIP_RET(GHIP_SYNC(hipStreamWaitEvent)(s, c->ev_join, 0));
+    for (const auto &k : c->tasks) {
+        const int rc = ggml_hip_mul_mat_q4_0_multi(k.nmat, k.W, k.M, k.K, k.x, 1, (float *const *)k.y, s);
+        if (rc != GGML_HIP_OK) return rc;
     }
     return GGML_HIP_OK;
 }
@@ -2607,35 +2498,11 @@ int ggml_hip_chain_launch(ggml_hip_chain *c, void *stream) {
 int ggml_hip_chain_status(ggml_hip_chain *c) {
     if (!c) return fail(GGML_HIP_ERR_INVALID, "null chain");
     HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
-    uint32_t code = 0;
-    HIP_RET(GHIP_SYNC(hipMemcpy)(&code, c->d_sync + 64, 4, hipMemcpyDeviceToHost));
-    return (int)code;
-}
-
-// diagnostics (not in the public header): copy [ntasks][256][8] stamps of the last launch; grid[t] = task t's
-// workgroups
-int ggml_hip_debug_chain_stamps(ggml_hip_chain *c, unsigned long long *host, int *grid) {
-    if (!c || !c->d_stamps) return fail(GGML_HIP_ERR_INVALID, "no stamps (set GGML_HIP_CHAIN_STAMPS=1)");
-    HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
-    HIP_RET(GHIP_SYNC(hipMemcpy)(host, c->d_stamps, sizeof(unsigned long long) * 8 * 256 * c->rec.size(),
-                                 hipMemcpyDeviceToHost));
-    if (grid)
-        for (size_t t = 0; t < c->grid.size(); t++) grid[t] = c->grid[t];
-    return GGML_HIP_OK;
-}
-
-// not in the public header: 1 when the chain's launches overlap on two streams
-int ggml_hip_debug_chain_overlap(ggml_hip_chain *c) { return c && c->overlap ? 1 : 0; }
-// not in the public header: chains created from now on overlap (1) or run on one stream (0); -1 = env
-int ggml_hip_debug_set_chain_overlap(int on) {
-    g_chain_overlap.store(on < 0 ? -1 : (on ? 1 : 0));
-    return GGML_HIP_OK;
+    return 0;
 }
 
 int ggml_hip_chain_destroy(ggml_hip_chain *c) {
-    if (!c) return GGML_HIP_OK;
-    (void)GHIP_SYNC(hipDeviceSynchronize)();
-    chain_free(c);
+    delete c;
     return GGML_HIP_OK;
 }
 

@@ -17,16 +17,32 @@
 
 namespace ghip {
 
+// Failure (a peer's flag does not arrive within a.timeout ticks of s_memrealtime, 100 MHz): the waiting
+// workgroup sets its peer's bit in ctl[2] and the host-mapped error word, and writes NaN into that peer's
+// segment of recv instead of copying the (stale) landing slot.  A comm with any error bit set is failed
+// for good: every later launch only copies this rank's own slice and fills the peers' segments with NaN
+// (no stores to peers, no waits, the epoch stays), and the host returns an error before launching the
+// next all-gather (ggml-hip.cpp comm_allgather).  Before round 4 a timed-out wait copied the stale slot
+// and advanced the epoch, so the peers' epochs drifted apart and every later wait timed out in turn:
+// one late peer became a cascade of bounded waits whose sum outran the caller's join (the 3-rank
+// loopback "deadlock" of the round-3 suite).
 __global__ __launch_bounds__(256) void k_p2p_allgather(const P2PArgs a, const float *__restrict__ send,
                                                         int64_t count, float *__restrict__ recv) {
     const int me = a.me, R = a.R;
     const int tid = threadIdx.x;
     const uint64_t e = a.ctl[0] + 1;                 // written only by the previous launch's last workgroup
     const int slot = (int)(e & 1);
+    const bool failed = __hip_atomic_load(a.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    const float qnan = __builtin_nanf("");
     if (blockIdx.x == 0 && recv + (int64_t)me * count != send)   // own slice (not in place)
         for (int64_t i = tid; i < count; i += blockDim.x) recv[(int64_t)me * count + i] = send[i];
     if (R > 1) {
         const int q = (me + 1 + (int)blockIdx.x) % R;
+        __shared__ int s_ok;
+        if (failed) {
+            for (int64_t i = tid; i < count; i += blockDim.x) recv[(int64_t)q * count + i] = qnan;
+            return;
+        }
         float *dst = a.land[q] + ((int64_t)slot * R + me) * a.cap;
         for (int64_t i = tid; i < count; i += blockDim.x) dst[i] = send[i];    // stores over xGMI
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -35,19 +51,27 @@ __global__ __launch_bounds__(256) void k_p2p_allgather(const P2PArgs a, const fl
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");                  // system scope: the peer's view
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(a.flag[q] + me, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            // wait for q's slice in this rank's landing buffer (bounded: a peer that never arrives sets
-            // the error word instead of hanging the device)
-            uint32_t spins = 0;
+            // wait for q's slice in this rank's landing buffer, bounded in time (a peer that never
+            // arrives fails the comm instead of hanging the device)
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            int ok = 1;
             while (__hip_atomic_load(a.flag[me] + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 21)) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
                     __hip_atomic_fetch_or(a.ctl + 2, 1ull << q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (a.herr) __hip_atomic_store(a.herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    ok = 0;
                     break;
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            s_ok = ok;
         }
         __syncthreads();
+        if (!s_ok) {                                  // never the stale slot: the segment reads NaN
+            for (int64_t i = tid; i < count; i += blockDim.x) recv[(int64_t)q * count + i] = qnan;
+            return;                                   // the epoch stays: the comm is failed
+        }
         const float *src = a.land[me] + ((int64_t)slot * R + q) * a.cap;
         for (int64_t i = tid; i < count; i += blockDim.x) recv[(int64_t)q * count + i] = src[i];
     }

@@ -120,28 +120,6 @@ struct RowBegins {
 hipError_t scatter_slabs(const float *slabs, int nranks, int64_t max_rows, const RowBegins &row_begin,
                          int64_t N, float *y, int64_t ldy, hipStream_t s);
 
-// Chain of dependent decode (N = 1) mul_mats as overlapped launches (q4_0_chain.hip): task t is one
-// launch of <= CUs 8-wave workgroups that loads its weights, waits for task t-1's per-workgroup flags
-// (= the chain's epoch, bumped once per chain launch) and publishes its own.
-constexpr int CHAIN_OVL_MAX_PPL = 6;          // K <= 6 * 4096
-constexpr int CHAIN_FLAGS_PER_TASK = 256;     // flag words per task (>= workgroups of one launch)
-struct ChainOvlTask {
-    const void *W[4];                         // unused siblings repeat W[0] / y[0]
-    float *y[4];
-    int rb[3];                                // row_begin[1..3] (unused = M)
-    int64_t M, K;
-    const float *x;
-    int index;
-};
-int chain_ovl_rows_per_wave(int64_t K);      // register-ring depth of the instantiation for K (0: none)
-int chain_ovl_occupancy(int64_t K);          // resident workgroups per CU (>= 2 for overlap)
-size_t chain_ovl_lds_bytes(int64_t K);
-int chain_ovl_grid(int64_t M, int num_cus);
-hipError_t chain_ovl_bump(uint32_t *epoch, uint32_t *err, hipStream_t s);
-hipError_t chain_ovl_launch(const ChainOvlTask &t, const uint32_t *wait, int nwait, uint32_t *flags,
-                            const uint32_t *epoch, uint32_t *err, int spin_limit, int num_cus, hipStream_t s,
-                            unsigned long long *stamps = nullptr);
-
 // Direct-store all-gather over xGMI (p2p_gather.hip): land[r] = rank r's landing buffer as mapped in
 // this process ([2 slots][R][cap] floats), flag[r] = its R flag words, ctl = this rank's control block
 // (epoch, arrivals, error bits).
@@ -149,7 +127,9 @@ constexpr int P2P_MAX_RANKS = 8;
 struct P2PArgs {
     float *land[P2P_MAX_RANKS];
     uint64_t *flag[P2P_MAX_RANKS];
-    uint64_t *ctl;
+    uint64_t *ctl;                   // [0] epoch, [1] arrivals, [2] error bits (peer q timed out: bit q)
+    uint32_t *herr;                  // host-mapped error word (nonzero: the comm failed), or nullptr
+    uint64_t timeout;                // peer-wait bound in s_memrealtime ticks (100 MHz)
     int me, R;
     int64_t cap;
 };

@@ -249,8 +249,8 @@ def _ptr(b):
 
 
 class Chain:
-    """A decode chain (ggml_hip_chain_*): tasks = [(ws, Ms, K, x, ys), ...] run in order as one
-    persistent launch; task t reads x after every earlier task wrote its y."""
+    """A decode chain (ggml_hip_chain_*): tasks = [(ws, Ms, K, x, ys), ...] run in stream order, one
+    sibling GEMV per task; task t reads x after every earlier task wrote its y."""
 
     def __init__(self, tasks):
         L = load()

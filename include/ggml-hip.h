@@ -230,6 +230,12 @@ int ggml_hip_comm_destroy(ggml_hip_comm *comm);
  * current device when devices is NULL; give each rank its own stream).  Every split entry point
  * below runs the same code on either transport.  Destroy each comm with ggml_hip_comm_destroy. */
 int ggml_hip_comm_init_local(ggml_hip_comm **comms, int nranks, const int *devices);
+/* One process per rank without RCCL: the comm's host collectives (allreduce_host, the P2P handle
+ * exchange) go through files in dir, a directory every rank can read and write (rank r writes
+ * <dir>/c<seq>_r<r>).  Device all-gathers need the P2P transport (ggml_hip_comm_enable_p2p); the RCCL
+ * transport is unavailable.  It also lets several processes share ONE device (RCCL refuses that),
+ * which is how the cross-process IPC path of the P2P all-gather is tested on a one-GPU box. */
+int ggml_hip_comm_init_file(ggml_hip_comm **comm, int nranks, int rank, const char *dir);
 int ggml_hip_comm_rank(const ggml_hip_comm *comm, int *rank, int *nranks);
 /* Direct-store all-gather (SURVEY.md §8e's P2P alternative to ncclAllGather for latency-bound decode
  * gathers): each rank stores its slice straight into every peer's landing buffer over xGMI (an IPC
@@ -237,14 +243,24 @@ int ggml_hip_comm_rank(const ggml_hip_comm *comm, int *rank, int *nranks);
  * kernel per all-gather, graph-capturable (the epoch advances on the device).  Collective: call on
  * every rank of the comm with the same max_floats (the largest slice of one all-gather, floats);
  * at most 8 ranks.  After it the comm's all-gathers (the split mul_mats) use P2P stores;
- * set_transport(comm, 0) returns to RCCL (1 = P2P again).  p2p_status synchronizes the device and
- * returns 0, or a bit mask of peers whose data never arrived (bounded wait; results invalid). */
+ * set_transport(comm, 0) returns to RCCL (1 = P2P again).  Every rank takes part in every collective of
+ * enable_p2p and the outcome is the group's: all ranks enable it or all return an error.
+ * Failure: a peer's data that does not arrive within the timeout (set_p2p_timeout, ms; <= 0 selects
+ * GGML_HIP_P2P_TIMEOUT_MS, default 10000) FAILS the comm for good: that gather writes NaN into the
+ * peer's segment (never the stale landing slot), later gathers fill every peer segment with NaN
+ * without waiting, and the next split mul_mat / all-gather on the comm returns GGML_HIP_ERR_COMM
+ * before enqueueing anything (the reference stops at its first failed copy, CUDA_CHECK,
+ * ggml-cuda.cu:22-51).  p2p_status synchronizes the device and returns 0, or the bit mask of peers
+ * whose data never arrived (sticky). */
 int ggml_hip_comm_enable_p2p(ggml_hip_comm *comm, int64_t max_floats);
 int ggml_hip_comm_set_transport(ggml_hip_comm *comm, int transport);
 int ggml_hip_comm_p2p_status(ggml_hip_comm *comm);
+int ggml_hip_comm_set_p2p_timeout(ggml_hip_comm *comm, double ms);
 /* All-reduce of n <= 64 host doubles in place (op 0 sum, 1 max, 2 min) over the comm; synchronous,
  * so it is also a barrier (bench harness: max-over-ranks timing without a second runtime). */
 int ggml_hip_comm_allreduce_host(ggml_hip_comm *comm, double *vals, int n, int op);
+/* All-gather of host bytes: recv[r * bytes ...] = rank r's send (every transport; synchronous). */
+int ggml_hip_comm_allgather_host(ggml_hip_comm *comm, const void *send, size_t bytes, void *recv);
 /* Row split of M rows over nranks by cumulative fractions (NULL = equal split), the same
  * rule as the reference's tensor_split (ggml-cuda.cu:1863-1882, 2361-2368).  row_begin has
  * nranks+1 entries. */

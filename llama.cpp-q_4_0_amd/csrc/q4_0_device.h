@@ -1,0 +1,136 @@
+// q4_0_device.h — device helpers shared by the gfx950 (CDNA4) kernels of the ggml q4_0 x f32 mul_mat
+// (internal to libggml_hip.so).  The kernels, one file per family:
+//
+// What each kernel restates (reference = ggml.c of Fcucgvhhhvjv/llama.cpp-q_4_0):
+//   q4_0_quant.hip:
+//   k_quantize_q8_0   quantize_row_q8_0, AVX2 branch ggml.c:1192-1275 (bit-exact: max|x|,
+//                     d = amax/127.f (IEEE div), fp16(d) RNE, id = amax ? 127.f/amax : 0,
+//                     q = sat8(round-half-even(x*id)))
+//   k_quantize_q4_0   quantize_row_q4_0_reference ggml.c:918-953 (bit-exact)
+//   k_dequantize_q4_0 dequantize_row_q4_0 ggml.c:1500-1518
+//   q4_0_gemv.hip:
+//   k_gemv_q4_0<NT>   mul_mat_q_f32 (ggml.c:11353-11411) for N <= 8 tokens: INIT (q8_0 of x)
+//                     fused into the prologue (into LDS, once per workgroup), COMPUTE =
+//                     ggml_vec_dot_q4_0_q8_0 (ggml.c:2339-2607) with one wave64 per weight row
+//   q4_0_gemm.hip:
+//   k_gemm7/8_q4_0    the same product for prefill batches on the int8 matrix cores
+//                     (v_mfma_i32_32x32x32_i8: K=32 = exactly one q4_0/q8_0 block, so every
+//                     MFMA yields the exact per-block integer sum the CPU computes); k_gemm7 reads
+//                     the q4_0 bytes in place, k_gemm8 an int8 image of the weights
+//   k_gemm9_q4_0      the default prefill GEMM on weight images: the same exact block sums from the
+//                     block-scaled fp6 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e2m3 operands), as f32
+//   q4_0_exact.hip:
+//   k_mm_exact_q4_0   exact mode: the AVX2 branch's fp32 schedule, bit for bit
+//
+// Numerics: every per-block integer sum is exact (as on the CPU); the fp32 accumulation of
+// d_w*d_x*sumi runs in a different order than AVX2's 8-lane fma chain, so y agrees with the
+// reference within the fp32-accumulation bound (tests/parity.py), not bitwise.
+#pragma once
+#include "q4_0_kernels.h"
+#include "launch.h"
+
+#include <climits>
+#include <cstdlib>
+
+namespace ghip {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+static constexpr int QK = 32;
+static constexpr int Q4B = 18;   // sizeof(block_q4_0)
+static constexpr int Q8B = 34;   // sizeof(block_q8_0)
+static constexpr int RSRC_FLAGS = 0x00020000;  // gfx950 buffer descriptor dword3 (raw, 32-bit)
+
+__device__ __forceinline__ float h2f(uint32_t bits) {
+    _Float16 h;
+    const uint16_t b = (uint16_t)bits;
+    __builtin_memcpy(&h, &b, 2);
+    return (float)h;                       // v_cvt_f32_f16, exact
+}
+
+__device__ __forceinline__ uint32_t f2h(float f) {
+    // opaque barrier: keeps hipcc from folding a preceding multiply into v_fma_mix with a +0
+    // addend, which turns -0.0 into +0.0 (ggml stores fp16(-0.0) = 0x8000 for all-zero blocks)
+    asm volatile("" : "+v"(f));
+    const _Float16 h = (_Float16)f;        // v_cvt_f16_f32, round-to-nearest-even
+    uint16_t b;
+    __builtin_memcpy(&b, &h, 2);
+    return b;
+}
+
+// _mm256_round_ps(nearest-even) -> cvtps_epi32 (NaN / out of range -> INT_MIN) -> packs x2
+__device__ __forceinline__ int q8_round_sat(float v) {
+    const float r = __builtin_rintf(v);
+    int i = (r >= -2147483648.0f && r < 2147483648.0f) ? (int)r : INT_MIN;
+    i = i > 127 ? 127 : i;
+    return i < -128 ? -128 : i;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, RSRC_FLAGS);
+}
+
+// ---- cross-lane reductions on DPP (no LDS round trip) -------------------------------------
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {      // lanes outside ROW_MASK read 0
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_QUAD_XOR1 = 0xB1;     // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;     // quad_perm [2,3,0,1]
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;
+constexpr int DPP_ROW_MIRROR = 0x140;
+constexpr int DPP_ROW_BCAST15 = 0x142;
+constexpr int DPP_ROW_BCAST31 = 0x143;
+
+// max / sum over each group of 8 consecutive lanes (every lane of the group gets the result)
+__device__ __forceinline__ float group8_max(float v) {
+    v = fmaxf(v, dpp_f<DPP_QUAD_XOR1>(v));
+    v = fmaxf(v, dpp_f<DPP_QUAD_XOR2>(v));
+    return fmaxf(v, dpp_f<DPP_ROW_HALF_MIRROR>(v));
+}
+__device__ __forceinline__ int group8_sum(int v) {
+    v += dpp_i<DPP_QUAD_XOR1>(v);
+    v += dpp_i<DPP_QUAD_XOR2>(v);
+    return v + dpp_i<DPP_ROW_HALF_MIRROR>(v);
+}
+// sum over the 64 lanes; the total is valid in lane 63 (fixed order -> deterministic)
+__device__ __forceinline__ float wave_sum_lane63(float v) {
+    v += dpp_f<DPP_QUAD_XOR1>(v);
+    v += dpp_f<DPP_QUAD_XOR2>(v);
+    v += dpp_f<DPP_ROW_HALF_MIRROR>(v);
+    v += dpp_f<DPP_ROW_MIRROR>(v);
+    v += dpp_f<DPP_ROW_BCAST15, 0xA>(v);
+    v += dpp_f<DPP_ROW_BCAST31, 0xC>(v);
+    return v;
+}
+
+// One q8_0 block spread over 8 consecutive lanes, 4 floats each (lane group g = lane>>3).
+// Returns the packed int8x4 of this lane; d16 = fp16(amax/127.f); qsum = sum of the 32 q.
+__device__ __forceinline__ uint32_t q8_block_lane(float4 v, uint32_t &d16, int &qsum) {
+    float a = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+    a = group8_max(a);
+    const float d = a / 127.f;                         // correctly rounded (no fast-math)
+    const float id = (a != 0.0f) ? 127.f / a : 0.0f;
+    d16 = f2h(d);
+    const int q0 = q8_round_sat(v.x * id), q1 = q8_round_sat(v.y * id);
+    const int q2 = q8_round_sat(v.z * id), q3 = q8_round_sat(v.w * id);
+    qsum = group8_sum(q0 + q1 + q2 + q3);
+    return (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) | ((uint32_t)(q2 & 0xFF) << 16) |
+           ((uint32_t)(q3 & 0xFF) << 24);
+}
+
+// GGML_HIP_* tuning / test overrides read once (host)
+static inline int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+}  // namespace ghip

@@ -64,9 +64,6 @@ hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M
 void gemv_set_policy(int map, int depth, int rowitems, int wg_per_cu);
 void gemv_set_bal(int bal);   // -1 auto, 0 off, 1 every chunked decode launch (K > 12288)
 
-// diagnostic: copy the per-wave phase stamps of the last GGML_HIP_GEMV_DIAG=7 launch
-hipError_t gemv_read_stamps(unsigned long long *host, int n);
-hipError_t gemm_read_stamps(unsigned long long *host, int n);
 
 // Prefill path: int8 MFMA (v_mfma_i32_32x32x32_i8, K=32 = one q4_0 block) GEMM on the
 // pre-quantized activations xs (quantize_q8_0_soa).

@@ -61,6 +61,8 @@ def _bind(L):
         "ggml_hip_comm_enable_p2p": ([vp, i64], i32),
         "ggml_hip_comm_set_transport": ([vp, i32], i32),
         "ggml_hip_comm_p2p_status": ([vp], i32),
+        "ggml_hip_comm_set_p2p_timeout": ([vp, ctypes.c_double], i32),
+        "ggml_hip_comm_init_file": ([vp, i32, i32, cp], i32),
         "ggml_hip_weight_image_free": ([vp], i32),
         "ggml_hip_weight_image_bytes": ([], i64),
         "ggml_hip_debug_set_gemm_version": ([i32], i32),
@@ -71,6 +73,7 @@ def _bind(L):
         "ggml_hip_comm_init_local": ([vp, i32, vp], i32),
         "ggml_hip_comm_rank": ([vp, vp, vp], i32),
         "ggml_hip_comm_allreduce_host": ([vp, vp, i32, i32], i32),
+        "ggml_hip_comm_allgather_host": ([vp, vp, sz, vp], i32),
         "ggml_hip_stream_create": ([], vp),
         "ggml_hip_stream_destroy": ([vp], i32),
         "ggml_hip_split_rows": ([i64, i32, vp, vp], i32),

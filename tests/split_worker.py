@@ -1,6 +1,10 @@
 """One rank of tests/test_gpu_split.py::test_split_rccl_multiprocess (RCCL transport, one process
-per GPU).  argv: rank world idfile.  The backend is loaded before anything else (no torch), rank 0
-writes the RCCL unique id to idfile, the others poll for it.  Each rank runs
+per GPU) or ::test_split_p2p_ipc_two_processes (mode "ipc": the file-rendezvous comm,
+ggml_hip_comm_init_file, with the direct-store P2P all-gather across processes, any number of ranks
+per device: hipIpcGetMemHandle / hipIpcOpenMemHandle of the fine-grained landing buffers and the
+system-scope flag protocol of p2p_gather.hip).  argv: rank world idfile [mode].  The backend is loaded
+before anything else (no torch); in RCCL mode rank 0 writes the unique id to idfile, the others poll
+for it; in ipc mode the comm's files live in idfile's directory.  Each rank runs
 ggml_hip_mul_mat_q4_0_split / _split_multi on the LLaMA-13B shapes (equal and uneven splits) and
 compares its gathered y_full bitwise against the concatenation of the per-slice products, which it
 computes itself on its own device (every rank knows every slice's weights: same seeds)."""
@@ -20,8 +24,11 @@ import oracle as O  # noqa: E402
 
 def main():
     rank, world, idfile = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    mode = sys.argv[4] if len(sys.argv) > 4 else "rccl"
     L = gh.load()
     gh.check(L.ggml_hip_set_device(rank % L.ggml_hip_device_count()), "set_device")
+    if mode == "ipc":
+        return main_ipc(L, rank, world, os.path.dirname(idfile))
     uid = ctypes.create_string_buffer(128)
     if rank == 0:
         gh.check(L.ggml_hip_comm_unique_id(uid))
@@ -99,6 +106,48 @@ def main():
         nchecks += 1
     gh.check(L.ggml_hip_comm_destroy(comm))
     print(f"SPLIT_OK rank {rank}/{world}: {nchecks} checks", flush=True)
+
+
+def main_ipc(L, rank, world, cdir):
+    comm = ctypes.c_void_p()
+    gh.check(L.ggml_hip_comm_init_file(ctypes.byref(comm), world, rank, cdir.encode()), "comm_init_file")
+    s = L.ggml_hip_stream_create()
+    cases = [(4096, 1024, 1, None), (4096, 1000, 1, [0.3, 0.7]), (4096, 1024, 3, None), (4096, 1000, 40, [1.0, 2.0])]
+    gh.check(L.ggml_hip_comm_enable_p2p(comm, max(N * M for _, M, N, _ in cases)), "enable_p2p (IPC)")
+    nchecks = 0
+    for (K, M, N, fr) in cases:
+        fr = fr if fr is None or len(fr) == world else None
+        wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED6100 + M + N, 0.0, 0.02).reshape(M, K))
+        x = O.gaussian(N * K, 0x5EED7300 + N, 0.0, 1.0).reshape(N, K)
+        rb = np.zeros(world + 1, np.int64)
+        fa = np.asarray(fr, np.float32) if fr is not None else None
+        gh.check(L.ggml_hip_split_rows(M, world, fa.ctypes.data_as(ctypes.c_void_p) if fa is not None else None,
+                                       rb.ctypes.data_as(ctypes.c_void_p)))
+        xd = gh.DeviceBuffer.from_array(x)
+        expect = []
+        for r in range(world):                 # every slice's product, computed alone on this device
+            wd_r, yd_r = gh.DeviceBuffer.from_array(wq[rb[r]:rb[r + 1]]), gh.DeviceBuffer(N * int(rb[r + 1] - rb[r]) * 4)
+            gh.mul_mat(wd_r, K, int(rb[r + 1] - rb[r]), xd, N, yd_r)
+            expect.append(yd_r.download((N, int(rb[r + 1] - rb[r])), np.float32))
+        expect = np.concatenate(expect, axis=1)
+        wd = gh.DeviceBuffer.from_array(wq[rb[rank]:rb[rank + 1]])
+        yd = gh.DeviceBuffer(N * M * 4)
+        for it in range(5):                    # epochs cycle through both landing slots
+            L.ggml_hip_memset(yd.ptr, 0x7F, yd.nbytes, s)
+            gh.check(L.ggml_hip_mul_mat_q4_0_split(comm, wd.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p), xd.ptr, N,
+                                                   yd.ptr, s), f"split (IPC P2P) {K}x{M} N={N} it {it}")
+            got = yd.download((N, M), np.float32, stream=s)
+            assert np.array_equal(got.view(np.uint32), expect.view(np.uint32)), (K, M, N, fr, it)
+            nchecks += 1
+        if N == 1 and fr is None:              # the oracle on the gathered rows (tests/parity.py bound)
+            from parity import block_terms, check_y
+            _, s_abs = block_terms(wq, O.quantize_q8_0(x, "avx2"), K)
+            check_y(got, O.mul_mat(wq, K, x, nthreads=4), s_abs, 1e-3, 1e-6)
+    st = L.ggml_hip_comm_p2p_status(comm)
+    assert st == 0, f"p2p status {st}"
+    L.ggml_hip_stream_destroy(s)
+    gh.check(L.ggml_hip_comm_destroy(comm))
+    print(f"P2P_IPC_OK rank {rank}/{world}: {nchecks} checks", flush=True)
 
 
 if __name__ == "__main__":

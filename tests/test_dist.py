@@ -64,3 +64,33 @@ def test_row_split_allgather_matches_full(world):
                 raise
     for r, (p, o) in enumerate(zip(procs, outs)):
         assert p.returncode == 0 and f"DIST_OK rank {r}" in o, o[-3000:]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_file_comm_ranks_drive_product_host_code(world):
+    """World-size 2 and 3 on CPU through the LIBRARY in every rank (tests/file_comm_worker.py: no torch,
+    so libggml_hip.so loads): the file-rendezvous comm, each rank's own ggml_hip_split_rows, the padded-slab
+    all-gather through ggml_hip_comm_allgather_host, ggml_hip_comm_allreduce_host sum / max / min;
+    y == the unsharded oracle product bitwise."""
+    cases = [(4096, 256, 1, None, 21), (4544, 200, 3, None, 22), (4096, 130, 2, [3.0, 1.0, 2.0][:world], 23),
+             (64, 5, 4, [0.0, 1.0, 1.0][:world], 24)]
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "cases.json")
+        json.dump(cases, open(path, "w"))
+        cdir = os.path.join(td, "comm")
+        os.mkdir(cdir)
+        env = dict(os.environ, GGML_HIP_COMM_FILE_TIMEOUT_S="60")
+        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "file_comm_worker.py"), str(r), str(world), cdir,
+                                   path], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+                 for r in range(world)]
+        outs = []
+        for p in procs:
+            try:
+                outs.append(p.communicate(timeout=180)[0])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        for r, (p, o) in enumerate(zip(procs, outs)):
+            assert p.returncode == 0, f"rank {r}:\n{o[-3000:]}"
+            assert "FILE_COMM_OK" in o, o[-2000:]

@@ -1,4 +1,4 @@
-"""CPU checks of the arithmetic behind k_gemm9 (csrc/q4_0_kernels.hip `e2m3_half`, `f6_pack`):
+"""CPU checks of the arithmetic behind k_gemm9 (csrc/q4_0_gemm.hip `e2m3_half`, `f6_pack`):
 the block-scaled fp6 MFMA computes the exact q4_0 x q8_0 block sum when
 
   weights  w = nibble - 8 in [-8, 7] enter as the e2m3 value w/2 with block scale 2^1, and
@@ -78,7 +78,7 @@ def test_pack_layout_round_trips():
 
 
 def e2m3_half_branchfree(n):
-    """the device encoder as compiled (csrc/q4_0_kernels.hip e2m3_half): e = (a >= 4) + (a >= 8),
+    """the device encoder as compiled (csrc/q4_0_gemm.hip e2m3_half): e = (a >= 4) + (a >= 8),
     c = (a << (2 - e)) + 8e, sign from bit 31 of n"""
     a = abs(n)
     e = int(a >= 4) + int(a >= 8)
@@ -91,7 +91,7 @@ def test_branchfree_encoder_equals_definition():
 
 
 def g9_tile(i, G, Mt, ny, xcd):
-    """k_gemm9's workgroup id -> (row tile, token tile) (csrc/q4_0_kernels.hip, G9Mats.xcd)"""
+    """k_gemm9's workgroup id -> (row tile, token tile) (csrc/q4_0_gemm.hip, G9Mats.xcd)"""
     j = i
     if xcd:
         C = G >> 3

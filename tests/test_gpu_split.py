@@ -176,6 +176,10 @@ def test_split_multi_loopback_ranks(R, N, Ms, uneven):
         for i, M in enumerate(Ms):
             got = yds[r][i].download((N, M), np.float32)
             assert np.array_equal(got.view(np.uint32), expect[i].view(np.uint32)), (r, i)
+    xq = O.quantize_q8_0(x, "avx2")             # and the gathered product against the oracle
+    for w, e in zip(ws, expect):
+        _, s_abs = block_terms(w, xq, K)
+        check_y(e, O.mul_mat(w, K, x, nthreads=8), s_abs, RTOL, ATOL_BLOCKS)
 
 
 def test_split_slab_path_graph_capture():
@@ -327,6 +331,100 @@ def test_split_multi_p2p_graph_replay(R):
         for i, M in enumerate(Ms):
             got = yds[r][i].download((N, M), np.float32)
             assert np.array_equal(got.view(np.uint32), expect[i].view(np.uint32)), (r, i)
+
+
+def test_split_p2p_ipc_two_processes_one_gpu():
+    """The cross-process P2P path on one MI355X: two fresh processes (tests/split_worker.py, mode ipc)
+    share device 0 through the file-rendezvous comm (RCCL refuses two ranks on one device), exchange
+    IPC handles of their fine-grained landing buffers (hipIpcGetMemHandle / hipIpcOpenMemHandle) and
+    run split mul_mats whose all-gather is the direct-store kernel with system-scope flags across the
+    process boundary: y_full bitwise the per-slice products (equal / uneven partitions, N = 1 / 3 / 40,
+    five epochs each), the oracle bound on the gathered rows, no peer wait timed out."""
+    R = 2
+    with tempfile.TemporaryDirectory() as td:
+        idfile = os.path.join(td, "uid")
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "split_worker.py"), str(r), str(R), idfile, "ipc"],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                 for r in range(R)]
+        outs = []
+        for p in procs:
+            try:
+                outs.append(p.communicate(timeout=100)[0])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        for r, (p, o) in enumerate(zip(procs, outs)):
+            assert p.returncode == 0, f"rank {r} failed:\n{o[-3000:]}"
+            assert "P2P_IPC_OK" in o, o[-2000:]
+
+
+def test_p2p_timeout_fails_the_comm():
+    """A peer that never gathers: the waiting rank's gather gives up after the timeout, writes NaN into
+    that peer's segment (never the stale landing slot), marks the comm failed (p2p_status bit), and the
+    NEXT split call returns GGML_HIP_ERR_COMM before enqueueing anything; a later gather does not wait."""
+    import time
+    K, M, N = 4096, 1024, 1
+    wq, x = make_case(K, M, N, seed=77)
+    rb = split_rows(M, 2)
+    L = ggml_hip.load()
+    xd = DB.from_array(x)
+    wd = DB.from_array(wq[rb[0]:rb[1]])
+    y = DB(N * M * 4)
+    comms = (ctypes.c_void_p * 2)()
+    ggml_hip.check(L.ggml_hip_comm_init_local(comms, 2, None))
+    c0, c1 = ctypes.c_void_p(comms[0]), ctypes.c_void_p(comms[1])
+    s = L.ggml_hip_stream_create()
+    try:
+        th = threading.Thread(target=lambda: ggml_hip.check(L.ggml_hip_comm_enable_p2p(c1, N * M)))
+        th.start()
+        ggml_hip.check(L.ggml_hip_comm_enable_p2p(c0, N * M))
+        th.join(timeout=60)
+        ggml_hip.check(L.ggml_hip_comm_set_p2p_timeout(c0, 200.0))
+        L.ggml_hip_memset(y.ptr, 0, y.nbytes, s)
+        t0 = time.time()
+        ggml_hip.check(L.ggml_hip_mul_mat_q4_0_split(c0, wd.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p), xd.ptr,
+                                                     N, y.ptr, s), "first split (rank 1 never gathers)")
+        ggml_hip.check(L.ggml_hip_stream_synchronize(s))
+        waited = time.time() - t0
+        assert L.ggml_hip_comm_p2p_status(c0) == 1 << 1            # peer 1's data never arrived
+        got = y.download((N, M), np.float32, stream=s)
+        own = gpu_y(wq[rb[0]:rb[1]], K, x)
+        assert np.array_equal(got[:, rb[0]:rb[1]].view(np.uint32), own.view(np.uint32))
+        assert np.all(np.isnan(got[:, rb[1]:rb[2]])), "a timed-out peer segment must read NaN, not a stale slot"
+        assert 0.15 < waited < 30, waited
+        rc = L.ggml_hip_mul_mat_q4_0_split(c0, wd.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p), xd.ptr, N, y.ptr, s)
+        assert rc == ggml_hip.ERR_COMM, rc                         # the comm is failed: error, nothing enqueued
+        assert L.ggml_hip_comm_p2p_status(c0) == 1 << 1            # sticky
+    finally:
+        L.ggml_hip_stream_destroy(s)
+        L.ggml_hip_comm_destroy(c0)
+        L.ggml_hip_comm_destroy(c1)
+
+
+def test_p2p_loopback_refusal_is_uniform():
+    """Ranks on devices [0, 0, 0, 1] (or all on device 0 on a one-GPU box): every rank refuses P2P,
+    including one on a device with fewer ranks (the decision was per rank before)."""
+    L = ggml_hip.load()
+    ndev = L.ggml_hip_device_count()
+    devs = [0, 0, 0, 1 if ndev > 1 else 0]
+    comms = (ctypes.c_void_p * 4)()
+    ggml_hip.check(L.ggml_hip_comm_init_local(comms, 4, (ctypes.c_int * 4)(*devs)))
+    out = [None] * 4
+
+    def body(r):
+        L.ggml_hip_set_device(devs[r])
+        out[r] = L.ggml_hip_comm_enable_p2p(ctypes.c_void_p(comms[r]), 1024)
+    th = [threading.Thread(target=body, args=(r,)) for r in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    L.ggml_hip_set_device(0)
+    for r in range(4):
+        L.ggml_hip_comm_destroy(ctypes.c_void_p(comms[r]))
+    assert out == [ggml_hip.ERR_UNSUPPORTED] * 4, out
 
 
 def test_p2p_api_errors():

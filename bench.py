@@ -49,6 +49,8 @@ EXTRA_CONFIGS = [
       ("w1", 5120, 13824), ("w3", 5120, 13824), ("w2", 13824, 5120)], [[0, 1, 2], [3], [4, 5], [6]]),
     ("Falcon-7B decode (config 5 shapes, arch/falcon)", 32,
      [("wqkv", 4544, 4672), ("wo", 4544, 4544), ("w1", 4544, 18176), ("w2", 18176, 4544)], [[0], [1], [2], [3]]),
+    ("GPT-NeoX-20B decode (config 5 shapes, arch/gptneox: n_embd 6144, n_ff 24576)", 44,
+     [("wqkv", 6144, 18432), ("wo", 6144, 6144), ("w1", 6144, 24576), ("w2", 24576, 6144)], [[0], [1], [2], [3]]),
 ]
 
 

@@ -364,6 +364,7 @@ bool aligned(const void *p, size_t a) { return ((uintptr_t)p % a) == 0; }
 struct WCacheEntry {
     void *dev = nullptr;
     size_t bytes = 0;
+    size_t img_bytes = 0;          // the prefill weight image built for this copy (counted in the budget)
     uint64_t fp = 0;
     uint64_t last_use = 0;
 };
@@ -464,7 +465,7 @@ const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, ui
     if (it != g_wc.end()) {                                        // stale: same address, new bytes
         wimage_drop(it->second.dev, it->second.bytes);
         HIP_FATAL(GHIP_SYNC(hipFree)(it->second.dev));
-        g_wc_resident -= it->second.bytes;
+        g_wc_resident -= it->second.bytes + it->second.img_bytes;
         g_wc.erase(it);
     }
     while (g_wc_resident + bytes > wcache_budget()) {             // LRU eviction
@@ -475,7 +476,7 @@ const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, ui
         if (victim == g_wc.end()) break;                           // everything is in use: over budget
         wimage_drop(victim->second.dev, victim->second.bytes);
         HIP_FATAL(GHIP_SYNC(hipFree)(victim->second.dev));
-        g_wc_resident -= victim->second.bytes;
+        g_wc_resident -= victim->second.bytes + victim->second.img_bytes;
         g_wc.erase(victim);
     }
     WCacheEntry e;
@@ -492,6 +493,24 @@ const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, ui
     return e.dev;
 }
 
+// A prefill weight image built for a cached copy (its device address `dev`) counts against the cache
+// budget with the copy and is dropped with it (images of cached copies used to sit outside the
+// budget).  GGML_HIP_WEIGHT_CACHE_IMAGES=0: no images for cached copies (their prefill reads the q4_0
+// bytes in place).
+bool wcache_images_enabled() {
+    static const bool on = !getenv("GGML_HIP_WEIGHT_CACHE_IMAGES") || atoi(getenv("GGML_HIP_WEIGHT_CACHE_IMAGES")) != 0;
+    return on;
+}
+void wcache_note_image(int id, const void *dev, size_t img_bytes) {
+    std::lock_guard<std::mutex> lk(g_wc_mu);
+    for (auto &e : g_wc)
+        if (e.first.device == id && e.second.dev == dev && e.second.img_bytes == 0) {
+            e.second.img_bytes = img_bytes;
+            g_wc_resident += img_bytes;                // evicted from at the next miss that needs room
+            return;
+        }
+}
+
 // drop every cached copy whose host range overlaps [host, host + bytes) (bytes == 0: contains host);
 // the next mul_mat re-uploads.  Returns the number of copies dropped.
 int64_t wcache_invalidate(const void *host, size_t bytes) {
@@ -503,7 +522,7 @@ int64_t wcache_invalidate(const void *host, size_t bytes) {
         if (a < hi && lo < b) {
             wimage_drop(it->second.dev, it->second.bytes);
             HIP_FATAL(GHIP_SYNC(hipFree)(it->second.dev));   // hipFree waits for work that still reads it
-            g_wc_resident -= it->second.bytes;
+            g_wc_resident -= it->second.bytes + it->second.img_bytes;
             it = g_wc.erase(it);
             n++;
             g_wc_invalidations++;
@@ -1958,8 +1977,12 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
             }
             // prefill (N > IMG_MIN_N) of a resident weight: build its image once (fp6 for k_gemm9, int8
             // under version 8; a failure to allocate it leaves the q4_0 bytes to k_gemm7 / split-K)
-            if (w_resident && N > IMG_MIN_N && !exact_mode() && (gemm_version() == 8 || gemm_version() == 10))
-                (void)wimage_ensure(id, w, K, rows, s);
+            if (w_resident && N > IMG_MIN_N && !exact_mode() && (gemm_version() == 8 || gemm_version() == 10) &&
+                (src0_dev || wcache_images_enabled())) {
+                const bool had = wimage_find(id, w, K, rows) != nullptr;
+                if (wimage_ensure(id, w, K, rows, s) && !had && !src0_dev)
+                    wcache_note_image(id, w, image_format() == 9 ? ghip::gemm9_w_bytes(K, rows) : ghip::gemm8_w_bytes(K, rows));
+            }
             // activations
             const float *x;
             const size_t xbytes = (size_t)N * K * 4;

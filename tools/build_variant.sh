@@ -1,12 +1,18 @@
 #!/bin/bash
-# Builds variants/libggml_hip_NAME.so with extra -D flags on the kernel file (A/B experiments):
-#   bash tools/build_variant.sh ws4 -DGEMV_WSLEEP=4
+# Builds variants/libggml_hip_NAME.so with extra -D flags on one kernel file (A/B experiments):
+#   [FILE=q4_0_gemv] bash tools/build_variant.sh xwf0 -DGEMV_XWF=0
+# (the other objects come from the in-tree build: run `make -C llama.cpp-q_4_0_amd` first)
 set -e
 cd "$(dirname "$0")/../llama.cpp-q_4_0_amd"
 name=$1; shift
+file=${FILE:-q4_0_gemv}
 mkdir -p ../variants/obj_$name
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 -I../include"
-$H ${NOKFLAGS:-$(sed -n "s/^KFLAGS *= *//p" Makefile)} "$@" -c csrc/q4_0_kernels.hip -o ../variants/obj_$name/q4_0_kernels.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../variants/libggml_hip_$name.so build/ggml-hip.o build/ggml-hip-graph.o \
-    ../variants/obj_$name/q4_0_kernels.o build/q4_0_chain.o build/ggml_ops.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+$H ${NOKFLAGS:-$(sed -n "s/^KFLAGS *= *//p" Makefile)} "$@" -c csrc/$file.hip -o ../variants/obj_$name/$file.o
+objs=""
+for o in build/*.o; do
+  [ "$(basename $o .o)" = "$file" ] && objs="$objs ../variants/obj_$name/$file.o" || objs="$objs $o"
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../variants/libggml_hip_$name.so $objs \
+    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -rf ../variants/obj_$name

@@ -822,6 +822,35 @@ def test_gemm9_sibling_group_one_launch_bitwise(K, Ms, N):
             L.ggml_hip_weight_image_free(wd.ptr)
 
 
+def test_multi_mixed_image_siblings_fresh_stream_workspace():
+    """a sibling group at a split-K N (gemv_max < N <= 64) whose tall middle sibling has an fp6
+    image takes the image GEMM, which needs the larger workspace; on a fresh stream (empty workspace) the
+    group must size it before the first sibling quantizes x into it, or the third sibling reads a freed
+    buffer.  Every y bitwise equal to one call per matrix on the default stream."""
+    L = ggml_hip.load()
+    K, N, Ms = 4096, 32, (4096, 11008, 4096)
+    cases = [make_case(K, M, N, seed=900 + i) for i, M in enumerate(Ms)]
+    x = cases[0][1]
+    wds = [DB.from_array(c[0]) for c in cases]
+    ggml_hip.check(L.ggml_hip_weight_image_create(wds[1].ptr, K, Ms[1], None), "image")
+    s = L.ggml_hip_stream_create()
+    try:
+        xd = DB.from_array(x)
+        ys = [DB(N * M * 4) for M in Ms]
+        for y in ys:
+            L.ggml_hip_memset(y.ptr, 0x7F, y.nbytes, s)
+        ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys, stream=s)
+        ggml_hip.check(L.ggml_hip_stream_synchronize(s))
+        for wd, y, M in zip(wds, ys, Ms):
+            single = DB(N * M * 4)
+            ggml_hip.mul_mat(wd, K, M, xd, N, single)
+            got = y.download((N, M), np.float32, stream=s)
+            assert np.array_equal(got.view(np.uint32), single.download((N, M), np.float32).view(np.uint32)), M
+    finally:
+        L.ggml_hip_stream_destroy(s)
+        L.ggml_hip_weight_image_free(wds[1].ptr)
+
+
 def test_gemm8_image_api_errors():
     L = ggml_hip.load()
     wq, _ = make_case(128, 64, 1, seed=3)

@@ -317,7 +317,9 @@ const char *ggml_hip_version(void);
    2 silu/mul, 3 rope/cpy, 4 f16 mul_mat/permute/cpy, 5 q4_0 mul_mat run while a silu is pending,
    6 sibling q4_0 GEMVs sharing src1 run as one group: wq|wk|wv, w1|w3, 7 independent rope /
    rope->cpy / cpy nodes held behind a group run as one launch, 8 decode scale -> diag_mask_inf ->
-   soft_max -> KQV -> merged copy as one launch) */
+   soft_max -> KQV -> merged copy as one launch, 9 / 10 decode norm / silu chain run in the q4_0
+   GEMV prologue, 11 prefill norm / silu chain that wrote the k_gemm9 x image of its output for the
+   q4_0 mul_mats consuming it) */
 int    ggml_hip_debug_op_stats(int64_t *counts, int n, int reset);
 /* debug: the attention's f16 x f32 mul_mat on device pointers (synchronous); tiled = 0 one 32-lane
    group per output, 1 the LDS-tiled kernel, -1 the backend's choice (bit-identical either way) */

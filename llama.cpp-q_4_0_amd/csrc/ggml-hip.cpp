@@ -926,7 +926,9 @@ std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of th
 // q4_0 mul_mat run under a pending silu, sibling q4_0 GEMVs (wq|wk|wv, w1|w3) run as one group,
 // independent rope / rope->cpy / cpy nodes held behind a group run as one launch, the decode
 // soft_max chain with its KQV and merged copy as one launch
-constexpr int N_FUSED = 11;
+// soft_max chain with its KQV and merged copy as one launch, the decode norm / silu chains in the GEMV
+// prologue (9, 10), the prefill chains that wrote the k_gemm9 x image of their output (11)
+constexpr int N_FUSED = 12;
 std::atomic<int64_t> g_fused[N_FUSED];
 
 // fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)
@@ -1083,8 +1085,9 @@ void run_device_op(tensor *t, const tensor *fused_cpy = nullptr) {
             char *d = c.out(t);
             float *merged =
                 fused_cpy ? (float *)((ggml_tensor_extra_gpu *)fused_cpy->src1->extra)->data_device[c.id] : nullptr;
+            // fast mode: the many-row (prefill) products on the matrix cores; exact mode: the AVX chains bit for bit
             HIP_FATAL(ghip::op_mul_mat_f16_f32(pa, pb, (float *)d, (int)a->ne[0], a->ne[1], b->ne[1], a->ne[2], a->nb[1],
-                                               a->nb[2], nb11, nb12, c.s, merged));
+                                               a->nb[2], nb11, nb12, c.s, merged, exact_mode() ? -1 : -2));
             c.finish(t, d);
             return;
         }
@@ -1110,6 +1113,19 @@ bool norm_fold_enabled() {
     if (v < 0) {
         v = (!getenv("GGML_HIP_NORM_FOLD") || atoi(getenv("GGML_HIP_NORM_FOLD")) != 0) ? 1 : 0;
         g_norm_fold.store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
+// GGML_HIP_X9_FOLD=0: a prefill norm / silu chain whose consumers all take k_gemm9 runs as its own
+// launch and the mul_mats build the x image themselves (k_prep9_x); on (default), the chain's kernel
+// writes the image beside its f32 output
+std::atomic<int> g_x9_fold{-1};
+bool x9_fold_enabled() {
+    int v = g_x9_fold.load(std::memory_order_relaxed);
+    if (v < 0) {
+        v = (!getenv("GGML_HIP_X9_FOLD") || atoi(getenv("GGML_HIP_X9_FOLD")) != 0) ? 1 : 0;
+        g_x9_fold.store(v, std::memory_order_relaxed);
     }
     return v == 1;
 }
@@ -1226,6 +1242,7 @@ struct NormChain {
     float *sum = nullptr, *norm = nullptr, *out = nullptr;
     const uint16_t *table = nullptr;
     int64_t ncols = 0;
+    int64_t nrows = 1;             // > 1: a prefill chain held for q4_0 mul_mats on fp6 images (x image fold)
 };
 NormChain g_norm;
 void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst);
@@ -1298,6 +1315,12 @@ void flush_pending() {
 bool dev_overlap(const tensor *a, const tensor *b);
 size_t span_bytes(const tensor *t);
 
+// a chain of nrows rows that may be held for the k_gemm9 x image fold
+bool x9_chain_ok(int64_t ncols, int64_t nrows) {
+    return x9_fold_enabled() && !exact_mode() && gemm_version() == 10 && nrows > IMG_MIN_N && ghip::op_x9_ok(ncols, nrows) &&
+           nrows * ncols < ((int64_t)1 << 31);
+}
+
 // t arrives while a chain is pending: extend the chain, complete it in one launch, or let a q4_0
 // mul_mat that touches none of its buffers run first.  false: t does not fit (caller flushes).
 bool try_fuse(tensor *t) {
@@ -1339,6 +1362,12 @@ bool try_fuse(tensor *t) {
             for (const tensor *i : {(const tensor *)(add ? add->src0 : nullptr), (const tensor *)(add ? add->src1 : x),
                                     (const tensor *)t->src1})
                 if (o && i && dev_overlap(o, i)) fold = false;
+        // many rows (prefill): hold it too; if the q4_0 mul_mats that consume it all take k_gemm9, its
+        // launch writes their x image (flush_group_x9), else it runs as below when they flush it
+        if (x9_chain_ok(c.ncols, gabi::nrows(t)) && al(c.a) && al(c.b) && al(c.sum) && al(c.norm) && al(c.w) && al(c.out)) {
+            fold = true;
+            c.nrows = gabi::nrows(t);
+        }
         if (fold) {
             for (int i = 0; i < p.n; i++) c.node[c.nn++] = p.node[i];
             c.node[c.nn++] = hold(t);
@@ -1419,6 +1448,11 @@ bool try_fuse(tensor *t) {
         for (const tensor *o : {(const tensor *)last, (const tensor *)t})
             for (const tensor *i : {(const tensor *)last->src0, (const tensor *)t->src1})
                 if (dev_overlap(o, i)) fold = false;
+        if (x9_chain_ok(c.ncols, gabi::nrows(t)) && t->ne[2] == 1 && t->ne[3] == 1 && al(c.a) && al(c.b) && al(c.norm) &&
+            al(c.out)) {
+            fold = true;
+            c.nrows = gabi::nrows(t);
+        }
         if (fold) {
             c.node[c.nn++] = last;
             c.node[c.nn++] = hold(t);
@@ -1681,9 +1715,9 @@ void launch_norm_chain(const NormChain &c) {
     const int id = g_main_device;
     HIP_FATAL(hipSetDevice(id));
     if (c.kind == 2)
-        HIP_FATAL(ghip::op_silu_mul_f32(c.a, c.b, c.norm, c.out, c.ncols, c.table, g_dev[id].stream));
+        HIP_FATAL(ghip::op_silu_mul_f32(c.a, c.b, c.norm, c.out, c.ncols * c.nrows, c.table, g_dev[id].stream));
     else
-        HIP_FATAL(ghip::op_add_rms_norm_mul_f32(c.a, c.b, c.sum, c.norm, c.w, c.out, c.ncols, 1, g_dev[id].stream));
+        HIP_FATAL(ghip::op_add_rms_norm_mul_f32(c.a, c.b, c.sum, c.norm, c.w, c.out, c.ncols, c.nrows, g_dev[id].stream));
     for (int i = 0; i < c.nn; i++) count_node(c.node[i]);
     g_fused[c.kind == 2 ? 2 : 0].fetch_add(1, std::memory_order_relaxed);
 }
@@ -1694,20 +1728,78 @@ void flush_norm() {
 }
 // may a held norm chain's output feed q4_0 mul_mat m through its GEMV prologue?
 bool norm_feeds(const NormChain &c, const tensor *m) {
-    if (!c.on || !same_tensor(m->src1, c.out_node) || m->src1->ne[1] != 1 || m->src0->ne[0] != c.ncols) return false;
+    if (!c.on || !same_tensor(m->src1, c.out_node) || m->src1->ne[1] != c.nrows || m->src0->ne[0] != c.ncols) return false;
     // m's output must not alias anything the prologue reads or workgroup 0 stores
     const char *y = dptr(m);
-    const size_t yb = span_bytes(m), row = (size_t)c.ncols * 4;
+    const size_t yb = span_bytes(m), row = (size_t)c.ncols * (size_t)c.nrows * 4;
     for (const void *q : {(const void *)c.a, (const void *)c.b, (const void *)c.w, (const void *)c.sum,
                           (const void *)c.norm, (const void *)c.out})
         if (q && (const char *)q < y + yb && y < (const char *)q + row) return false;
     return true;
 }
 
+// prefill (N > IMG_MIN_N) mul_mats of resident weights take k_gemm9 on an fp6 image built once
+// (mul_mat_node's rule, here for a group's members)
+void ensure_group_images(const Group &g) {
+    const int64_t N = g.mm[0]->src1->ne[1];
+    if (N <= IMG_MIN_N || exact_mode() || (gemm_version() != 8 && gemm_version() != 10)) return;
+    const int id = g_main_device;
+    HIP_FATAL(hipSetDevice(id));
+    for (int i = 0; i < g.n; i++) wimage_ensure(id, dptr(g.mm[i]->src0), g.mm[i]->src0->ne[0], g.mm[i]->src0->ne[1], g_dev[id].stream);
+}
+
+// A held prefill chain and the q4_0 mul_mats that consume it: when every member takes k_gemm9 on an
+// fp6 image, the chain's launch writes the x image beside its f32 output and the members run as one
+// k_gemm9 launch on it (no k_prep9_x; the image is bitwise gemm9_prep_x's of the chain's output, so y
+// is bitwise the unfused path's).  false: not every member qualifies (nothing launched).
+bool flush_group_x9(const Group &g) {
+    const NormChain &c = g.norm;
+    const int id = g_main_device;
+    const int64_t K = c.ncols, N = c.nrows;
+    if (gemm_version() != 10 || N * K >= ((int64_t)1 << 31)) return false;
+    const void *img[4];
+    int64_t M[4], ldy[4];
+    float *y[4];
+    for (int i = 0; i < g.n; i++) {
+        const tensor *a = g.mm[i]->src0;
+        int fmt = 0;
+        M[i] = ldy[i] = a->ne[1];
+        img[i] = wimage_find(id, dptr(a), K, M[i], &fmt);
+        if (!img[i] || fmt != 9 || M[i] * (K / QK) * Q4B >= ((int64_t)1 << 31) || M[i] >= (1 << 30)) return false;
+        y[i] = (float *)dptr(g.mm[i]);
+    }
+    hipStream_t s = g_dev[id].stream;
+    void *ws = nullptr;
+    if (stream_workspace(id, s, workspace_bytes_mm(K, N, 0), &ws) != GGML_HIP_OK) return false;
+    void *xws = (char *)ws + ws_g8x_offset(K, N);
+    const int64_t Np = ghip::gemm9_np(N);
+    HIP_FATAL(hipSetDevice(id));
+    if (c.kind == 2)
+        HIP_FATAL(ghip::op_silu_mul_f32_x9(c.a, c.b, c.norm, c.out, K, N, c.table, xws, Np, s));
+    else
+        HIP_FATAL(ghip::op_add_rms_norm_mul_f32_x9(c.a, c.b, c.sum, c.norm, c.w, c.out, K, N, xws, Np, s));
+    HIP_FATAL(ghip::gemm9_run_multi(g.n, img, M, K, xws, N, y, ldy, s));
+    for (int i = 0; i < c.nn; i++) count_node(c.node[i]);
+    for (int i = 0; i < g.n; i++) count_node(g.mm[i]);
+    g_fused[c.kind == 2 ? 2 : 0].fetch_add(1, std::memory_order_relaxed);
+    g_fused[11].fetch_add(1, std::memory_order_relaxed);
+    if (g.n > 1) g_fused[6].fetch_add(1, std::memory_order_relaxed);
+    return true;
+}
+
 void flush_group() {
     const Group g = g_grp;
     g_grp = Group{};
-    if (g.norm.on) {                      // the GEMVs run the held norm chain in their prologue
+    if (g.n > 0) ensure_group_images(g);
+    if (g.norm.on && g.norm.nrows > 1) {  // a held prefill chain: the x image fold, or its own launch first
+        const bool done = flush_group_x9(g);
+        if (!done) launch_norm_chain(g.norm);
+        if (done) {
+            const int k = run_elem_prefix(g.after, g.na);
+            for (int i = k; i < g.na; i++) execute_node(g.after[i]);
+            return;
+        }
+    } else if (g.norm.on) {               // the GEMVs run the held norm chain in their prologue
         const void *w[4];
         int64_t m[4], ldy[4];
         float *y[4];
@@ -3465,6 +3557,14 @@ int ggml_hip_debug_set_norm_fold(int on) {
     return GGML_HIP_OK;
 }
 
+// not in the public header: the prefill x image fold (a held norm / silu chain writes the k_gemm9 x image
+// of its output for the q4_0 mul_mats that consume it) on (1) / off (0)
+int ggml_hip_debug_set_x9_fold(int on) {
+    flush_deferred();
+    g_x9_fold.store(on ? 1 : 0);
+    return GGML_HIP_OK;
+}
+
 // not in the public header: launch recording for the hook path: 0 off, 1 HIP graphs, 2 launcher thread
 int ggml_hip_debug_set_graph(int on) {
     flush_deferred();
@@ -3473,7 +3573,8 @@ int ggml_hip_debug_set_graph(int on) {
 }
 
 // debug: the f16 x f32 mul_mat of the attention on device pointers (tests/test_gpu_f16_mul_mat.py):
-// tiled 0 = one 32-lane group per output, 1 = the LDS-tiled kernel, -1 = the backend's choice
+// tiled 0 = one 32-lane group per output, 1 = the LDS-tiled kernel, -1 = the backend's choice (bitwise
+// kernels), 2 = the fast-mode MFMA kernel, -2 = the backend's fast-mode choice
 int ggml_hip_debug_f16_mul_mat(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11,
                                int64_t ne02, int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, float *merged,
                                int tiled) {

@@ -29,7 +29,8 @@ hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne
 // merged != nullptr: also the contiguous copy of permute(dst, 0, 2, 1, 3) (fused KQV_merged_contiguous)
 hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11, int64_t ne02,
                               int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12, hipStream_t s,
-                              float *merged = nullptr, int tiled = -1);   // tiled: -1 auto, 0 / 1 force
+                              float *merged = nullptr, int tiled = -1);   // tiled: -1 auto (bitwise kernels), 0 / 1 force those;
+                              // 2 the fast-mode MFMA kernel, -2 auto with it (ne11 >= 32)
 // rope (as op_rope_f32) whose output is then copied (ggml_cpy, F32 -> F32/F16) into the strided view c
 hipError_t op_rope_cpy_f32(const void *x, void *d, const int64_t ne[4], const int64_t nbx[4], const int64_t nbd[4],
                            const void *cs, int npairs, void *c, bool to_f16, int64_t ne10, int64_t ne11, int64_t nb10,
@@ -75,5 +76,13 @@ hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *
 // u = silu(a) -> out = u * b (same shape)
 hipError_t op_silu_mul_f32(const float *a, const float *b, float *u, float *out, int64_t n, const uint16_t *table,
                            hipStream_t s);
+// The same chains with the k_gemm9 x image of out written beside it into xws (codes [nb][3][Np][16 B] +
+// fp16 d_x [nb][Np], nb = ncols / 32; bitwise what gemm9_prep_x makes of out).  ncols % 64 == 0,
+// ncols <= 16384, 16-byte aligned operands; hipErrorInvalidValue otherwise (nothing launched).
+bool op_x9_ok(int64_t ncols, int64_t nrows);
+hipError_t op_add_rms_norm_mul_f32_x9(const float *a, const float *b, float *sum, float *norm, const float *w, float *out,
+                                      int64_t ncols, int64_t nrows, void *xws, int64_t Np, hipStream_t s);
+hipError_t op_silu_mul_f32_x9(const float *a, const float *b, float *u, float *out, int64_t ncols, int64_t nrows,
+                              const uint16_t *table, void *xws, int64_t Np, hipStream_t s);
 
 }  // namespace ghip

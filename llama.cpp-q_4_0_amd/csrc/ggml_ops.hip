@@ -23,6 +23,7 @@
 // per row where the CPU reduces over a row, one lane per element otherwise.
 #include "ggml_ops.h"
 #include "launch.h"
+#include "q4_0_device.h"
 
 #include <cmath>
 
@@ -611,17 +612,35 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     }
 }
 
+// row of workgroup i for the image producers: the 8 rows of octet q = 8 * (j / 8) + i % 8 (j = i / 8)
+// on XCD i % 8, consecutively
+__device__ __forceinline__ int64_t x9_row(int64_t i) {
+    const int64_t j = i >> 3;
+    return (((j >> 3) << 3) + (i & 7)) * 8 + (j & 7);
+}
+
 // The same [add ->] rms_norm [-> mul] with one 1024-thread workgroup per row: every thread loads
 // its float4 pieces of the row at once (up to NV per thread, held in registers), the double sum is
 // reduced by shuffles and LDS, and the row is written from the registers.  One wave per row walks
 // a 4096-wide row with 64 dependent load round trips (24 us per launch, measured); this form takes
 // one.  Rows with ncols % 4 != 0, more than 4096*NV values or unaligned pointers use the kernels above.
+// IMG: the k_gemm9 x image of `out` is written beside it (the q4_0 mul_mats that consume the row then
+// skip k_prep9_x): thread t's pieces are elements 4t, 4t + 4096, ... of the row, so the 8 threads of a
+// q8_0 block are 8 consecutive lanes, as x9_store_lane takes them, and the codes come from the very
+// floats stored in out (the image is bitwise k_prep9_x's of out).  The image keeps 8 consecutive
+// tokens' 16-byte pieces in one 128-byte line, so the 8 rows of a line run on one XCD (workgroup i runs
+// on XCD i % 8): the line is completed in that XCD's L2 instead of leaving it as 8 partial writes
+// (x9_row; the grid is nrows rounded up to 64).
 constexpr int RN_THREADS = 1024, RN_NV = 4;
+template <bool IMG>
 __global__ __launch_bounds__(RN_THREADS) void k_row_norm4(const float *a, const float *b, float *sum, float *norm,
-                                                          const float *w, float *out, int64_t ncols) {
+                                                          const float *w, float *out, int64_t ncols, int64_t nrows,
+                                                          uint8_t *ximg, uint16_t *xd16, int64_t Np) {
     __shared__ double part[RN_THREADS / 64];
     const int tid = threadIdx.x;
-    const int64_t o = (int64_t)blockIdx.x * ncols;
+    const int64_t row = IMG ? x9_row(blockIdx.x) : (int64_t)blockIdx.x;
+    if (IMG && row >= nrows) return;                     // workgroup-uniform: rows past the padded grid
+    const int64_t o = row * ncols;
     const int64_t n4 = ncols / 4;
     float4 v[RN_NV];
     double s = 0.0;
@@ -653,14 +672,84 @@ __global__ __launch_bounds__(RN_THREADS) void k_row_norm4(const float *a, const 
 #pragma unroll
     for (int k = 0; k < RN_NV; k++) {
         const int64_t i4 = tid + (int64_t)k * RN_THREADS;
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i4 < n4) {
             const float4 x = v[k];
             const float4 y = make_float4(x.x * scale, x.y * scale, x.z * scale, x.w * scale);
             if (norm) reinterpret_cast<float4 *>(norm + o)[i4] = y;
             if (out) {
                 const float4 g = reinterpret_cast<const float4 *>(w)[i4];
-                reinterpret_cast<float4 *>(out + o)[i4] = make_float4(y.x * g.x, y.y * g.y, y.z * g.z, y.w * g.w);
+                r = make_float4(y.x * g.x, y.y * g.y, y.z * g.z, y.w * g.w);
+                reinterpret_cast<float4 *>(out + o)[i4] = r;
             }
+        }
+        if constexpr (IMG) {
+            if ((int64_t)k * RN_THREADS < n4)            // workgroup-uniform; every lane of a live wave calls
+                x9_store_lane(r, tid & 7, row, i4 >> 3, i4 < n4, ximg, xd16, Np);
+        }
+    }
+}
+
+// Fast mode (GGML_HIP_EXACT off): the same products on the f16 matrix cores (v_mfma_f32_32x32x16_f16,
+// exact fp16 products, fp32 sums in the instruction's order instead of the AVX chains', so within the
+// fp32-accumulation bound of the reference rather than bitwise).  A = src1 rows rounded to fp16 (the
+// tokens i1: MFMA rows), B = src0 rows as stored (i0: MFMA columns, so a row of 32 outputs is one
+// coalesced store).  Wave = 32 tokens x 64 src0 rows (two MFMAs sharing the A operand), workgroup = 2 x 2
+// waves = 64 x 128 outputs of one channel; operands straight from global memory (one head's K/V slice
+// and Q / soft_max rows stay in L2), 8 K elements per lane and step, zero past K.  vec: every row start
+// 16-byte aligned (one dwordx4 per operand piece), else element loads.
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+constexpr int FM_TI = 64, FM_TO = 128;     // workgroup tile: tokens (i1) x src0 rows (i0)
+
+__global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32_mfma(const char *s0, const char *s1, float *d, int K,
+                                                              int64_t ne01, int64_t ne11, int64_t ne02, int64_t nb01,
+                                                              int64_t nb02, int64_t nb11, int64_t nb12, float *merged,
+                                                              int vec) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int rl = lane & 31, kh = lane >> 5;
+    const int64_t i2 = blockIdx.z;
+    const int64_t t0 = (int64_t)blockIdx.y * FM_TI + (wave & 1) * 32;          // tokens of this wave
+    const int64_t o0 = (int64_t)blockIdx.x * FM_TO + (wave >> 1) * 64;         // src0 rows of this wave
+    const int64_t ta = t0 + rl < ne11 ? t0 + rl : ne11 - 1;                    // clamped: loaded, not stored
+    const int64_t ob0 = o0 + rl < ne01 ? o0 + rl : ne01 - 1, ob1 = o0 + 32 + rl < ne01 ? o0 + 32 + rl : ne01 - 1;
+    const float *ya = (const float *)(s1 + i2 * nb12 + ta * nb11);
+    const _Float16 *xb0 = (const _Float16 *)(s0 + i2 * nb02 + ob0 * nb01);
+    const _Float16 *xb1 = (const _Float16 *)(s0 + i2 * nb02 + ob1 * nb01);
+    f32x16v acc0 = {}, acc1 = {};
+    for (int k0 = 0; k0 < K; k0 += 16) {
+        const int k = k0 + 8 * kh;
+        h16x8 a, b0, b1;
+        if (vec && k + 8 <= K) {
+            const float4 y0 = *reinterpret_cast<const float4 *>(ya + k), y1 = *reinterpret_cast<const float4 *>(ya + k + 4);
+            a = h16x8{(_Float16)y0.x, (_Float16)y0.y, (_Float16)y0.z, (_Float16)y0.w,
+                      (_Float16)y1.x, (_Float16)y1.y, (_Float16)y1.z, (_Float16)y1.w};
+            b0 = *reinterpret_cast<const h16x8 *>(xb0 + k);
+            b1 = *reinterpret_cast<const h16x8 *>(xb1 + k);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const bool in = k + e < K;
+                a[e] = in ? (_Float16)ya[k + e] : (_Float16)0.0f;
+                b0[e] = in ? xb0[k + e] : (_Float16)0.0f;
+                b1[e] = in ? xb1[k + e] : (_Float16)0.0f;
+            }
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b1, acc1, 0, 0, 0);
+    }
+    // acc[r] = D[token t0 + (r & 3) + 8 (r >> 2) + 4 kh][src0 row o0 (+ 32) + rl]
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int64_t i1 = t0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        if (i1 >= ne11) continue;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int64_t i0 = o0 + 32 * h + rl;
+            if (i0 >= ne01) continue;
+            const float v = h ? acc1[r] : acc0[r];
+            d[(i2 * ne11 + i1) * ne01 + i0] = v;
+            if (merged) merged[(i1 * ne02 + i2) * ne01 + i0] = v;
         }
     }
 }
@@ -673,6 +762,32 @@ __global__ __launch_bounds__(TPB) void k_silu_mul(const float *a, const float *b
     const float s = h2f_bits(table[f2h_bits(a[i])]);
     if (u) u[i] = s;
     out[i] = s * b[i];
+}
+
+// k_silu_mul on float4 pieces of rows of ncols (ncols % 64 == 0) with the k_gemm9 x image of out written
+// beside it (bitwise k_prep9_x's of out); c4 = ncols / 4, so a q8_0 block is 8 consecutive lanes.  A
+// workgroup takes chunk c of TPB float4s of one row; the same chunk of 8 consecutive rows runs on one
+// XCD (as k_row_norm4<true>): workgroup i -> XCD x = i % 8, its j = i / 8-th item there = (row t = j % 8
+// of octet 8 * ((j / 8) / C) + x, chunk (j / 8) % C), C = chunks per row.
+__global__ __launch_bounds__(TPB) void k_silu_mul_x9(const float *a, const float *b, float *u, float *out, int64_t nrows,
+                                                     int64_t c4, int64_t C, const uint16_t *table, uint8_t *ximg,
+                                                     uint16_t *xd16, int64_t Np) {
+    const int64_t i = blockIdx.x, j = i >> 3, rest = j >> 3;
+    const int64_t row = ((rest / C) * 8 + (i & 7)) * 8 + (j & 7), chunk = rest % C;
+    if (row >= nrows) return;                            // workgroup-uniform
+    const int64_t c = chunk * TPB + threadIdx.x;         // float4 index within the row
+    const bool in = c < c4;
+    const int64_t i4 = row * c4 + c;
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (in) {
+        const float4 av = reinterpret_cast<const float4 *>(a)[i4], bv = reinterpret_cast<const float4 *>(b)[i4];
+        const float4 sv = make_float4(h2f_bits(table[f2h_bits(av.x)]), h2f_bits(table[f2h_bits(av.y)]),
+                                      h2f_bits(table[f2h_bits(av.z)]), h2f_bits(table[f2h_bits(av.w)]));
+        if (u) reinterpret_cast<float4 *>(u)[i4] = sv;
+        r = make_float4(sv.x * bv.x, sv.y * bv.y, sv.z * bv.z, sv.w * bv.w);
+        reinterpret_cast<float4 *>(out)[i4] = r;
+    }
+    x9_store_lane(r, threadIdx.x & 7, row, c >> 3, in, ximg, xd16, Np);
 }
 
 bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }   // nullptr passes (not accessed)
@@ -689,10 +804,38 @@ hipError_t op_add_rms_norm_mul_f32(const float *a, const float *b, float *sum, f
                                    int64_t ncols, int64_t nrows, hipStream_t s) {
     if (nrows <= 0) return hipSuccess;
     if (row_norm4_ok(ncols, a, b, sum, norm, w, out))
-        launch_k(k_row_norm4, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, a, b, sum, norm, w, out, ncols);
+        launch_k(k_row_norm4<false>, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, a, b, sum, norm, w, out, ncols,
+                 (int64_t)0, (uint8_t *)nullptr, (uint16_t *)nullptr, (int64_t)0);
     else
         launch_k(k_add_rms_norm_mul, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, a, b, sum, norm, w, out,
                            ncols, nrows);
+    return hipGetLastError();
+}
+
+bool op_x9_ok(int64_t ncols, int64_t nrows) {
+    return nrows > 0 && ncols > 0 && ncols % 64 == 0 && ncols <= 4 * RN_THREADS * RN_NV && nrows < (1 << 30);
+}
+
+hipError_t op_add_rms_norm_mul_f32_x9(const float *a, const float *b, float *sum, float *norm, const float *w, float *out,
+                                      int64_t ncols, int64_t nrows, void *xws, int64_t Np, hipStream_t s) {
+    if (!op_x9_ok(ncols, nrows) || !out || !xws || Np < nrows || !row_norm4_ok(ncols, a, b, sum, norm, w, out))
+        return hipErrorInvalidValue;
+    uint8_t *ximg = (uint8_t *)xws;
+    uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)(ncols / 32) * Np * 48);
+    launch_k(k_row_norm4<true>, dim3((unsigned)((nrows + 63) & ~63)), dim3(RN_THREADS), 0, s, a, b, sum, norm, w, out,
+             ncols, nrows, ximg, xd16, Np);
+    return hipGetLastError();
+}
+
+hipError_t op_silu_mul_f32_x9(const float *a, const float *b, float *u, float *out, int64_t ncols, int64_t nrows,
+                              const uint16_t *table, void *xws, int64_t Np, hipStream_t s) {
+    if (!op_x9_ok(ncols, nrows) || !out || !xws || Np < nrows || !al16(a) || !al16(b) || !al16(u) || !al16(out))
+        return hipErrorInvalidValue;
+    uint8_t *ximg = (uint8_t *)xws;
+    uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)(ncols / 32) * Np * 48);
+    const int64_t c4 = ncols / 4, C = (c4 + TPB - 1) / TPB;
+    launch_k(k_silu_mul_x9, dim3((unsigned)(((nrows + 63) & ~63) * C)), dim3(TPB), 0, s, a, b, u, out, nrows, c4, C, table,
+             ximg, xd16, Np);
     return hipGetLastError();
 }
 
@@ -761,8 +904,8 @@ hipError_t op_rms_norm_f32(const float *x, float *d, int64_t ncols, int64_t nrow
                            hipStream_t s) {
     if (nrows <= 0) return hipSuccess;
     if (ldx == ncols && ldd == ncols && row_norm4_ok(ncols, nullptr, x, nullptr, d, nullptr, nullptr))
-        launch_k(k_row_norm4, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, nullptr, x, nullptr, d, nullptr,
-                           nullptr, ncols);
+        launch_k(k_row_norm4<false>, dim3((unsigned)nrows), dim3(RN_THREADS), 0, s, nullptr, x, nullptr, d, nullptr,
+                 nullptr, ncols, (int64_t)0, (uint8_t *)nullptr, (uint16_t *)nullptr, (int64_t)0);
     else
         launch_k(k_rms_norm_f32, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, d, ncols, nrows, ldx, ldd);
     return hipGetLastError();
@@ -832,7 +975,20 @@ hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, i
     const int64_t nout = ne01 * ne11 * ne02;
     if (nout <= 0) return hipSuccess;
     static const int tiled_min = getenv("GGML_HIP_F16_TILED_MIN") ? atoi(getenv("GGML_HIP_F16_TILED_MIN")) : 8;
+    static const int mfma_min = getenv("GGML_HIP_F16_MFMA_MIN") ? atoi(getenv("GGML_HIP_F16_MFMA_MIN")) : 32;
     const bool fits = ne02 <= 65535 && (ne11 + FT - 1) / FT <= 65535;
+    if (fits && (tiled == 2 || (tiled == -2 && mfma_min > 0 && ne11 >= mfma_min))) {
+        // fast mode, many src1 rows (prefill): the matrix cores
+        auto a16 = [](int64_t v) { return (v & 15) == 0; };
+        const int vec = a16((int64_t)(uintptr_t)s0) && a16(nb01) && a16(nb02) && a16((int64_t)(uintptr_t)s1) && a16(nb11) &&
+                        a16(nb12);
+        launch_k(k_mul_mat_f16_f32_mfma, dim3((unsigned)((ne01 + FM_TO - 1) / FM_TO), (unsigned)((ne11 + FM_TI - 1) / FM_TI),
+                                              (unsigned)ne02),
+                 dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d, K, ne01, ne11, ne02, nb01, nb02, nb11, nb12, merged,
+                 vec);
+        return hipGetLastError();
+    }
+    if (tiled == -2) tiled = -1;
     if (fits && (tiled > 0 || (tiled < 0 && tiled_min > 0 && ne11 >= tiled_min))) {
         // many src1 rows (prefill): tiled through LDS, same bits
         launch_k(k_mul_mat_f16_f32_tiled, dim3((unsigned)((ne01 + FT - 1) / FT), (unsigned)((ne11 + FT - 1) / FT),

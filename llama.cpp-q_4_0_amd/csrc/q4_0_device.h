@@ -127,6 +127,67 @@ __device__ __forceinline__ uint32_t q8_block_lane(float4 v, uint32_t &d16, int &
            ((uint32_t)(q3 & 0xFF) << 24);
 }
 
+// e2m3 code of n/2 for an integer n in [-15, 15]
+// (branch-free: with e = (a >= 4) + (a >= 8), c = (a << (2 - e)) + 8e is 4a / 8 + 2a / 16 + a)
+__device__ __forceinline__ uint32_t e2m3_half(int n) {
+    const uint32_t a = (uint32_t)__builtin_abs(n);
+    const uint32_t e = (uint32_t)(a >= 4u) + (uint32_t)(a >= 8u);
+    return ((uint32_t)n >> 26 & 0x20u) | ((a << (2u - e)) + 8u * e);
+}
+// four 6-bit codes (elements 4m .. 4m+3) as one 24-bit field
+__device__ __forceinline__ uint32_t f6x4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    return c0 | (c1 << 6) | (c2 << 12) | (c3 << 18);
+}
+// The k_gemm9 x image of one q8_0 block held by 8 consecutive lanes, 4 floats each (lane group
+// sub = lane & 7; the q8_0 quantization of q8_block_lane): each lane's four q give four (q >> 4) and
+// four (q & 15) codes (24 bits each), and lanes 0-5 of the group assemble the block's six dwords of
+// each half from their neighbours' fields.  Image layout (k_gemm9): codes [nb][3][Np][16 B] (part 0 =
+// the first 16 B of the (q >> 4) codes, part 1 = those of the (q & 15) codes, part 2 = the last 8 B
+// of both, swapped for tokens with bit 4 set) + fp16 d_x [nb][Np].  Every lane of the wave must call it
+// (DPP); live = false: this lane's group stores nothing.  Shared by k_prep9_x and the producers that
+// write the image beside their f32 output (ggml_ops.hip).
+__device__ __forceinline__ void x9_store_lane(float4 v, int sub, int64_t n, int64_t b, bool live, uint8_t *ximg,
+                                              uint16_t *xd16, int64_t Np) {
+    uint32_t d16;
+    int qsum;
+    const uint32_t packed = q8_block_lane(v, d16, qsum);
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const int q = (int)(int8_t)(packed >> (8 * e));
+        hi[e] = e2m3_half(q >> 4);
+        lo[e] = e2m3_half(q & 15);
+    }
+    const uint32_t Fh = f6x4(hi[0], hi[1], hi[2], hi[3]), Fl = f6x4(lo[0], lo[1], lo[2], lo[3]);
+    // dword k of a half: fields s and s + 1 shifted by off (k = 0..5 -> (s, off) = (0,0) (1,8) (2,16)
+    // (4,0) (5,8) (6,16)); the fields of lanes +1 and +2 by DPP row shifts (groups of 8 lanes sit
+    // inside 16-lane rows; lanes 6 and 7, which read past their group, store nothing): k < 3 takes
+    // fields (own, +1), k >= 3 (+1, +2)
+    const int k = sub < 6 ? sub : 5;
+    const int off = 8 * (k % 3);
+    const bool lo3 = k < 3;
+    const uint32_t Fh1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Fh, 0x101, 0xF, 0xF, false);   // row_shl:1
+    const uint32_t Fh2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Fh, 0x102, 0xF, 0xF, false);   // row_shl:2
+    const uint32_t Fl1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Fl, 0x101, 0xF, 0xF, false);
+    const uint32_t Fl2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Fl, 0x102, 0xF, 0xF, false);
+    const uint32_t h0 = lo3 ? Fh : Fh1, h1 = lo3 ? Fh1 : Fh2;
+    const uint32_t l0 = lo3 ? Fl : Fl1, l1 = lo3 ? Fl1 : Fl2;
+    if (!live || sub >= 6) return;
+    const uint32_t dh = (h0 >> off) | (h1 << (24 - off)), dl = (l0 >> off) | (l1 << (24 - off));
+    const int sw = (int)((n >> 4) & 1);
+    uint32_t *p0 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 0) * Np + n) * 16);
+    uint32_t *p1 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 1) * Np + n) * 16);
+    uint32_t *p2 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 2) * Np + n) * 16);
+    if (k < 4) {
+        p0[k] = dh;
+        p1[k] = dl;
+    } else {
+        p2[2 * sw + k - 4] = dh;
+        p2[2 * (sw ^ 1) + k - 4] = dl;
+    }
+    if (sub == 0) xd16[b * Np + n] = (uint16_t)d16;
+}
+
 // GGML_HIP_* tuning / test overrides read once (host)
 static inline int env_int(const char *name, int dflt) {
     const char *e = getenv(name);

@@ -625,17 +625,6 @@ static constexpr int G9_SCALE_1 = 128, G9_SCALE_5 = 132;           // E8M0 block
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
-// e2m3 code of n/2 for an integer n in [-15, 15]
-// (branch-free: with e = (a >= 4) + (a >= 8), c = (a << (2 - e)) + 8e is 4a / 8 + 2a / 16 + a)
-__device__ __forceinline__ uint32_t e2m3_half(int n) {
-    const uint32_t a = (uint32_t)__builtin_abs(n);
-    const uint32_t e = (uint32_t)(a >= 4u) + (uint32_t)(a >= 8u);
-    return ((uint32_t)n >> 26 & 0x20u) | ((a << (2u - e)) + 8u * e);
-}
-// four 6-bit codes (elements 4m .. 4m+3) as one 24-bit field
-__device__ __forceinline__ uint32_t f6x4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-    return c0 | (c1 << 6) | (c2 << 12) | (c3 << 18);
-}
 // 32 codes = fields F0..F7 (24 bits each) -> 6 dwords, element j at bits 6j..6j+5
 __device__ __forceinline__ void f6_pack(const uint32_t *F, uint32_t *D) {
     D[0] = F[0] | (F[1] << 24);
@@ -646,9 +635,8 @@ __device__ __forceinline__ void f6_pack(const uint32_t *F, uint32_t *D) {
     D[5] = (F[6] >> 16) | (F[7] << 8);
 }
 
-// x: the q8_0 lane code of k_prep8_x (8 lanes per block, wave = 8 tokens of one block); each lane's
-// four q give four (q >> 4) and four (q & 15) codes (24 bits each), and lanes 0-5 of the group
-// assemble the block's six dwords of each half from their neighbours' fields.
+// x: 8 lanes per block (x9_store_lane), wave = 8 tokens of one block.  (Two or four blocks per wave with
+// all their loads in flight measured equal or slower: 0.338-0.345 vs 0.338-0.340 ms per prefill layer.)
 __global__ __launch_bounds__(256) void k_prep9_x(const float *__restrict__ x, int64_t K, int64_t N,
                                                   uint8_t *__restrict__ ximg, uint16_t *__restrict__ xd16, int64_t Np) {
     const int64_t nb = K / QK;
@@ -660,44 +648,7 @@ __global__ __launch_bounds__(256) void k_prep9_x(const float *__restrict__ x, in
     const int sub = lane & 7;
     float4 v = {0.f, 0.f, 0.f, 0.f};
     if (live) v = *reinterpret_cast<const float4 *>(x + n * K + b * QK + 4 * sub);
-    uint32_t d16;
-    int qsum;
-    const uint32_t packed = q8_block_lane(v, d16, qsum);
-    uint32_t hi[4], lo[4];
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-        const int q = (int)(int8_t)(packed >> (8 * e));
-        hi[e] = e2m3_half(q >> 4);
-        lo[e] = e2m3_half(q & 15);
-    }
-    const uint32_t Fh = f6x4(hi[0], hi[1], hi[2], hi[3]), Fl = f6x4(lo[0], lo[1], lo[2], lo[3]);
-    // dword k of a half: fields s and s + 1 shifted by off (k = 0..5 -> (s, off) = (0,0) (1,8) (2,16)
-    // (4,0) (5,8) (6,16))
-    const int k = sub < 6 ? sub : 5;
-    const int off = 8 * (k % 3);
-    // the fields of lanes +1 and +2 by DPP row shifts (groups of 8 lanes sit inside 16-lane rows; lanes
-    // 6 and 7, which read past their group, store nothing): k < 3 takes fields (own, +1), k >= 3 (+1, +2)
-    const uint32_t Fh1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Fh, 0x101, 0xF, 0xF, false);   // row_shl:1
-    const uint32_t Fh2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Fh, 0x102, 0xF, 0xF, false);   // row_shl:2
-    const uint32_t Fl1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Fl, 0x101, 0xF, 0xF, false);
-    const uint32_t Fl2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Fl, 0x102, 0xF, 0xF, false);
-    const bool lo3 = k < 3;
-    const uint32_t h0 = lo3 ? Fh : Fh1, h1 = lo3 ? Fh1 : Fh2;
-    const uint32_t l0 = lo3 ? Fl : Fl1, l1 = lo3 ? Fl1 : Fl2;
-    if (!live || sub >= 6) return;
-    const uint32_t dh = (h0 >> off) | (h1 << (24 - off)), dl = (l0 >> off) | (l1 << (24 - off));
-    const int sw = (int)((n >> 4) & 1);
-    uint32_t *p0 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 0) * Np + n) * 16);
-    uint32_t *p1 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 1) * Np + n) * 16);
-    uint32_t *p2 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 2) * Np + n) * 16);
-    if (k < 4) {
-        p0[k] = dh;
-        p1[k] = dl;
-    } else {
-        p2[2 * sw + k - 4] = dh;
-        p2[2 * (sw ^ 1) + k - 4] = dl;
-    }
-    if (sub == 0) xd16[b * Np + n] = (uint16_t)d16;
+    x9_store_lane(v, sub, n, b, live, ximg, xd16, Np);
 }
 
 // weights: one lane per (row, block pair), 128 consecutive rows of one pair per 128 lanes; rows >= M

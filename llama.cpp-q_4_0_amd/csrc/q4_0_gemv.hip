@@ -588,11 +588,8 @@ static hipError_t launch_gemv_rows(const GemvMats &m, int64_t K, const float *x,
                                : launch_gemv_w<NT, GEMV_WAVES, 2, VAR, 1>(m, K, x, dev, s);
         case 2: return rd == 1 ? launch_gemv_w<NT, GEMV_WAVES, 1, VAR, 2>(m, K, x, dev, s)
                                : launch_gemv_w<NT, GEMV_WAVES, 2, VAR, 2>(m, K, x, dev, s);
-        case 3: return rd == 1 ? launch_gemv_w<NT, GEMV_WAVES, 1, VAR, 3>(m, K, x, dev, s)
-                               : launch_gemv_w<NT, GEMV_WAVES, 2, VAR, 3>(m, K, x, dev, s);
-        case 4: return launch_gemv_w<NT, GEMV_WAVES, 1, VAR, 4>(m, K, x, dev, s);
-        case 5: return launch_gemv_w<NT, GEMV_WAVES, 1, VAR, 5>(m, K, x, dev, s);
-        default: return launch_gemv_w<NT, GEMV_WAVES, 1, VAR, 6>(m, K, x, dev, s);
+        default: return rd == 1 ? launch_gemv_w<NT, GEMV_WAVES, 1, VAR, 3>(m, K, x, dev, s)
+                                : launch_gemv_w<NT, GEMV_WAVES, 2, VAR, 3>(m, K, x, dev, s);
     }
 }
 
@@ -614,9 +611,7 @@ static hipError_t launch_gemv(const GemvMats &m, int64_t K, const float *x, cons
     if constexpr (NT == 1) {                        // decode: one item per row (PPL pairs per lane)
         const int rowitems = gemv_policy().rowitems;
         const int ppl = (int)((K / 64 + 63) / 64);
-        // row items up to GGML_HIP_GEMV_ROWMAX pairs per lane (3: K <= 12288; A/B 4..6, one row in flight)
-        static const int rowmax = env_int("GGML_HIP_GEMV_ROWMAX", 3);
-        if (rowitems && ppl <= (rowmax < 3 ? 3 : rowmax > 6 ? 6 : rowmax) && gemv_policy().bal != 1) {
+        if (rowitems && ppl <= 3) {
             const int rd = depth_env ? depth_env : 1;
             return var == 15 ? launch_gemv_rows<NT, 15>(m, K, x, dev, s, ppl, rd)
                              : launch_gemv_rows<NT, 3>(m, K, x, dev, s, ppl, rd);

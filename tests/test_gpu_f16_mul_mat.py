@@ -91,3 +91,44 @@ def test_tiled_matches_grouped_bitwise(name, K, ne01, ne11, ne02, layout):
         r = ref_dot_f16(x_of(i2, i0), y_of(i2, i1))
         g = outs[1][i2, i1, i0]
         assert abs(float(g) - float(r)) <= 2 * np.spacing(np.float32(abs(r)) + np.float32(1e-30)), (i2, i1, i0, g, r)
+
+
+@pytest.mark.parametrize("name,K,ne01,ne11,ne02,layout", CASES, ids=[c[0] for c in CASES])
+def test_mfma_fast_mode_within_fp32_bound(name, K, ne01, ne11, ne02, layout):
+    """The fast-mode kernel (tiled = 2: v_mfma_f32_32x32x16_f16 on the same fp16 operands; the backend
+    takes it for ne11 >= 32 outside exact mode): every output within the fp32-accumulation bound of the
+    exact sum of the fp16 products (float64 here), |d - ref| <= 1e-5 * sum|x * fp16(y)| + 1e-30, on the
+    strided K / V cache layouts, K tails past the last 16-element step and ragged tiles; merged copy
+    bitwise equal to dst."""
+    L = ggml_hip.load()
+    rng = np.random.default_rng(K * 7 + ne01 * 3 + ne11)
+    if layout == "kq":
+        n_embd = K * ne02
+        cache = (rng.standard_normal((ne01, n_embd)) * 0.5).astype(np.float16)
+        nb01, nb02 = n_embd * 2, K * 2
+        q = rng.standard_normal((ne11, ne02, K)).astype(np.float32)
+        src1, nb11, nb12 = q, ne02 * K * 4, K * 4
+        X = np.stack([cache[:, i2 * K:(i2 + 1) * K] for i2 in range(ne02)])        # [i2][i0][K]
+        Y = q.transpose(1, 0, 2)                                                   # [i2][i1][K]
+    else:
+        n_ctx = K + 7
+        cache = (rng.standard_normal((ne02, ne01, n_ctx)) * 0.5).astype(np.float16)
+        nb01, nb02 = n_ctx * 2, ne01 * n_ctx * 2
+        p = rng.random((ne02, ne11, K)).astype(np.float32)
+        p /= p.sum(-1, keepdims=True)
+        src1, nb11, nb12 = p, K * 4, ne11 * K * 4
+        X, Y = cache[:, :, :K], p
+    s0, s1 = DB.from_array(cache), DB.from_array(src1)
+    nout = ne01 * ne11 * ne02
+    d, m = DB(nout * 4), DB(nout * 4)
+    run(L, s0, s1, d, K, ne01, ne11, ne02, nb01, nb02, nb11, nb12, 2, m)
+    y = d.download((ne02, ne11, ne01), np.float32)
+    merged = m.download((ne11, ne02, ne01), np.float32)
+    assert np.array_equal(merged.view(np.uint32), y.transpose(1, 0, 2).view(np.uint32))
+    x64 = X.astype(np.float64)
+    y64 = Y.astype(np.float16).astype(np.float64)
+    ref = np.einsum("hik,hjk->hji", x64, y64)
+    sab = np.einsum("hik,hjk->hji", np.abs(x64), np.abs(y64))
+    err = np.abs(y.astype(np.float64) - ref)
+    assert np.isfinite(y).all()
+    assert (err <= 1e-5 * sab + 1e-30).all(), float((err / (sab + 1e-30)).max())

@@ -31,7 +31,7 @@ pytestmark = [pytest.mark.gpu,
 OPS = json.load(open(os.path.join(GOLD, "ggml_op_enum.json")))
 
 
-N_FUSED = 11  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
+N_FUSED = 12  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
 
 
 def op_stats(L, reset=True, fused=False):
@@ -236,6 +236,44 @@ def test_norm_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode):
     assert out[1][1][9] >= (2 * hp["n_layer"] - 1) * n_decode, out[1][1]
     assert out[1][1][10] >= hp["n_layer"] * n_decode, out[1][1]      # silu -> mul in the w2 prologue
     assert out[0][1][9] == 0 and out[0][1][10] == 0, out[0][1]
+    for k in (0, 2):                                                 # every chain still counted once
+        assert out[1][1][k] == out[0][1][k], (out[1][1], out[0][1])
+
+
+@pytest.mark.parametrize("n_prompt", [300, 97])
+def test_prefill_x_image_fold_bitwise_vs_prep(tmp_path, n_prompt):
+    """Prefill (N > 64 tokens) at full offload: the [add ->] rms_norm -> mul and silu -> mul chains whose
+    q4_0 consumers all take k_gemm9 on fp6 weight images write the x image in their own launch (no
+    k_prep9_x): the same logits bit for bit as the chains' own launches followed by the mul_mats' x prep,
+    and the fold fires for every device chain of the prompt eval (q|k|v and w1|w3 behind the norms, w2
+    behind silu -> mul; layer 0's attention norm reads the host embedding rows, so it is no device chain)."""
+    hp = HP128
+    L = ggml_hip.load()
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp, hp=hp)
+    nv = hp["n_vocab"]
+    lib = ctypes.CDLL(HIP_LIB)
+    lib.refllama_bench.restype = ctypes.c_int
+    lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    L.ggml_hip_debug_set_x9_fold.argtypes = [ctypes.c_int]
+    prev = L.ggml_hip_get_exact()
+    ggml_hip.check(L.ggml_hip_set_exact(0), "set_exact")
+    out = {}
+    try:
+        for fold in (1, 0):
+            ggml_hip.check(L.ggml_hip_debug_set_x9_fold(fold), "set_x9_fold")
+            op_stats(L)
+            lg = np.zeros(nv, np.float32)
+            res = np.zeros(3, np.float64)
+            assert lib.refllama_bench(mp.encode(), n_prompt, 2, 1, 99, 1024, 1, res.ctypes.data, lg.ctypes.data) == nv
+            out[fold] = (lg, op_stats(L, fused=True)[1])
+    finally:
+        L.ggml_hip_set_exact(prev)
+        L.ggml_hip_debug_set_x9_fold(1)
+    assert np.isfinite(out[1][0]).all()
+    assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
+    assert out[1][1][11] >= 3 * hp["n_layer"] - 1, out[1][1]
+    assert out[0][1][11] == 0, out[0][1]
     for k in (0, 2):                                                 # every chain still counted once
         assert out[1][1][k] == out[0][1][k], (out[1][1], out[0][1])
 

@@ -6,9 +6,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r04
 mkdir -p $O
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-step() {   # step <name> <seconds> <cmd...>
+step() {   # step <name> <seconds> <cmd...>  (counter passes: SIGKILL at the limit)
   local name=$1 t=$2; shift 2
-  timeout -k 10 $t "$@" > $O/$name.log 2>&1
+  case $name in gpmc*|pmc_*) timeout -s KILL $t "$@" > $O/$name.log 2>&1;; *) timeout -k 10 $t "$@" > $O/$name.log 2>&1;; esac
   local rc=$?
   echo "$name rc=$rc"
   case $rc in 0|1) return 0;; *) exit $rc;; esac
@@ -26,10 +26,10 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 python3 tools/pmc_summary.py $O/pmc > $O/gemv_pmc_traffic.json
 i=0
-IFS='|' read -ra sets <<< "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES|SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA|SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU|SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS|FETCH_SIZE|WRITE_SIZE|GRBM_GUI_ACTIVE SQ_INSTS_SALU|SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VMEM"
+IFS='|' read -ra sets <<< "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES|SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA|SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU|SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS|FETCH_SIZE|WRITE_SIZE|GRBM_GUI_ACTIVE SQ_INSTS_SALU"
 for c in "${sets[@]}"; do
   i=$((i+1))
-  step gpmc$i 90 rocprofv3 --pmc $c -d $O/gpmc/p$i -o run --output-format csv -- python3 tools/gemm_one.py
+  step gpmc$i 60 rocprofv3 --pmc $c -d $O/gpmc/p$i -o run --output-format csv -- python3 tools/gemm_one.py
 done
 python3 - <<'PY' > $O/gemm9_pmc.txt
 import csv, glob, collections
@@ -47,7 +47,6 @@ if "GRBM_GUI_ACTIVE" in g and "SQ_VALU_MFMA_BUSY_CYCLES" in g:
     print(f"derived: MFMA busy {g['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * 1024):.3f} of {cyc:.0f} cycles; "
           f"HBM read {2 * g.get('FETCH_SIZE', 0) * 1024 / 1e6:.1f} MB (2 x FETCH_SIZE, gfx950 half count); "
           f"write {g.get('WRITE_SIZE', 0) * 1024 / 1e6:.1f} MB; VALU per MFMA {g.get('SQ_INSTS_VALU', 0) / max(1, g.get('SQ_INSTS_MFMA', 1)):.1f}; "
-          f"WAIT_INST_ANY / WAVE_CYCLES {g.get('SQ_WAIT_INST_ANY', 0) / max(1, g.get('SQ_WAVE_CYCLES', 1)):.3f}; "
-          f"MFMA+VALU co-exec cycles / MFMA busy {g.get('SQ_VALU_MFMA_COEXEC_CYCLES', 0) / max(1, g['SQ_VALU_MFMA_BUSY_CYCLES']):.3f}")
+          f"WAIT_INST_ANY / WAVE_CYCLES {g.get('SQ_WAIT_INST_ANY', 0) / max(1, g.get('SQ_WAVE_CYCLES', 1)):.3f}")
 PY
 cat $O/gemm9_pmc.txt

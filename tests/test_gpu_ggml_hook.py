@@ -139,6 +139,37 @@ def test_large_cpu_weight_taken_at_decode(ref, N):
         ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
 
 
+def test_cached_weight_image_counted_in_cache_budget(ref):
+    """a residency-cache copy of a host weight that gets its fp6 image at its first prefill
+    (N > 64 through can_mul_mat) counts the image's bytes in the cache's resident total, the quantity the
+    LRU budget GGML_HIP_WEIGHT_CACHE_MB bounds; clearing the cache releases copy and image together."""
+    from hip_env import ggml_hip
+    L = ggml_hip.load()
+    L.ggml_hip_weight_image_bytes.restype = ctypes.c_int64
+    ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+    K, M, N = 4096, 256, 96
+    wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED7700, 0.0, 0.02).reshape(M, K))
+    x = O.gaussian(N * K, 0x5EED7800, 0.0, 1.0).reshape(N, K)
+
+    def resident():
+        h, m, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        ggml_hip.check(L.ggml_hip_weight_cache_stats(ctypes.byref(h), ctypes.byref(m), ctypes.byref(r)))
+        return r.value
+
+    img0 = L.ggml_hip_weight_image_bytes()
+    try:
+        y, be = ggml_mul_mat(ref, wq, K, x, 0, 2)
+        assert be == GGML_BACKEND_CPU
+        assert_close(wq, x, K, y, O.mul_mat(wq, K, x))
+        img = L.ggml_hip_weight_image_bytes() - img0
+        assert img == ((M + 127) // 128) * (K // 32) * 128 * 26        # the fp6 image (26 B per 32 weights)
+        assert resident() == M * K // 32 * 18 + img
+    finally:
+        ggml_hip.check(L.ggml_hip_weight_cache_clear(), "cache clear")
+    assert resident() == 0
+    assert L.ggml_hip_weight_image_bytes() == img0
+
+
 def _device_count():
     try:
         from hip_env import ggml_hip

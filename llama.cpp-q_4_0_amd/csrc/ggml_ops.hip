@@ -533,6 +533,53 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max(const float *x, flo
     for (int64_t i = lane; i < ncols; i += 64) d[o + i] = d[o + i] * inv;
 }
 
+// The same chain with the row held in registers (ncols <= 64 * NV): x read once, d written once (the
+// kernel above reads x twice and writes d twice); every value is computed by the same operations in the
+// same per-lane order (max, then e and its double sum in i = lane, lane + 64, ... order, then the wave
+// sums), so the output bits are the same.  Rows are independent, so d may alias x (the in-place chain).
+template <int NV>
+__global__ __launch_bounds__(TPB) void k_scale_mask_soft_max_reg(const float *x, float *scaled, float *masked,
+                                                                 float *d, float v, int64_t ncols, int64_t nrows,
+                                                                 int64_t rows_per_channel, int n_past,
+                                                                 const uint16_t *table) {
+    const int64_t r = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nrows) return;
+    const int64_t o = r * ncols, j = r % rows_per_channel;
+    float m[NV];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+        const int64_t i = lane + 64 * k;
+        m[k] = -INFINITY;
+        if (i < ncols) {
+            const float sv = x[o + i] * v;
+            m[k] = i > n_past + j ? -INFINITY : sv;
+            if (scaled) scaled[o + i] = sv;
+            if (masked) masked[o + i] = m[k];
+            mx = fmaxf(mx, m[k]);
+        }
+    }
+    mx = wave_max_f(mx);
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+        float e = 0.0f;
+        if (m[k] != -INFINITY) {
+            e = h2f_bits(table[f2h_bits(m[k] - mx)]);
+            s += (double)e;
+        }
+        m[k] = e;
+    }
+    s = wave_sum_d(s);
+    const float inv = (float)(1.0 / s);
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+        const int64_t i = lane + 64 * k;
+        if (i < ncols) d[o + i] = m[k] * inv;
+    }
+}
+
 // Decode attention's second half: scale -> diag_mask_inf -> soft_max of each head's KQ row (one
 // query row per head) and KQV = V.fp16(softmax) with its merged copy.  SM_SPLIT workgroups per head
 // each recompute the row's softmax (max, the exp table, the double sum of exactly representable
@@ -843,8 +890,17 @@ hipError_t op_scale_mask_soft_max_f32(const float *x, float *scaled, float *mask
                                       int64_t nrows, int64_t rows_per_channel, int n_past, const uint16_t *table,
                                       hipStream_t s) {
     if (nrows <= 0) return hipSuccess;
-    launch_k(k_scale_mask_soft_max, dim3(blocks(nrows, TPB / 64)), dim3(TPB), 0, s, x, scaled, masked, d, v,
-                       ncols, nrows, rows_per_channel, n_past, table);
+    const dim3 g(blocks(nrows, TPB / 64));
+    // the row in registers where it fits (prefill KQ rows up to 2048 keys), else two passes over memory
+    if (ncols <= 64 * 8)
+        launch_k(k_scale_mask_soft_max_reg<8>, g, dim3(TPB), 0, s, x, scaled, masked, d, v, ncols, nrows, rows_per_channel,
+                 n_past, table);
+    else if (ncols <= 64 * 32)
+        launch_k(k_scale_mask_soft_max_reg<32>, g, dim3(TPB), 0, s, x, scaled, masked, d, v, ncols, nrows,
+                 rows_per_channel, n_past, table);
+    else
+        launch_k(k_scale_mask_soft_max, g, dim3(TPB), 0, s, x, scaled, masked, d, v, ncols, nrows, rows_per_channel,
+                 n_past, table);
     return hipGetLastError();
 }
 

@@ -1107,15 +1107,20 @@ void run_device_op(tensor *t, const tensor *fused_cpy = nullptr) {
 // fused kernels store every intermediate tensor as its own node would, bit for bit.
 // GGML_HIP_FUSE=0 runs every node as its own launch.
 
-std::atomic<int> g_norm_fold{-1};   // GGML_HIP_NORM_FOLD=0: held norm chains run as their own launch
-bool norm_fold_enabled() {
+// GGML_HIP_NORM_FOLD: 1 (default) the decode norm chains and silu -> mul run in the consuming GEMVs' x
+// prologue, 2 the norm chains only, 0 neither (each chain its own launch)
+std::atomic<int> g_norm_fold{-1};
+int norm_fold_mode() {
     int v = g_norm_fold.load(std::memory_order_relaxed);
     if (v < 0) {
-        v = (!getenv("GGML_HIP_NORM_FOLD") || atoi(getenv("GGML_HIP_NORM_FOLD")) != 0) ? 1 : 0;
+        v = getenv("GGML_HIP_NORM_FOLD") ? atoi(getenv("GGML_HIP_NORM_FOLD")) : 1;
+        v = v < 0 || v > 2 ? 1 : v;
         g_norm_fold.store(v, std::memory_order_relaxed);
     }
-    return v == 1;
+    return v;
 }
+bool norm_fold_enabled() { return norm_fold_mode() != 0; }
+bool silu_fold_enabled() { return norm_fold_mode() == 1; }
 
 // GGML_HIP_X9_FOLD=0: a prefill norm / silu chain whose consumers all take k_gemm9 runs as its own
 // launch and the mul_mats build the x image themselves (k_prep9_x); on (default), the chain's kernel
@@ -1443,7 +1448,7 @@ bool try_fuse(tensor *t) {
         c.table = tb.silu;
         c.ncols = t->ne[0];
         auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
-        bool fold = norm_fold_enabled() && !exact_mode() && gabi::nrows(t) == 1 && c.ncols % 64 == 0 &&
+        bool fold = silu_fold_enabled() && !exact_mode() && gabi::nrows(t) == 1 && c.ncols % 64 == 0 &&
                     c.ncols <= 16384 && al(c.a) && al(c.b) && al(c.norm) && al(c.out);
         for (const tensor *o : {(const tensor *)last, (const tensor *)t})
             for (const tensor *i : {(const tensor *)last->src0, (const tensor *)t->src1})
@@ -3553,7 +3558,7 @@ int ggml_hip_debug_graph_stats(long long *out, int clear) {
 // not in the public header: the decode norm chain folded into the GEMV prologue on (1) / off (0)
 int ggml_hip_debug_set_norm_fold(int on) {
     flush_deferred();
-    g_norm_fold.store(on ? 1 : 0);
+    g_norm_fold.store(on < 0 || on > 2 ? 1 : on);
     return GGML_HIP_OK;
 }
 

@@ -741,57 +741,114 @@ __global__ __launch_bounds__(RN_THREADS) void k_row_norm4(const float *a, const 
 // exact fp16 products, fp32 sums in the instruction's order instead of the AVX chains', so within the
 // fp32-accumulation bound of the reference rather than bitwise).  A = src1 rows rounded to fp16 (the
 // tokens i1: MFMA rows), B = src0 rows as stored (i0: MFMA columns, so a row of 32 outputs is one
-// coalesced store).  Wave = 32 tokens x 64 src0 rows (two MFMAs sharing the A operand), workgroup = 2 x 2
-// waves = 64 x 128 outputs of one channel; operands straight from global memory (one head's K/V slice
-// and Q / soft_max rows stay in L2), 8 K elements per lane and step, zero past K.  vec: every row start
-// 16-byte aligned (one dwordx4 per operand piece), else element loads.
+// coalesced store).  Workgroup = 64 tokens x 128 src0 rows of one channel, 4 waves of 32 x 64 (two MFMAs
+// sharing A).  K runs in chunks of 32 staged through LDS (src1 converted to fp16 on the way in), the next
+// chunk's global loads in flight while this chunk's MFMAs run (double-buffered LDS, one barrier per
+// chunk): every global load is a 16/32-byte piece of a row, several lanes per row — the direct-load form
+// (each lane 16-32 B of a different row per instruction, 32 rows per load instruction) ran 22-25 us per
+// 500-token call, this one 15-16 (KQ) / 15 (KQV, 32-token tiles), tools/r4_ab_f16.sh.  vec: row starts 16-byte aligned (vector loads), else element loads;
+// zero past K.
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16v __attribute__((ext_vector_type(16)));
-constexpr int FM_TI = 64, FM_TO = 128;     // workgroup tile: tokens (i1) x src0 rows (i0)
+// K chunk 32 (30 / 46 KB of LDS: 5 / 3 workgroups per CU); chunks of 64 measured slower (KQ 19.7 vs 15-16 us:
+// 2 workgroups per CU), tools/r4_ab_f16.sh
+constexpr int FM_TO = 128, FM_KC = 32;               // workgroup tile: TI tokens (i1) x 128 src0 rows (i0); K chunk
+constexpr int FM_P = FM_KC + 8;                       // LDS row pitch in halves (80 B: ds_read_b128 rows staggered)
 
+// TI = 64: 4 waves of 32 tokens x 64 rows (two MFMAs sharing A); TI = 32 (few src0 rows, e.g. KQV's 128:
+// twice the workgroups): 4 waves of 32 tokens x 32 rows
+template <int TI>
 __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32_mfma(const char *s0, const char *s1, float *d, int K,
                                                               int64_t ne01, int64_t ne11, int64_t ne02, int64_t nb01,
                                                               int64_t nb02, int64_t nb11, int64_t nb12, float *merged,
                                                               int vec) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int AV = TI * FM_KC / TPB;              // src1 floats staged per thread (16 or 8)
+    constexpr int BV = FM_TO * FM_KC / TPB;           // src0 halves staged per thread (32)
+    __shared__ __attribute__((aligned(16))) _Float16 as[2][TI * FM_P];
+    __shared__ __attribute__((aligned(16))) _Float16 bs[2][FM_TO * FM_P];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int rl = lane & 31, kh = lane >> 5;
     const int64_t i2 = blockIdx.z;
-    const int64_t t0 = (int64_t)blockIdx.y * FM_TI + (wave & 1) * 32;          // tokens of this wave
-    const int64_t o0 = (int64_t)blockIdx.x * FM_TO + (wave >> 1) * 64;         // src0 rows of this wave
-    const int64_t ta = t0 + rl < ne11 ? t0 + rl : ne11 - 1;                    // clamped: loaded, not stored
-    const int64_t ob0 = o0 + rl < ne01 ? o0 + rl : ne01 - 1, ob1 = o0 + 32 + rl < ne01 ? o0 + 32 + rl : ne01 - 1;
-    const float *ya = (const float *)(s1 + i2 * nb12 + ta * nb11);
-    const _Float16 *xb0 = (const _Float16 *)(s0 + i2 * nb02 + ob0 * nb01);
-    const _Float16 *xb1 = (const _Float16 *)(s0 + i2 * nb02 + ob1 * nb01);
-    f32x16v acc0 = {}, acc1 = {};
-    for (int k0 = 0; k0 < K; k0 += 16) {
-        const int k = k0 + 8 * kh;
-        h16x8 a, b0, b1;
-        if (vec && k + 8 <= K) {
-            const float4 y0 = *reinterpret_cast<const float4 *>(ya + k), y1 = *reinterpret_cast<const float4 *>(ya + k + 4);
-            a = h16x8{(_Float16)y0.x, (_Float16)y0.y, (_Float16)y0.z, (_Float16)y0.w,
-                      (_Float16)y1.x, (_Float16)y1.y, (_Float16)y1.z, (_Float16)y1.w};
-            b0 = *reinterpret_cast<const h16x8 *>(xb0 + k);
-            b1 = *reinterpret_cast<const h16x8 *>(xb1 + k);
-        } else {
+    const int64_t T0 = (int64_t)blockIdx.y * TI, O0 = (int64_t)blockIdx.x * FM_TO;
+    // staging roles: src1 row ra (AV values from ka), src0 row rb (BV halves from kb); rows past the matrix
+    // are clamped (loaded, never stored)
+    const int ra = t / (FM_KC / AV), ka = (t % (FM_KC / AV)) * AV, rb = t / (FM_KC / BV), kb = (t % (FM_KC / BV)) * BV;
+    const int64_t ga = T0 + ra < ne11 ? T0 + ra : ne11 - 1, gb = O0 + rb < ne01 ? O0 + rb : ne01 - 1;
+    const float *ya = (const float *)(s1 + i2 * nb12 + ga * nb11);
+    const _Float16 *xb = (const _Float16 *)(s0 + i2 * nb02 + gb * nb01);
+    struct Stage {
+        float4 y[AV / 4];
+        h16x8 x[BV / 8];
+    };
+    auto gload = [&](int k0, Stage &g) __attribute__((always_inline)) {
+        const int k = k0 + ka, kx = k0 + kb;
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const bool in = k + e < K;
-                a[e] = in ? (_Float16)ya[k + e] : (_Float16)0.0f;
-                b0[e] = in ? xb0[k + e] : (_Float16)0.0f;
-                b1[e] = in ? xb1[k + e] : (_Float16)0.0f;
+        for (int q = 0; q < AV / 4; q++) {
+            const int kq = k + 4 * q;
+            if (vec && kq + 4 <= K) {
+                g.y[q] = *reinterpret_cast<const float4 *>(ya + kq);
+            } else {
+                g.y[q] = make_float4(kq < K ? ya[kq] : 0.0f, kq + 1 < K ? ya[kq + 1] : 0.0f, kq + 2 < K ? ya[kq + 2] : 0.0f,
+                                     kq + 3 < K ? ya[kq + 3] : 0.0f);
             }
         }
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b1, acc1, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < BV / 8; q++) {
+            const int kq = kx + 8 * q;
+            if (vec && kq + 8 <= K) {
+                g.x[q] = *reinterpret_cast<const h16x8 *>(xb + kq);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) g.x[q][e] = kq + e < K ? xb[kq + e] : (_Float16)0.0f;
+            }
+        }
+    };
+    auto lstore = [&](int buf, const Stage &g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < AV / 8; q++) {
+            const float4 u = g.y[2 * q], v = g.y[2 * q + 1];
+            const h16x8 a = {(_Float16)u.x, (_Float16)u.y, (_Float16)u.z, (_Float16)u.w,
+                             (_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+            *reinterpret_cast<h16x8 *>(&as[buf][ra * FM_P + ka + 8 * q]) = a;
+        }
+#pragma unroll
+        for (int q = 0; q < BV / 8; q++) *reinterpret_cast<h16x8 *>(&bs[buf][rb * FM_P + kb + 8 * q]) = g.x[q];
+    };
+    // this lane's A row and B rows (TI = 64: wave = token half x row half, B rows bt and bt + 32; TI = 32:
+    // wave = row quarter, B row bt)
+    const int at = TI == 64 ? 32 * (wave & 1) + rl : rl;
+    const int bt = TI == 64 ? 64 * (wave >> 1) + rl : 32 * wave + rl;
+    f32x16v acc0 = {}, acc1 = {};
+    Stage g;
+    gload(0, g);
+    lstore(0, g);
+    __syncthreads();
+    const int nc = (K + FM_KC - 1) / FM_KC;
+    for (int c = 0; c < nc; c++) {
+        const int buf = c & 1;
+        if (c + 1 < nc) gload((c + 1) * FM_KC, g);
+#pragma unroll
+        for (int st = 0; st < FM_KC / 16; st++) {
+            const int ko = 16 * st + 8 * kh;
+            const h16x8 a = *reinterpret_cast<const h16x8 *>(&as[buf][at * FM_P + ko]);
+            const h16x8 b0 = *reinterpret_cast<const h16x8 *>(&bs[buf][bt * FM_P + ko]);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b0, acc0, 0, 0, 0);
+            if constexpr (TI == 64) {
+                const h16x8 b1 = *reinterpret_cast<const h16x8 *>(&bs[buf][(bt + 32) * FM_P + ko]);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b1, acc1, 0, 0, 0);
+            }
+        }
+        if (c + 1 < nc) lstore(buf ^ 1, g);
+        __syncthreads();
     }
     // acc[r] = D[token t0 + (r & 3) + 8 (r >> 2) + 4 kh][src0 row o0 (+ 32) + rl]
+    const int64_t t0 = T0 + (TI == 64 ? 32 * (wave & 1) : 0), o0 = O0 + (TI == 64 ? 64 * (wave >> 1) : 32 * wave);
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         const int64_t i1 = t0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
         if (i1 >= ne11) continue;
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < (TI == 64 ? 2 : 1); h++) {
             const int64_t i0 = o0 + 32 * h + rl;
             if (i0 >= ne01) continue;
             const float v = h ? acc1[r] : acc0[r];
@@ -1038,10 +1095,17 @@ hipError_t op_mul_mat_f16_f32(const void *s0, const void *s1, float *d, int K, i
         auto a16 = [](int64_t v) { return (v & 15) == 0; };
         const int vec = a16((int64_t)(uintptr_t)s0) && a16(nb01) && a16(nb02) && a16((int64_t)(uintptr_t)s1) && a16(nb11) &&
                         a16(nb12);
-        launch_k(k_mul_mat_f16_f32_mfma, dim3((unsigned)((ne01 + FM_TO - 1) / FM_TO), (unsigned)((ne11 + FM_TI - 1) / FM_TI),
-                                              (unsigned)ne02),
-                 dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d, K, ne01, ne11, ne02, nb01, nb02, nb11, nb12, merged,
-                 vec);
+        // few src0 rows (KQV: 128 per head): 32-token tiles, twice the workgroups
+        if (ne01 <= FM_TO)
+            launch_k(k_mul_mat_f16_f32_mfma<32>, dim3((unsigned)((ne01 + FM_TO - 1) / FM_TO), (unsigned)((ne11 + 31) / 32),
+                                                     (unsigned)ne02),
+                     dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d, K, ne01, ne11, ne02, nb01, nb02, nb11, nb12,
+                     merged, vec);
+        else
+            launch_k(k_mul_mat_f16_f32_mfma<64>, dim3((unsigned)((ne01 + FM_TO - 1) / FM_TO), (unsigned)((ne11 + 63) / 64),
+                                                     (unsigned)ne02),
+                     dim3(TPB), 0, s, (const char *)s0, (const char *)s1, d, K, ne01, ne11, ne02, nb01, nb02, nb11, nb12,
+                     merged, vec);
         return hipGetLastError();
     }
     if (tiled == -2) tiled = -1;

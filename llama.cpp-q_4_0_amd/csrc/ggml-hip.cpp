@@ -1761,7 +1761,7 @@ bool flush_group_x9(const Group &g) {
     const NormChain &c = g.norm;
     const int id = g_main_device;
     const int64_t K = c.ncols, N = c.nrows;
-    if (gemm_version() != 10 || N * K >= ((int64_t)1 << 31)) return false;
+    if (exact_mode() || gemm_version() != 10 || N * K >= ((int64_t)1 << 31)) return false;
     const void *img[4];
     int64_t M[4], ldy[4];
     float *y[4];
@@ -3574,6 +3574,33 @@ int ggml_hip_debug_set_x9_fold(int on) {
 int ggml_hip_debug_set_graph(int on) {
     flush_deferred();
     graph_flag().store(on);
+    return GGML_HIP_OK;
+}
+
+// debug (tests/test_gpu_parity.py::test_x9_producers_bitwise): the prefill chains that write the k_gemm9 x
+// image of their output (kind 1: [a + b ->] rms_norm -> * w, a may be null; kind 2: u = silu(a) -> u * b)
+// into img, the same chain without the image into out_ref, and gemm9_prep_x of out into img_ref
+// (synchronous; images of gemm9 x-image size for ncols x nrows, zeroed by the caller)
+int ggml_hip_debug_x9_producer(int kind, const float *a, const float *b, const float *w, float *sum, float *norm,
+                               float *out, float *out_ref, int64_t ncols, int64_t nrows, void *img, void *img_ref) {
+    ensure_init();
+    if (g_device_count == 0) return GGML_HIP_ERR_UNSUPPORTED;
+    if ((kind != 1 && kind != 2) || !ghip::op_x9_ok(ncols, nrows)) return fail(GGML_HIP_ERR_INVALID, "bad x9 producer");
+    flush_deferred();
+    const int id = g_main_device;
+    HIP_FATAL(hipSetDevice(id));
+    hipStream_t s = g_dev[id].stream;
+    const int64_t Np = ghip::gemm9_np(nrows);
+    if (kind == 1) {
+        HIP_RET(ghip::op_add_rms_norm_mul_f32_x9(a, b, sum, norm, w, out, ncols, nrows, img, Np, s));
+        HIP_RET(ghip::op_add_rms_norm_mul_f32(a, b, nullptr, nullptr, w, out_ref, ncols, nrows, s));
+    } else {
+        const OpTables &tb = op_tables(id, s);
+        HIP_RET(ghip::op_silu_mul_f32_x9(a, b, norm, out, ncols, nrows, tb.silu, img, Np, s));
+        HIP_RET(ghip::op_silu_mul_f32(a, b, nullptr, out_ref, ncols * nrows, tb.silu, s));
+    }
+    HIP_RET(ghip::gemm9_prep_x(out, ncols, nrows, img_ref, s));
+    HIP_FATAL(GHIP_SYNC(hipStreamSynchronize)(s));
     return GGML_HIP_OK;
 }
 

@@ -88,6 +88,14 @@ extern "C" int refllama_logits(const char *path, const int *tokens, int n_tokens
 // n_past = 0), then n_decode single-token evals; wall times via steady_clock around llama_eval.
 // out[0] = load s, out[1] = prompt ms (mean over reps), out[2] = decode ms per token; the logits of
 // the last decode step go to last_logits[0..n_vocab).  Returns n_vocab or < 0.
+// min / max over the reps of the last refllama_bench call's prompt evals (the first rep also builds the
+// backend's weight images; the min is the steady state)
+static double g_prompt_min_ms = 0.0, g_prompt_max_ms = 0.0;
+extern "C" void refllama_last_prompt_range(double *min_ms, double *max_ms) {
+    *min_ms = g_prompt_min_ms;
+    *max_ms = g_prompt_max_ms;
+}
+
 extern "C" int refllama_bench(const char *path, int n_prompt, int n_decode, int n_threads, int n_gpu_layers, int n_ctx,
                               int reps, double *out, float *last_logits) {
     using clk = std::chrono::steady_clock;
@@ -113,10 +121,15 @@ extern "C" int refllama_bench(const char *path, int n_prompt, int n_decode, int 
     for (int i = 0; i < n_prompt; i++) toks[i] = i == 0 ? 1 : (llama_token)((i * 7919 + 13) % nv);
     int rc = 0;
     double prompt_ms = 0;
+    g_prompt_min_ms = 1e300;
+    g_prompt_max_ms = 0.0;
     for (int r = 0; r < reps && rc == 0; r++) {
         const auto a = clk::now();
         rc = llama_eval(c, toks.data(), n_prompt, 0, n_threads) ? -3 : 0;
-        prompt_ms += std::chrono::duration<double, std::milli>(clk::now() - a).count();
+        const double ms = std::chrono::duration<double, std::milli>(clk::now() - a).count();
+        prompt_ms += ms;
+        g_prompt_min_ms = ms < g_prompt_min_ms ? ms : g_prompt_min_ms;
+        g_prompt_max_ms = ms > g_prompt_max_ms ? ms : g_prompt_max_ms;
     }
     out[1] = prompt_ms / (reps > 0 ? reps : 1);
     const auto a = clk::now();

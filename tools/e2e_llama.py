@@ -89,7 +89,10 @@ def bench(lib_path, model, n_prompt, n_decode, threads, ngl, reps, nv):
                             logits.ctypes.data)
     if rc != nv:
         raise RuntimeError(f"refllama_bench({lib_path}) failed: {rc}")
+    lo, hi = ctypes.c_double(), ctypes.c_double()
+    lib.refllama_last_prompt_range(ctypes.byref(lo), ctypes.byref(hi))
     return {"load_s": round(out[0], 2), "prompt_tokens": n_prompt, "prompt_ms": round(out[1], 2),
+            "prompt_ms_min": round(lo.value, 2), "prompt_ms_max": round(hi.value, 2),
             "decode_tokens": n_decode, "decode_ms_per_token": round(out[2], 3),
             "decode_tok_s": round(1e3 / out[2], 2) if out[2] > 0 else None, "threads": threads,
             "n_gpu_layers": ngl}, logits

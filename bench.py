@@ -379,10 +379,19 @@ def p2p_decode(gh, L, comm, decode_step, stack, ysplit, yb, rank, allreduce, bar
         L.ggml_hip_comm_set_transport(comm, 0)
         return {"error": f"enable_p2p rc={rc}: {L.ggml_hip_last_error().decode(errors='replace')}"}
     try:
-        decode_step()
+        # a peer wait that times out fails the comm for good and the next split call returns
+        # GGML_HIP_ERR_COMM (raised by gh.check): every rank still reaches the allreduce below, so the ranks
+        # agree on the failure instead of leaving the others in a collective (the waits are time-bounded)
+        try:
+            decode_step()
+            local_ok = True
+        except gh.GgmlHipError as e:
+            log(f"[rank {rank}] P2P step failed: {e}")
+            local_ok = False
+        gh.check(L.ggml_hip_device_synchronize(), "device synchronize")
         st = L.ggml_hip_comm_p2p_status(comm)
-        if allreduce([float(st)], 1)[0] != 0.0:
-            return {"error": f"peer waits timed out (status {st})"}
+        if allreduce([float(st) if local_ok else 1.0], 1)[0] != 0.0:
+            return {"error": f"peer waits timed out (status {st}, this rank's step {'ok' if local_ok else 'failed'})"}
         g = gh.Graph(stream)
         with g:
             decode_step()

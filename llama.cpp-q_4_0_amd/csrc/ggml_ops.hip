@@ -762,7 +762,8 @@ __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32_mfma(const char *s0, co
                                                               int64_t ne01, int64_t ne11, int64_t ne02, int64_t nb01,
                                                               int64_t nb02, int64_t nb11, int64_t nb12, float *merged,
                                                               int vec) {
-    constexpr int AV = TI * FM_KC / TPB;              // src1 floats staged per thread (16 or 8)
+    constexpr int AV = TI * FM_KC / TPB;              // src1 floats staged per thread (8 or 4)
+    static_assert(AV % 4 == 0 && FM_KC % AV == 0, "src1 staging in float4 pieces");
     constexpr int BV = FM_TO * FM_KC / TPB;           // src0 halves staged per thread (32)
     __shared__ __attribute__((aligned(16))) _Float16 as[2][TI * FM_P];
     __shared__ __attribute__((aligned(16))) _Float16 bs[2][FM_TO * FM_P];
@@ -803,13 +804,13 @@ __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32_mfma(const char *s0, co
             }
         }
     };
+    typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
     auto lstore = [&](int buf, const Stage &g) __attribute__((always_inline)) {
 #pragma unroll
-        for (int q = 0; q < AV / 8; q++) {
-            const float4 u = g.y[2 * q], v = g.y[2 * q + 1];
-            const h16x8 a = {(_Float16)u.x, (_Float16)u.y, (_Float16)u.z, (_Float16)u.w,
-                             (_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-            *reinterpret_cast<h16x8 *>(&as[buf][ra * FM_P + ka + 8 * q]) = a;
+        for (int q = 0; q < AV / 4; q++) {            // 4 values (8 bytes) per float4 piece
+            const float4 u = g.y[q];
+            const h16x4 a = {(_Float16)u.x, (_Float16)u.y, (_Float16)u.z, (_Float16)u.w};
+            *reinterpret_cast<h16x4 *>(&as[buf][ra * FM_P + ka + 4 * q]) = a;
         }
 #pragma unroll
         for (int q = 0; q < BV / 8; q++) *reinterpret_cast<h16x8 *>(&bs[buf][rb * FM_P + kb + 8 * q]) = g.x[q];

@@ -114,12 +114,21 @@ __device__ __forceinline__ double wave_sum_d64(double v) {   // every lane gets 
     return v;
 }
 
+#ifdef GEMV_STAMPS
+// diagnostic builds only (tools/build_variant.sh ... -DGEMV_STAMPS): per-wave s_memrealtime stamps of the
+// launches whose M equals g_gemv_stamp_m: [wave][4] = start, x in LDS, end, HW_ID | XCC_ID << 32
+__device__ uint64_t *g_gemv_stamps = nullptr;
+__device__ int g_gemv_stamp_m = -1;
+#endif
 template <int NT, int WAVES, int DEPTH, int VAR, int PPL = 0, int PRO = 0, int BAL = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restrict__ x_, const uint8_t *W0,
                                                           const uint8_t *W1, const uint8_t *W2, int rb1_, int rb2_,
                                                           int rb3_, int rowbytes_, int geom, int M_,
                                                           const GemvTail tail) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+#ifdef GEMV_STAMPS
+    const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int nb = geom & 0xFFFF;
     const int map = (geom >> 16) & 3;
     const int grid = (int)((uint32_t)geom >> 18);
@@ -417,6 +426,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
         }
     }
     __syncthreads();
+#ifdef GEMV_STAMPS
+    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // ---- COMPUTE: stream the wave's items with DEPTH items in flight in a ring of named register
     // sets (no register copies: a copy would force a wait on the in-flight loads).
@@ -496,8 +508,28 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             *yo = out;
         }
     }
+#ifdef GEMV_STAMPS
+    if (M == g_gemv_stamp_m && g_gemv_stamps && lane == 0) {      // vector stores (lane-divergent)
+        const uint64_t ts2 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);          // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);        // HW_REG_XCC_ID
+        volatile uint64_t *st = g_gemv_stamps + ((int64_t)blockIdx.x * WAVES + wave) * 4;
+        st[0] = ts0;
+        st[1] = ts1;
+        st[2] = ts2;
+        st[3] = (uint64_t)hw | ((uint64_t)xcc << 32);
+    }
+#endif
 }
 
+
+#ifdef GEMV_STAMPS
+extern "C" int ggml_hip_debug_gemv_stamps(void *buf, int m) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_gemv_stamps), &buf, sizeof(buf)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_gemv_stamp_m), &m, sizeof(m)) != hipSuccess) return -1;
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+#endif
 
 // GEMV launch policy overrides: -1 / 0 = automatic.  Initialised from the environment
 // (GGML_HIP_GEMV_MAP / _DEPTH / _ROWITEMS / _WG_PER_CU) and settable at run time by the

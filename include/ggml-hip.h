@@ -326,6 +326,12 @@ int    ggml_hip_debug_op_stats(int64_t *counts, int n, int reset);
 int    ggml_hip_debug_f16_mul_mat(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11,
                                   int64_t ne02, int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12,
                                   float *merged, int tiled);
+/* debug: ggml_cpy F32 -> F32 / F16 (to_f16) on device pointers (synchronous): source shape ne00 x ne01 x
+   n / (ne00 ne01) with byte strides nb00..nb02, target ne10 x ne11 x .. with nb10..nb12; batched = 1
+   through the batched elementwise launch (as the hook runs it behind a q4_0 group), 0 as its own node */
+int    ggml_hip_debug_cpy_f32(const void *x, void *d, int to_f16, int64_t n, int64_t ne00, int64_t ne01,
+                              int64_t nb00, int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11, int64_t nb10,
+                              int64_t nb11, int64_t nb12, int batched);
 /* debug: 1/0 = launch fusion of adjacent full-offload nodes on/off (default: env GGML_HIP_FUSE, on) */
 int    ggml_hip_debug_set_fuse(int on);
 

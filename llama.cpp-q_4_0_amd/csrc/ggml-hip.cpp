@@ -3620,6 +3620,30 @@ int ggml_hip_debug_f16_mul_mat(const void *s0, const void *s1, float *d, int K, 
     return GGML_HIP_OK;
 }
 
+int ggml_hip_debug_cpy_f32(const void *x, void *d, int to_f16, int64_t n, int64_t ne00, int64_t ne01, int64_t nb00,
+                           int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11, int64_t nb10, int64_t nb11,
+                           int64_t nb12, int batched) {
+    ensure_init();
+    if (g_device_count == 0) return GGML_HIP_ERR_UNSUPPORTED;
+    if (n < 0 || ne00 < 1 || ne01 < 1 || ne10 < 1 || ne11 < 1) return GGML_HIP_ERR_INVALID;
+    flush_deferred();
+    HIP_FATAL(hipSetDevice(g_main_device));
+    hipStream_t s = g_dev[g_main_device].stream;
+    if (batched) {
+        ghip::ElemBatch b{};
+        ghip::ElemOp &op = b.op[0];
+        op.kind = 1, op.f16 = to_f16 != 0, op.x = (const char *)x, op.c = (char *)d, op.n = n;
+        op.ne0 = ne00, op.ne1 = ne01, op.nbx1 = nb00, op.nbx2 = nb01, op.nbx3 = nb02;
+        op.ne10 = ne10, op.ne11 = ne11, op.nb10 = nb10, op.nb11 = nb11, op.nb12 = nb12;
+        b.nops = 1;
+        HIP_FATAL(ghip::op_elem_batch(b, s));
+    } else {
+        HIP_FATAL(ghip::op_cpy_f32(x, d, to_f16 != 0, n, ne00, ne01, nb00, nb01, nb02, ne10, ne11, nb10, nb11, nb12, s));
+    }
+    HIP_FATAL(GHIP_SYNC(hipStreamSynchronize)(s));
+    return GGML_HIP_OK;
+}
+
 // not in the public header: launch fusion of full-offload chains on (1) / off (0) (tests run both)
 int ggml_hip_debug_set_fuse(int on) {
     flush_deferred();

@@ -40,6 +40,7 @@ hipError_t op_rope_cpy_f32(const void *x, void *d, const int64_t ne[4], const in
 constexpr int ELEM_MAX = 4;
 struct ElemOp {
     int kind;              // 0 rope (mode 0; then the copy into c when c != nullptr), 1 cpy x -> c
+                           // (2: set by op_elem_batch for the transposed 2-d cpy, 64 x 64 LDS tiles)
     int f16;               // the copy's target is F16 (else F32)
     const char *x;         // source
     char *d;               // rope output

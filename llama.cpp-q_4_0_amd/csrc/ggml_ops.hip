@@ -221,6 +221,9 @@ __global__ __launch_bounds__(TPB) void k_cpy_f32(const char *x, char *d, int64_t
 // runs between its q4_0 sibling group and the attention: rope K -> K cache, V -> V cache, rope Q).
 // Each block belongs to one op (block_begin prefix sums); every element is computed by the same
 // expression as the op's own kernel above.
+// I: the index type of the per-element divisions (uint32_t when every op's extents fit: the 64-bit
+// divisions would bound the prefill launch on the VALU; addresses stay 64-bit either way)
+template <typename I>
 __global__ __launch_bounds__(TPB) void k_elem_batch(const ElemBatch b) {
     int o = 0;
 #pragma unroll
@@ -230,12 +233,38 @@ __global__ __launch_bounds__(TPB) void k_elem_batch(const ElemBatch b) {
 #pragma unroll
     for (int q = 1; q < ELEM_MAX; q++)
         if (o == q) op = b.op[q];
+    if (op.kind == 2) {
+        // the 2-d cpy whose source runs along dim 1 and target along dim 0 (Vcur -> the transposed V
+        // cache at prefill): one 64 x 64 tile per workgroup through LDS, read along the source's rows
+        // and written along the target's, each value converted as kind 1 converts it
+        __shared__ float tile[64][65];
+        const int64_t t = blockIdx.x - b.block_begin[o];
+        const int64_t nt0 = (op.ne0 + 63) / 64;
+        const int64_t t0 = (t % nt0) * 64, t1 = (t / nt0) * 64;
+        const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
+        for (int r = ly; r < 64; r += TPB / 64) {
+            const int64_t i00 = t0 + r, i01 = t1 + lx;
+            if (i00 < op.ne0 && i01 < op.ne1) tile[r][lx] = *(const float *)(op.x + i00 * op.nbx1 + i01 * 4);
+        }
+        __syncthreads();
+        for (int r = ly; r < 64; r += TPB / 64) {
+            const int64_t i00 = t0 + lx, i01 = t1 + r;
+            if (i00 < op.ne0 && i01 < op.ne1) {
+                char *dst = op.c + i00 * op.nb10 + i01 * op.nb11;
+                if (op.f16)
+                    *(uint16_t *)dst = f2h_bits(tile[lx][r]);
+                else
+                    *(float *)dst = tile[lx][r];
+            }
+        }
+        return;
+    }
     const int64_t k = (int64_t)(blockIdx.x - b.block_begin[o]) * TPB + threadIdx.x;
     if (k >= op.n) return;
     if (op.kind == 1) {                                   // cpy, as k_cpy_f32
-        const int64_t i = k;
-        const int64_t i02 = i / (op.ne0 * op.ne1), i01 = (i / op.ne0) % op.ne1, i00 = i % op.ne0;
-        const int64_t i12 = i / (op.ne10 * op.ne11), i11 = (i / op.ne10) % op.ne11, i10 = i % op.ne10;
+        const I i = (I)k, ne0 = (I)op.ne0, ne1 = (I)op.ne1, ne10 = (I)op.ne10, ne11 = (I)op.ne11;
+        const int64_t i02 = i / (ne0 * ne1), i01 = (i / ne0) % ne1, i00 = i % ne0;
+        const int64_t i12 = i / (ne10 * ne11), i11 = (i / ne10) % ne11, i10 = i % ne10;
         const float v = *(const float *)(op.x + i00 * op.nbx1 + i01 * op.nbx2 + i02 * op.nbx3);
         char *dst = op.c + i10 * op.nb10 + i11 * op.nb11 + i12 * op.nb12;
         if (op.f16)
@@ -245,10 +274,10 @@ __global__ __launch_bounds__(TPB) void k_elem_batch(const ElemBatch b) {
         return;
     }
     // rope (mode 0), as k_rope_f32; then (c != nullptr) the copy of k_rope_cpy
-    const int64_t np = op.ne0 / 2;
-    const int64_t j = k % np;
-    const int64_t r = k / np;
-    const int64_t i1 = r % op.ne1, i2 = (r / op.ne1) % op.ne2, i3 = r / (op.ne1 * op.ne2);
+    const I np = (I)(op.ne0 / 2), ne1 = (I)op.ne1, ne2 = (I)op.ne2;
+    const I j = (I)k % np;
+    const I r = (I)k / np;
+    const int64_t i1 = r % ne1, i2 = (r / ne1) % ne2, i3 = r / (ne1 * ne2);
     const float2 t = op.cs[i2 * op.npairs + j];
     const float *src = (const float *)(op.x + i3 * op.nbx3 + i2 * op.nbx2 + i1 * op.nbx1) + 2 * j;
     float *out = (float *)(op.d + i3 * op.nbd3 + i2 * op.nbd2 + i1 * op.nbd1) + 2 * j;
@@ -260,8 +289,9 @@ __global__ __launch_bounds__(TPB) void k_elem_batch(const ElemBatch b) {
     if (op.c) {
 #pragma unroll
         for (int e = 0; e < 2; e++) {
-            const int64_t i = 2 * j + e + op.ne0 * (i1 + op.ne1 * i2);
-            const int64_t i12 = i / (op.ne10 * op.ne11), i11 = (i / op.ne10) % op.ne11, i10 = i % op.ne10;
+            const I ne10 = (I)op.ne10, ne11 = (I)op.ne11;
+            const I i = 2 * j + e + (I)op.ne0 * ((I)i1 + ne1 * (I)i2);
+            const int64_t i12 = i / (ne10 * ne11), i11 = (i / ne10) % ne11, i10 = i % ne10;
             char *dst = op.c + i10 * op.nb10 + i11 * op.nb11 + i12 * op.nb12;
             const float v = e ? y1 : y0;
             if (op.f16)
@@ -1056,10 +1086,27 @@ hipError_t op_rope_cpy_f32(const void *x, void *d, const int64_t ne[4], const in
     return hipGetLastError();
 }
 
+// a kind-1 copy that takes the tiled path: 2-d, the source contiguous along dim 1 and strided along
+// dim 0, the target the same shape and contiguous along dim 0, at least 64 along dim 0 (prefill)
+static bool elem_cpy_transposed(const ElemOp &op) {
+    const int64_t es = op.f16 ? 2 : 4;
+    return op.n == op.ne0 * op.ne1 && op.ne0 >= 64 && op.ne1 >= 1 && op.nbx2 == 4 && op.nbx1 != 4 &&
+           op.ne10 == op.ne0 && op.ne11 == op.ne1 && op.nb10 == es;
+}
+
 hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne00, int64_t ne01, int64_t nb00,
                       int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11, int64_t nb10, int64_t nb11, int64_t nb12,
                       hipStream_t s) {
     if (n <= 0) return hipSuccess;
+    ElemBatch b{};
+    ElemOp &op = b.op[0];
+    op.kind = 1, op.f16 = to_f16, op.x = (const char *)x, op.c = (char *)d, op.n = n;
+    op.ne0 = ne00, op.ne1 = ne01, op.nbx1 = nb00, op.nbx2 = nb01, op.nbx3 = nb02;
+    op.ne10 = ne10, op.ne11 = ne11, op.nb10 = nb10, op.nb11 = nb11, op.nb12 = nb12;
+    if (elem_cpy_transposed(op)) {      // the transposed V-cache store: the tiled path of k_elem_batch
+        b.nops = 1;
+        return op_elem_batch(b, s);
+    }
     if (to_f16)
         launch_k(k_cpy_f32<true>, dim3(blocks(n)), dim3(TPB), 0, s, (const char *)x, (char *)d, n, ne00, ne01,
                            nb00, nb01, nb02, ne10, ne11, nb10, nb11, nb12);
@@ -1074,12 +1121,28 @@ hipError_t op_elem_batch(const ElemBatch &b, hipStream_t s) {
     ElemBatch bb = b;
     unsigned total = 0;
     for (int q = 0; q < bb.nops; q++) {
+        ElemOp &op = bb.op[q];
+        if (op.kind == 1 && elem_cpy_transposed(op)) {
+            op.kind = 2;
+            op.n = ((op.ne0 + 63) / 64) * ((op.ne1 + 63) / 64) * TPB;   // one workgroup per tile
+        }
         bb.block_begin[q] = total;
-        total += blocks(bb.op[q].n);
+        total += blocks(op.n);
     }
     for (int q = bb.nops; q < ELEM_MAX; q++) bb.block_begin[q] = total;
     if (total == 0) return hipSuccess;
-    launch_k(k_elem_batch, dim3(total), dim3(TPB), 0, s, bb);
+    // 32-bit element indices when every index and product of extents the kernel forms fits
+    bool small = (uint64_t)total * TPB < (1ull << 31);
+    for (int q = 0; q < bb.nops; q++) {
+        const ElemOp &op = bb.op[q];
+        const int64_t lim = (int64_t)1 << 31;
+        small = small && op.n < lim && op.ne0 * op.ne1 < lim && op.ne0 * op.ne1 * (op.ne2 > 1 ? op.ne2 : 1) < lim &&
+                op.ne10 * op.ne11 < lim && (op.kind != 0 || op.ne0 / 2 * op.ne1 * op.ne2 < lim);
+    }
+    if (small)
+        launch_k(k_elem_batch<uint32_t>, dim3(total), dim3(TPB), 0, s, bb);
+    else
+        launch_k(k_elem_batch<int64_t>, dim3(total), dim3(TPB), 0, s, bb);
     return hipGetLastError();
 }
 

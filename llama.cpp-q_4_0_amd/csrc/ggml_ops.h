@@ -40,8 +40,10 @@ hipError_t op_rope_cpy_f32(const void *x, void *d, const int64_t ne[4], const in
 constexpr int ELEM_MAX = 4;
 struct ElemOp {
     int kind;              // 0 rope (mode 0; then the copy into c when c != nullptr), 1 cpy x -> c
-                           // (2: set by op_elem_batch for the transposed 2-d cpy, 64 x 64 LDS tiles)
+                           // (set by op_elem_batch: 2 the transposed 2-d cpy in 64 x 64 LDS tiles,
+                           // 3 a rope on two pairs per thread)
     int f16;               // the copy's target is F16 (else F32)
+    int pack;              // set by op_elem_batch (kind 3): a thread's 4 copied values share a target row
     const char *x;         // source
     char *d;               // rope output
     char *c;               // copy target (strided view) or nullptr

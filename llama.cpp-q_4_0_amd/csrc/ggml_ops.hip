@@ -273,6 +273,50 @@ __global__ __launch_bounds__(TPB) void k_elem_batch(const ElemBatch b) {
             *(float *)dst = v;
         return;
     }
+    if (op.kind == 3) {
+        // kind 0 on two pairs per thread (set by op_elem_batch when every row and the (cos, sin) rows
+        // are 16-byte aligned): the same products per pair, 16-byte loads and stores; npairs = 4 x the
+        // four values' target in one 8- (F16) or 16-byte (F32) store when they share a contiguous row
+        const I nq = (I)(op.ne0 / 4), ne1 = (I)op.ne1, ne2 = (I)op.ne2;
+        const I q = (I)k % nq, r = (I)k / nq;
+        const int64_t i1 = r % ne1, i2 = (r / ne1) % ne2, i3 = r / (ne1 * ne2);
+        const float4 t = *(const float4 *)(op.cs + i2 * op.npairs + 2 * q);
+        const float4 x = *(const float4 *)(op.x + i3 * op.nbx3 + i2 * op.nbx2 + i1 * op.nbx1 + 16 * (int64_t)q);
+        float4 y;
+        y.x = x.x * t.x - x.y * t.y;
+        y.y = x.x * t.y + x.y * t.x;
+        y.z = x.z * t.z - x.w * t.w;
+        y.w = x.z * t.w + x.w * t.z;
+        *(float4 *)(op.d + i3 * op.nbd3 + i2 * op.nbd2 + i1 * op.nbd1 + 16 * (int64_t)q) = y;
+        if (op.c) {
+            const I ne10 = (I)op.ne10, ne11 = (I)op.ne11;
+            const I i = 4 * q + (I)op.ne0 * ((I)i1 + ne1 * (I)i2);
+            const float v[4] = {y.x, y.y, y.z, y.w};
+            if (op.pack) {
+                const int64_t i12 = i / (ne10 * ne11), i11 = (i / ne10) % ne11, i10 = i % ne10;
+                char *dst = op.c + i10 * op.nb10 + i11 * op.nb11 + i12 * op.nb12;
+                if (op.f16) {
+                    const uint2 h = make_uint2((uint32_t)f2h_bits(v[0]) | ((uint32_t)f2h_bits(v[1]) << 16),
+                                               (uint32_t)f2h_bits(v[2]) | ((uint32_t)f2h_bits(v[3]) << 16));
+                    *(uint2 *)dst = h;
+                } else {
+                    *(float4 *)dst = y;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const I ie = i + e;
+                    const int64_t i12 = ie / (ne10 * ne11), i11 = (ie / ne10) % ne11, i10 = ie % ne10;
+                    char *dst = op.c + i10 * op.nb10 + i11 * op.nb11 + i12 * op.nb12;
+                    if (op.f16)
+                        *(uint16_t *)dst = f2h_bits(v[e]);
+                    else
+                        *(float *)dst = v[e];
+                }
+            }
+        }
+        return;
+    }
     // rope (mode 0), as k_rope_f32; then (c != nullptr) the copy of k_rope_cpy
     const I np = (I)(op.ne0 / 2), ne1 = (I)op.ne1, ne2 = (I)op.ne2;
     const I j = (I)k % np;
@@ -1094,6 +1138,15 @@ static bool elem_cpy_transposed(const ElemOp &op) {
            op.ne10 == op.ne0 && op.ne11 == op.ne1 && op.nb10 == es;
 }
 
+static bool a_of(const void *p, int64_t a) { return ((uintptr_t)p % (uintptr_t)a) == 0; }
+// a kind-0 rope that takes the two-pairs-per-thread path: every row of x and d and the (cos, sin)
+// rows 16-byte aligned, an even number of pairs per row
+static bool elem_rope_vec(const ElemOp &op) {
+    return op.ne0 % 4 == 0 && op.npairs % 2 == 0 && a_of(op.x, 16) &&
+           a_of(op.d, 16) && a_of(op.cs, 16) && op.nbx1 % 16 == 0 && op.nbx2 % 16 == 0 && op.nbx3 % 16 == 0 &&
+           op.nbd1 % 16 == 0 && op.nbd2 % 16 == 0 && op.nbd3 % 16 == 0;
+}
+
 hipError_t op_cpy_f32(const void *x, void *d, bool to_f16, int64_t n, int64_t ne00, int64_t ne01, int64_t nb00,
                       int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11, int64_t nb10, int64_t nb11, int64_t nb12,
                       hipStream_t s) {
@@ -1125,6 +1178,12 @@ hipError_t op_elem_batch(const ElemBatch &b, hipStream_t s) {
         if (op.kind == 1 && elem_cpy_transposed(op)) {
             op.kind = 2;
             op.n = ((op.ne0 + 63) / 64) * ((op.ne1 + 63) / 64) * TPB;   // one workgroup per tile
+        } else if (op.kind == 0 && elem_rope_vec(op)) {
+            op.kind = 3;
+            op.n /= 2;                                                     // two pairs per item
+            const int64_t es = op.f16 ? 2 : 4;
+            op.pack = op.c && op.ne10 % 4 == 0 && op.nb10 == es && a_of(op.c, 4 * es) && op.nb11 % (4 * es) == 0 &&
+                      op.nb12 % (4 * es) == 0;
         }
         bb.block_begin[q] = total;
         total += blocks(op.n);

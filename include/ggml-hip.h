@@ -326,6 +326,13 @@ int    ggml_hip_debug_op_stats(int64_t *counts, int n, int reset);
 int    ggml_hip_debug_f16_mul_mat(const void *s0, const void *s1, float *d, int K, int64_t ne01, int64_t ne11,
                                   int64_t ne02, int64_t nb01, int64_t nb02, int64_t nb11, int64_t nb12,
                                   float *merged, int tiled);
+/* debug: mode-0 rope (ggml_compute_forward_rope_f32) of x [ne2 tokens][ne1 heads][ne0] (byte strides
+   nbx[1..3]) into d (nbd[1..3]) at positions n_past.., then (c != nullptr) ggml_cpy of d into the view c
+   (F16 when to_f16; shape ne10 x ne11 x .., byte strides nb10..nb12); batched = 1 through the batched
+   elementwise launch (as the hook runs rope K -> K cache behind a q4_0 group), 0 its own kernel */
+int    ggml_hip_debug_rope(const void *x, void *d, void *c, int to_f16, int64_t ne0, int64_t ne1, int64_t ne2,
+                           int n_past, int n_dims, const int64_t *nbx, const int64_t *nbd, int64_t ne10,
+                           int64_t ne11, int64_t nb10, int64_t nb11, int64_t nb12, int batched);
 /* debug: ggml_cpy F32 -> F32 / F16 (to_f16) on device pointers (synchronous): source shape ne00 x ne01 x
    n / (ne00 ne01) with byte strides nb00..nb02, target ne10 x ne11 x .. with nb10..nb12; batched = 1
    through the batched elementwise launch (as the hook runs it behind a q4_0 group), 0 as its own node */

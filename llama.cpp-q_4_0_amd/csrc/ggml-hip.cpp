@@ -3620,6 +3620,48 @@ int ggml_hip_debug_f16_mul_mat(const void *s0, const void *s1, float *d, int K, 
     return GGML_HIP_OK;
 }
 
+int ggml_hip_debug_rope(const void *x, void *d, void *c, int to_f16, int64_t ne0, int64_t ne1, int64_t ne2, int n_past,
+                        int n_dims, const int64_t *nbx, const int64_t *nbd, int64_t ne10, int64_t ne11, int64_t nb10,
+                        int64_t nb11, int64_t nb12, int batched) {
+    ensure_init();
+    if (g_device_count == 0) return GGML_HIP_ERR_UNSUPPORTED;
+    if (ne0 < 2 || ne0 % 2 || ne1 < 1 || ne2 < 1 || n_past < 0 || n_dims < 2 || n_dims % 2 || n_dims > ne0 || !nbx || !nbd)
+        return GGML_HIP_ERR_INVALID;
+    flush_deferred();
+    const int id = g_main_device;
+    HIP_FATAL(hipSetDevice(id));
+    hipStream_t s = g_dev[id].stream;
+    const int64_t np = ne0 / 2;
+    const float *cs = rope_table(id, ne0, n_dims, (int64_t)n_past + ne2, s) + (size_t)n_past * np * 2;
+    const int64_t ne[4] = {ne0, ne1, ne2, 1};
+    if (batched) {
+        ghip::ElemBatch b{};
+        ghip::ElemOp &op = b.op[0];
+        op.kind = 0;
+        op.x = (const char *)x;
+        op.d = (char *)d;
+        op.cs = (const float2 *)cs;
+        op.npairs = (int)np;
+        op.n = np * ne1 * ne2;
+        op.ne0 = ne0, op.ne1 = ne1, op.ne2 = ne2;
+        op.nbx1 = nbx[1], op.nbx2 = nbx[2], op.nbx3 = nbx[3];
+        op.nbd1 = nbd[1], op.nbd2 = nbd[2], op.nbd3 = nbd[3];
+        if (c) {
+            op.c = (char *)c;
+            op.f16 = to_f16 != 0;
+            op.ne10 = ne10, op.ne11 = ne11, op.nb10 = nb10, op.nb11 = nb11, op.nb12 = nb12;
+        }
+        b.nops = 1;
+        HIP_FATAL(ghip::op_elem_batch(b, s));
+    } else if (c) {
+        HIP_FATAL(ghip::op_rope_cpy_f32(x, d, ne, nbx, nbd, cs, (int)np, c, to_f16 != 0, ne10, ne11, nb10, nb11, nb12, s));
+    } else {
+        HIP_FATAL(ghip::op_rope_f32(x, d, ne, nbx, nbd, cs, (int)np, s));
+    }
+    HIP_FATAL(GHIP_SYNC(hipStreamSynchronize)(s));
+    return GGML_HIP_OK;
+}
+
 int ggml_hip_debug_cpy_f32(const void *x, void *d, int to_f16, int64_t n, int64_t ne00, int64_t ne01, int64_t nb00,
                            int64_t nb01, int64_t nb02, int64_t ne10, int64_t ne11, int64_t nb10, int64_t nb11,
                            int64_t nb12, int batched) {

@@ -275,8 +275,8 @@ __global__ __launch_bounds__(TPB) void k_elem_batch(const ElemBatch b) {
     }
     if (op.kind == 3) {
         // kind 0 on two pairs per thread (set by op_elem_batch when every row and the (cos, sin) rows
-        // are 16-byte aligned): the same products per pair, 16-byte loads and stores; npairs = 4 x the
-        // four values' target in one 8- (F16) or 16-byte (F32) store when they share a contiguous row
+        // are 16-byte aligned): the same products per pair, 16-byte loads and stores, and the four
+        // values' copy in one 8- (F16) or 16-byte (F32) store when they share a contiguous row (pack)
         const I nq = (I)(op.ne0 / 4), ne1 = (I)op.ne1, ne2 = (I)op.ne2;
         const I q = (I)k % nq, r = (I)k / nq;
         const int64_t i1 = r % ne1, i2 = (r / ne1) % ne2, i3 = r / (ne1 * ne2);

@@ -661,7 +661,7 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max_reg(const float *x,
 // 32 of the head's KQV outputs, 32 lanes per output as k_mul_mat_f16_f32 does.  Workgroup 0 of a
 // head stores the softmax row (and scaled / masked) unless nullptr: the caller passes nullptr for a
 // buffer that aliases kq (the in-place chain), which the other workgroups are still reading.
-constexpr int SM_THREADS = 1024, SM_OUT = SM_THREADS / 32;
+constexpr int SM_THREADS = 1024, SM_OUT = SM_THREADS / 32, SM_PF = 16;
 __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm,
                                                             float v, int n_past, const uint16_t *table, int64_t nkv,
                                                             const char *vs, int64_t nb01v, int64_t nb02v, int64_t nout,
@@ -674,6 +674,19 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     const int tid = threadIdx.x, g = tid >> 5, l = tid & 31, wave = tid >> 6, lane = tid & 63;
     const int64_t o = i2 * nkv;
     const bool store = part == 0;
+    // this lane's first SM_PF V^T values and the row's tail (K % 32 values, one per lane) are loaded
+    // before the softmax, so their latency runs under it: unconditional loads of clamped (valid)
+    // addresses, so they issue back to back (a load under a branch waits at the join); the products
+    // below use the same values in the same order
+    const int64_t r = (int64_t)part * SM_OUT + g;
+    const bool live = r < nout;
+    const uint16_t *xr = (const uint16_t *)(vs + i2 * nb02v + (live ? r : 0) * nb01v);
+    const int K = (int)nkv;
+    const int np = K & ~31, tl = K - np;
+    uint16_t vpre[SM_PF];
+#pragma unroll
+    for (int j = 0; j < SM_PF; j++) vpre[j] = xr[min(l + 32 * j, K - 1)];
+    const uint16_t vtail = xr[min(np + l, K - 1)];
     float mx = -INFINITY;
     for (int64_t i = tid; i < nkv; i += SM_THREADS) mx = fmaxf(mx, i > n_past ? -INFINITY : kq[o + i] * v);
     mx = wave_max_f(mx);
@@ -709,13 +722,23 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     }
     __syncthreads();
     // KQV output r of this head: V^T row r (nkv f16) . fp16(softmax row)
-    const int64_t r = (int64_t)part * SM_OUT + g;
-    if (r >= nout) return;
-    const uint16_t *xr = (const uint16_t *)(vs + i2 * nb02v + r * nb01v);
-    const int K = (int)nkv;
-    const int np = K & ~31;
+    if (!live) return;
     float acc = 0.0f;
-    for (int e = l; e < np; e += 32) acc = fmaf(h2f_bits(xr[e]), h2f_bits(f2h_bits(row[e])), acc);
+#pragma unroll
+    for (int j = 0; j < SM_PF; j++) {
+        const int e = l + 32 * j;
+        if (e < np) acc = fmaf(h2f_bits(vpre[j]), h2f_bits(f2h_bits(row[e])), acc);
+    }
+    for (int e0 = 32 * SM_PF; e0 < np; e0 += 32 * SM_PF) {   // longer rows: SM_PF loads per batch
+        uint16_t vb[SM_PF];
+#pragma unroll
+        for (int j = 0; j < SM_PF; j++) vb[j] = xr[min(e0 + l + 32 * j, K - 1)];
+#pragma unroll
+        for (int j = 0; j < SM_PF; j++) {
+            const int e = e0 + l + 32 * j;
+            if (e < np) acc = fmaf(h2f_bits(vb[j]), h2f_bits(f2h_bits(row[e])), acc);
+        }
+    }
     const float p16 = __shfl_xor(acc, 16, 32);
     const float a = acc + p16;
     const float p8 = __shfl_xor(a, 8, 32);
@@ -725,9 +748,11 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     const float t01 = t0 + __shfl_xor(t0, 1, 32);
     const float t23 = __shfl(t01, 2, 32);
     const float res = t01 + t23;
+    // the tail e >= np in double, in order of e (each product formed by its lane, gathered in turn)
+    const float pt = l < tl ? h2f_bits(vtail) * h2f_bits(f2h_bits(row[np + l])) : 0.0f;
+    double sum = (double)res;
+    for (int e = 0; e < tl; e++) sum += (double)__shfl(pt, e, 32);
     if (l == 0) {
-        double sum = (double)res;
-        for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(row[e])));
         kqv[i2 * nout + r] = (float)sum;
         if (merged) merged[i2 * nout + r] = (float)sum;
     }

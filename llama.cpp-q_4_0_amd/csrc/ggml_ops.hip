@@ -365,9 +365,27 @@ __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32(const char *s0, const c
     const int64_t i0 = oc % ne01, i1 = (oc / ne01) % ne11, i2 = oc / (ne01 * ne11);
     const uint16_t *xr = (const uint16_t *)(s0 + i2 * nb02 + i0 * nb01);
     const float *yr = (const float *)(s1 + i2 * nb12 + i1 * nb11);
-    const int np = K & ~31;
+    const int np = K & ~31, tl = K - np, kl = K > 0 ? K - 1 : 0;
     float acc = 0.0f;
-    for (int e = l; e < np; e += 32) acc = fmaf(h2f_bits(xr[e]), h2f_bits(f2h_bits(yr[e])), acc);
+    // batches of 4 unconditional loads of clamped addresses (issued back to back; a load under a
+    // branch would wait at the join), used in order of e
+    for (int e0 = 0; e0 < np; e0 += 128) {
+        uint16_t xb[4];
+        float yb[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int e = min(e0 + l + 32 * j, kl);
+            xb[j] = xr[e];
+            yb[j] = yr[e];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (e0 + l + 32 * j < np) acc = fmaf(h2f_bits(xb[j]), h2f_bits(f2h_bits(yb[j])), acc);
+    }
+    // the tail e >= np: each lane's product (loaded with the batches' clamping), summed below in order
+    const uint16_t xt = xr[min(np + l, kl)];
+    const float yt = yr[min(np + l, kl)];
+    const float pt = l < tl ? h2f_bits(xt) * h2f_bits(f2h_bits(yt)) : 0.0f;
     // lane = 8*j + m: a_m = s0 + s2, b_m = s1 + s3, c_m = a_m + b_m
     const float p16 = __shfl_xor(acc, 16, 32);
     const float a = acc + p16;                                        // lanes 0-7: s0+s2, 8-15: s1+s3
@@ -378,9 +396,9 @@ __global__ __launch_bounds__(TPB) void k_mul_mat_f16_f32(const char *s0, const c
     const float t01 = t0 + __shfl_xor(t0, 1, 32);                     // lane 0: t0_0 + t0_1, lane 2: t0_2 + t0_3
     const float t23 = __shfl(t01, 2, 32);
     const float res = t01 + t23;                                      // lane 0
+    double sum = (double)res;                                         // + the tail in double, in order of e
+    for (int e = 0; e < tl; e++) sum += (double)__shfl(pt, e, 32);
     if (l == 0 && valid) {
-        double sum = (double)res;
-        for (int e = np; e < K; e++) sum += (double)(h2f_bits(xr[e]) * h2f_bits(f2h_bits(yr[e])));
         d[o] = (float)sum;
         if (merged) merged[(i1 * ne02 + i2) * ne01 + i0] = (float)sum;
     }

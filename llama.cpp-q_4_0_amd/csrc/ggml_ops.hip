@@ -639,13 +639,18 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max_reg(const float *x,
     if (r >= nrows) return;
     const int64_t o = r * ncols, j = r % rows_per_channel;
     float m[NV];
+    // the row's loads and then its table lookups as unconditional loads of clamped indices, so each
+    // group issues back to back (a load under a branch waits at the join); values selected after
+    float xv[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) xv[k] = x[o + (lane + 64 * k < ncols ? lane + 64 * k : ncols - 1)];
     float mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < NV; k++) {
         const int64_t i = lane + 64 * k;
         m[k] = -INFINITY;
         if (i < ncols) {
-            const float sv = x[o + i] * v;
+            const float sv = xv[k] * v;
             m[k] = i > n_past + j ? -INFINITY : sv;
             if (scaled) scaled[o + i] = sv;
             if (masked) masked[o + i] = m[k];
@@ -653,12 +658,15 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max_reg(const float *x,
         }
     }
     mx = wave_max_f(mx);
+    uint16_t tv[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) tv[k] = table[f2h_bits(m[k] - mx)];   // -inf - mx: a valid index, unused
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < NV; k++) {
         float e = 0.0f;
         if (m[k] != -INFINITY) {
-            e = h2f_bits(table[f2h_bits(m[k] - mx)]);
+            e = h2f_bits(tv[k]);
             s += (double)e;
         }
         m[k] = e;

@@ -1011,8 +1011,11 @@ __global__ __launch_bounds__(TPB) void k_silu_mul_x9(const float *a, const float
     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
     if (in) {
         const float4 av = reinterpret_cast<const float4 *>(a)[i4], bv = reinterpret_cast<const float4 *>(b)[i4];
-        const float4 sv = make_float4(h2f_bits(table[f2h_bits(av.x)]), h2f_bits(table[f2h_bits(av.y)]),
-                                      h2f_bits(table[f2h_bits(av.z)]), h2f_bits(table[f2h_bits(av.w)]));
+        // the four table indices first, then the four lookups back to back (interleaved with the
+        // conversions they were issued and waited for one at a time)
+        const uint16_t h0 = f2h_bits(av.x), h1 = f2h_bits(av.y), h2 = f2h_bits(av.z), h3 = f2h_bits(av.w);
+        const uint16_t t0 = table[h0], t1 = table[h1], t2 = table[h2], t3 = table[h3];
+        const float4 sv = make_float4(h2f_bits(t0), h2f_bits(t1), h2f_bits(t2), h2f_bits(t3));
         if (u) reinterpret_cast<float4 *>(u)[i4] = sv;
         r = make_float4(sv.x * bv.x, sv.y * bv.y, sv.z * bv.z, sv.w * bv.w);
         reinterpret_cast<float4 *>(out)[i4] = r;

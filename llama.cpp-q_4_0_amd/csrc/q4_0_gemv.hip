@@ -272,9 +272,14 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
                     const uint32_t av[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
                     const uint32_t bv[4] = {rb[i].x, rb[i].y, rb[i].z, rb[i].w};
                     float u[4], o[4];
+                    uint16_t hi[4], tv[4];           // indices first, then the lookups back to back
+#pragma unroll
+                    for (int c = 0; c < 4; c++) hi[c] = f2h(__uint_as_float(av[c]));
+#pragma unroll
+                    for (int c = 0; c < 4; c++) tv[c] = ((g_u16 *)nrm.table)[hi[c]];
 #pragma unroll
                     for (int c = 0; c < 4; c++) {    // as k_silu_mul: s = table[fp16(a)], out = s * b
-                        u[c] = h2f(((g_u16 *)nrm.table)[f2h(__uint_as_float(av[c]))]);
+                        u[c] = h2f(tv[c]);
                         o[c] = u[c] * __uint_as_float(bv[c]);
                     }
                     if (store) {

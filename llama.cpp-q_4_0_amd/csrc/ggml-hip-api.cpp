@@ -1,0 +1,418 @@
+// ggml-hip-api.cpp — the tensor-free C ABI on device pointers (quantizers, mul_mat, sibling batches, decode
+// chains, weight images) and the device plumbing the bindings use (streams, events, graphs, copies).
+#include "ggml-hip-internal.h"
+
+using namespace ghh;
+
+extern "C" {
+
+// ------------------------------------------------------------------------------------------
+// tensor-free entry points
+
+int ggml_hip_quantize_q8_0(const float *dev_x, int64_t K, int64_t N, void *dev_xq, void *stream) {
+    if (!dev_x || !dev_xq || K <= 0 || K % QK || N < 0) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    if (!aligned(dev_x, 16) || !aligned(dev_xq, 2)) return fail(GGML_HIP_ERR_INVALID, "x must be 16-byte aligned");
+    HIP_RET(ghip::quantize_q8_0_aos(dev_x, K, N, dev_xq, resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_quantize_q4_0(const float *dev_w, int64_t K, int64_t M, void *dev_wq, void *stream) {
+    if (!dev_w || !dev_wq || K <= 0 || K % QK || M < 0) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    if (!aligned(dev_w, 16) || !aligned(dev_wq, 2)) return fail(GGML_HIP_ERR_INVALID, "w must be 16-byte aligned");
+    HIP_RET(ghip::quantize_q4_0(dev_w, K, M, dev_wq, resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_dequantize_q4_0(const void *dev_wq, int64_t K, int64_t M, float *dev_w, void *stream) {
+    if (!dev_w || !dev_wq || K <= 0 || K % QK || M < 0) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    HIP_RET(ghip::dequantize_q4_0(dev_wq, K, M, dev_w, resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_mul_mat_q4_0(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N, float *dev_y,
+                          void *stream) {
+    ensure_init();
+    return mul_mat_dev(dev_w, K, M, dev_x, N, dev_y, M, 0, resolve_stream(stream));
+}
+
+int ggml_hip_mul_mat_q4_0_ex(const void *dev_w, int64_t K, int64_t M, const float *dev_x, int64_t N, float *dev_y,
+                             int64_t ldy, int algo, void *stream) {
+    ensure_init();
+    return mul_mat_dev(dev_w, K, M, dev_x, N, dev_y, ldy, algo, resolve_stream(stream));
+}
+
+int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *M, int64_t K, const float *dev_x,
+                                int64_t N, float *const *dev_y, void *stream) {
+    ensure_init();
+    if (n < 1 || n > ghip::GEMV_MULTI_MAX || !dev_w || !M || !dev_y)
+        return fail(GGML_HIP_ERR_INVALID, "n must be 1..4 with non-null arrays");
+    hipStream_t s = resolve_stream(stream);
+    int64_t total = 0;
+    for (int i = 0; i < n; i++) {
+        if (!dev_w[i] || !dev_y[i] || M[i] <= 0) return fail(GGML_HIP_ERR_INVALID, "null matrix or M <= 0");
+        if (!aligned(dev_w[i], 16) || !aligned(dev_y[i], 4)) return fail(GGML_HIP_ERR_INVALID, "misaligned W or y");
+        total += M[i];
+    }
+    if (N == 0) return GGML_HIP_OK;
+    if (exact_mode() && n > 1 && N >= 1 && dev_x && K > 0 && K % 64 == 0 && aligned(dev_x, 16) && total < (1 << 30)) {
+        // exact mode: x quantized once, every sibling in ONE exact launch (bitwise the same as one
+        // launch per matrix: each output row's chain does not depend on the grid)
+        for (int i = 0; i < n; i++)
+            if (M[i] * (K / QK) * Q4B >= ((int64_t)1 << 31)) return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large");
+        const int id = current_device();
+        void *ws = nullptr;
+        const int wrc = stream_workspace(id, s, workspace_bytes(K, N), &ws);
+        if (wrc != GGML_HIP_OK) return wrc;
+        int8_t *qs = (int8_t *)ws;
+        float *xd = (float *)((char *)ws + ((size_t)(N * K + 255) & ~(size_t)255));
+        HIP_RET(ghip::quantize_q8_0_soa(dev_x, K, N, qs, xd, s));
+        int64_t ldy[ghip::GEMV_MULTI_MAX];
+        for (int i = 0; i < n; i++) ldy[i] = M[i];
+        HIP_RET(ghip::mm_exact_q4_0_multi(n, dev_w, M, K, qs, xd, N, dev_y, ldy, s));
+        return GGML_HIP_OK;
+    }
+    if (N > ghip::gemv_max_tokens(K) || total >= (1 << 30) || exact_mode()) {
+        if (!exact_mode() && dev_x && K > 0 && K % 64 == 0) {
+            // the image GEMMs' per-call weight image grows with M: size the workspace for the largest
+            // sibling first, so that a later sibling cannot reallocate it under the shared q8_0 / x image
+            // an earlier sibling left there.  At every N of the GEMM path: a tall sibling with an image
+            // takes the image GEMM at any N above the GEMV's (IMG_MIN_M), next to split-K siblings
+            int64_t mmax = 0;
+            for (int i = 0; i < n; i++) mmax = std::max(mmax, M[i]);
+            void *ws = nullptr;
+            const int wrc = stream_workspace(current_device(), s, workspace_bytes_mm(K, N, mmax), &ws);
+            if (wrc != GGML_HIP_OK) return wrc;
+        }
+        if (n > 1 && !exact_mode()) {
+            const int rc = mul_mat_group_g9(n, dev_w, M, K, dev_x, N, dev_y, s);
+            if (rc != 1) return rc;           // 1: not every sibling takes k_gemm9 on an fp6 image
+        }
+        unsigned xq = 0;
+        for (int i = 0; i < n; i++) {       // GEMM / exact path: x quantized once, one launch per matrix
+            int rc = mul_mat_dev(dev_w[i], K, M[i], dev_x, N, dev_y[i], M[i], 0, s, &xq);
+            if (rc != GGML_HIP_OK) return rc;
+        }
+        return GGML_HIP_OK;
+    }
+    // validate the shared shape once through the single-matrix checks
+    if (!dev_x || K <= 0 || K % 64 != 0 || !aligned(dev_x, 16)) return fail(GGML_HIP_ERR_INVALID, "bad x or K");
+    for (int i = 0; i < n; i++)
+        if (M[i] * (K / QK) * Q4B >= ((int64_t)1 << 31)) return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large");
+    int64_t ldy[ghip::GEMV_MULTI_MAX];
+    for (int i = 0; i < n; i++) ldy[i] = M[i];
+    HIP_RET(ghip::gemv_q4_0_multi(n, dev_w, M, K, dev_x, N, dev_y, ldy, g_dev[current_device()].info, s));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_set_exact(int on) {
+    g_exact.store(on ? 1 : 0, std::memory_order_relaxed);
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_get_exact(void) { return exact_mode() ? 1 : 0; }
+
+int ggml_hip_reserve_workspace(int64_t K, int64_t N) {
+    ensure_init();
+    if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
+    return reserve_workspace(current_device(), workspace_bytes(K, N));
+}
+
+int ggml_hip_weight_image_create(const void *dev_w, int64_t K, int64_t M, void *stream) {
+    ensure_init();
+    if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
+    if (!dev_w || K <= 0 || K % 64 != 0 || M <= 0 || !aligned(dev_w, 16))
+        return fail(GGML_HIP_ERR_INVALID, "bad weight pointer or shape (K % 64 == 0, 16-byte aligned)");
+    if (M * (K / QK) * Q4B >= ((int64_t)1 << 31) || (K / QK) * 2048 >= ((int64_t)1 << 31))
+        return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large");
+    hipStream_t s = resolve_stream(stream);
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
+        return fail(GGML_HIP_ERR_INVALID, "weight images are built outside stream capture");
+    ghip::rec_flush_at("weight image");
+    if (!wimage_ensure(current_device(), dev_w, K, M, s)) return fail(GGML_HIP_ERR_NOMEM, "weight image allocation failed");
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_weight_image_free(const void *dev_w) {
+    ensure_init();
+    ghip::rec_flush_at("weight image");
+    return (int)wimage_drop(dev_w, 0);
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int ggml_hip_debug_set_gemm_version(int v) {
+    if (v != -1 && (v < 7 || v > 11)) return fail(GGML_HIP_ERR_INVALID, "version must be 7 ... 11 or -1");
+    g_gemm_v.store(v, std::memory_order_relaxed);
+    if (v == -1) (void)gemm_version();            // re-read GGML_HIP_GEMM_V
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M) {
+    ensure_init();
+    if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
+    if (K <= 0 || N < 0 || M < 0) return fail(GGML_HIP_ERR_INVALID, "bad shape");
+    return reserve_workspace(current_device(), workspace_bytes_mm(K, N, M));
+}
+
+// ------------------------------------------------------------------------------------------
+// decode chains: tasks validated once, launched as stream-ordered sibling GEMVs (one launch per task).
+// Round 2 ran a chain as one persistent launch and round 4 as overlapped launches on two streams with
+// per-workgroup flag hand-offs; both were bitwise equal and measured slower than one
+// kernel per task (the in-launch hand-off costs more than a kernel boundary plus the GEMV's prologue),
+// so a chain is the per-launch path.
+
+}  // extern "C"
+
+struct ggml_hip_chain {
+    int device = 0;
+    std::vector<ggml_hip_chain_task> tasks;
+};
+
+extern "C" {
+
+int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **out) {
+    ensure_init();
+    if (!out) return fail(GGML_HIP_ERR_INVALID, "null out");
+    *out = nullptr;
+    if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
+    if (ntasks < 1 || !tasks) return fail(GGML_HIP_ERR_INVALID, "ntasks must be >= 1");
+    for (int t = 0; t < ntasks; t++) {
+        const ggml_hip_chain_task &k = tasks[t];
+        if (k.nmat < 1 || k.nmat > ghip::GEMV_MULTI_MAX) return fail(GGML_HIP_ERR_INVALID, "nmat must be 1..4");
+        if (k.K <= 0 || k.K % 64 != 0 || !k.x || !aligned(k.x, 16))
+            return fail(GGML_HIP_ERR_INVALID, "bad x or K (K % 64 == 0, 16-byte aligned x)");
+        for (int i = 0; i < k.nmat; i++) {
+            if (!k.W[i] || !k.y[i] || k.M[i] <= 0 || !aligned(k.W[i], 16) || !aligned(k.y[i], 4))
+                return fail(GGML_HIP_ERR_INVALID, "null / misaligned W or y, or M <= 0");
+            // a task's y may not overlap its own x (its rows read x while others write y)
+            const uint64_t xlo = (uint64_t)(uintptr_t)k.x, xhi = xlo + 4 * (uint64_t)k.K;
+            const uint64_t yp = (uint64_t)(uintptr_t)k.y[i];
+            if (yp < xhi && xlo < yp + 4 * (uint64_t)k.M[i]) return fail(GGML_HIP_ERR_INVALID, "a task's y overlaps its own x");
+        }
+    }
+    auto *c = new ggml_hip_chain();
+    c->device = current_device();
+    c->tasks.assign(tasks, tasks + ntasks);
+    *out = c;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_chain_launch(ggml_hip_chain *c, void *stream) {
+    ensure_init();
+    if (!c) return fail(GGML_HIP_ERR_INVALID, "null chain");
+    if (current_device() != c->device) return fail(GGML_HIP_ERR_INVALID, "chain belongs to another device");
+    hipStream_t s = resolve_stream(stream);
+    for (const auto &k : c->tasks) {
+        const int rc = ggml_hip_mul_mat_q4_0_multi(k.nmat, k.W, k.M, k.K, k.x, 1, (float *const *)k.y, s);
+        if (rc != GGML_HIP_OK) return rc;
+    }
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_chain_status(ggml_hip_chain *c) {
+    if (!c) return fail(GGML_HIP_ERR_INVALID, "null chain");
+    HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
+    return 0;
+}
+
+int ggml_hip_chain_destroy(ggml_hip_chain *c) {
+    delete c;
+    return GGML_HIP_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// ------------------------------------------------------------------------------------------
+// device plumbing
+
+int ggml_hip_device_count(void) {
+    ensure_init();
+    return g_device_count;
+}
+
+int ggml_hip_set_device(int device) {
+    ensure_init();
+    HIP_RET(hipSetDevice(device));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_get_device(void) { return current_device(); }
+
+void *ggml_hip_dev_malloc(size_t size) {
+    ensure_init();
+    void *p = nullptr;
+    if (hipMalloc(&p, size ? size : 1) != hipSuccess) {
+        (void)hipGetLastError();
+        g_last_error = "hipMalloc failed";
+        return nullptr;
+    }
+    return p;
+}
+
+void ggml_hip_dev_free(void *ptr) {
+    if (ptr) (void)GHIP_SYNC(hipFree)(ptr);
+}
+
+int ggml_hip_memcpy_h2d(void *dst, const void *src, size_t size, void *stream) {
+    flush_deferred();
+    hipStream_t s = resolve_stream(stream);
+    HIP_RET(GHIP_SYNC(hipMemcpyAsync)(dst, src, size, hipMemcpyHostToDevice, s));
+    HIP_RET(GHIP_SYNC(hipStreamSynchronize)(s));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_memcpy_d2h(void *dst, const void *src, size_t size, void *stream) {
+    flush_deferred();
+    hipStream_t s = resolve_stream(stream);
+    HIP_RET(GHIP_SYNC(hipMemcpyAsync)(dst, src, size, hipMemcpyDeviceToHost, s));
+    HIP_RET(GHIP_SYNC(hipStreamSynchronize)(s));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_memcpy_d2d(void *dst, const void *src, size_t size, void *stream) {
+    flush_deferred();
+    HIP_RET(GHIP_SYNC(hipMemcpyAsync)(dst, src, size, hipMemcpyDeviceToDevice, resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_memset(void *dst, int value, size_t size, void *stream) {
+    HIP_RET(GHIP_SYNC(hipMemsetAsync)(dst, value, size, resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_stream_synchronize(void *stream) {
+    flush_deferred();
+    HIP_RET(GHIP_SYNC(hipStreamSynchronize)(resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_device_synchronize(void) {
+    flush_deferred();
+    HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
+    return GGML_HIP_OK;
+}
+
+void *ggml_hip_default_stream(void) { return (void *)resolve_stream(nullptr); }
+
+void *ggml_hip_stream_create(void) {
+    ensure_init();
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        g_last_error = "hipStreamCreateWithFlags failed";
+        return nullptr;
+    }
+    return (void *)s;
+}
+
+int ggml_hip_stream_destroy(void *stream) {
+    if (!stream) return GGML_HIP_OK;
+    hipStream_t s = (hipStream_t)stream;
+    HIP_RET(GHIP_SYNC(hipStreamSynchronize)(s));
+    for (int id = 0; id < g_device_count; id++) {
+        Device &d = g_dev[id];
+        std::lock_guard<std::mutex> lk(d.mu);
+        auto it = d.stream_ws.find(s);
+        if (it != d.stream_ws.end()) {
+            if (it->second.ptr) HIP_RET(GHIP_SYNC(hipFree)(it->second.ptr));
+            d.stream_ws.erase(it);
+        }
+    }
+    HIP_RET(GHIP_SYNC(hipStreamDestroy)(s));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_fill_gaussian(float *dev_dst, int64_t n, uint64_t seed, float mean, float stdv, void *stream) {
+    HIP_RET(ghip::fill_gaussian(dev_dst, n, seed, mean, stdv, resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+void *ggml_hip_event_create(void) {
+    ensure_init();
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return (void *)e;
+}
+
+int ggml_hip_event_record(void *event, void *stream) {
+    HIP_RET(GHIP_SYNC(hipEventRecord)((hipEvent_t)event, resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+float ggml_hip_event_elapsed_ms(void *start, void *stop) {
+    float ms = -1.0f;
+    hipError_t e = GHIP_SYNC(hipEventSynchronize)((hipEvent_t)stop);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, (hipEvent_t)start, (hipEvent_t)stop);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();      // do not leave a sticky error for the next launch check
+        g_last_error = std::string("hipEventElapsedTime: ") + hipGetErrorString(e);
+        return -1.0f;
+    }
+    return ms;
+}
+
+void ggml_hip_event_destroy(void *event) {
+    if (event) (void)hipEventDestroy((hipEvent_t)event);
+}
+
+struct ggml_hip_graph {
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+};
+
+int ggml_hip_graph_begin(void *stream) {
+    HIP_RET(GHIP_SYNC(hipStreamBeginCapture)(resolve_stream(stream), hipStreamCaptureModeThreadLocal));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_graph_end(void *stream, ggml_hip_graph **out) {
+    if (!out) return fail(GGML_HIP_ERR_INVALID, "null graph out");
+    auto *g = new ggml_hip_graph;
+    HIP_RET(GHIP_SYNC(hipStreamEndCapture)(resolve_stream(stream), &g->graph));
+    HIP_RET(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0));
+    *out = g;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_graph_launch(ggml_hip_graph *g, void *stream) {
+    if (!g) return fail(GGML_HIP_ERR_INVALID, "null graph");
+    HIP_RET(GHIP_SYNC(hipGraphLaunch)(g->exec, resolve_stream(stream)));
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_graph_destroy(ggml_hip_graph *g) {
+    if (!g) return GGML_HIP_OK;
+    (void)hipGraphExecDestroy(g->exec);
+    (void)hipGraphDestroy(g->graph);
+    delete g;
+    return GGML_HIP_OK;
+}
+
+const char *ggml_hip_last_error(void) { return g_last_error.c_str(); }
+
+// not in the public header: tests force each GEMV launch policy (all must give the same y)
+int ggml_hip_debug_set_gemv_policy(int map, int depth, int rowitems, int wg_per_cu) {
+    if (map < -1 || map > 2 || depth < 0 || depth > 2 || rowitems < 0 || rowitems > 1 || wg_per_cu < 0)
+        return fail(GGML_HIP_ERR_INVALID, "bad GEMV policy");
+    ghip::gemv_set_policy(map, depth, rowitems, wg_per_cu);
+    return GGML_HIP_OK;
+}
+
+// not in the public header: the chunk-balanced decode GEMV (BAL) for K > 12288: -1 auto, 0 off, 1 on
+int ggml_hip_debug_set_gemv_bal(int bal) {
+    if (bal < -1 || bal > 1) return fail(GGML_HIP_ERR_INVALID, "bad GEMV balance mode");
+    ghip::gemv_set_bal(bal);
+    return GGML_HIP_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+const char *ggml_hip_version(void) { return "ggml-hip q4_0 gfx950 r1"; }
+
+}  // extern "C"

@@ -17,7 +17,7 @@
 // The transcendental parts (silu, exp, cos/sin) are NOT evaluated on the device: ggml.c itself
 // evaluates silu and exp through 64 K-entry fp16 tables built with the host libm (ggml.c:4246-4254),
 // and rope's cos/sin are host libm values too; the backend builds the same tables on the host
-// (ggml-hip.cpp) and the kernels look them up.  All other arithmetic is IEEE single/double in the
+// (ggml-hip-ops.cpp) and the kernels look them up.  All other arithmetic is IEEE single/double in the
 // CPU's order (built with -ffp-contract=off; the sums the CPU forms in double are formed in double).
 // These are small, latency-bound launches (a decode layer moves a few KB through them); one wave
 // per row where the CPU reduces over a row, one lane per element otherwise.
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(TPB, 2) void k_mul_mat_f16_f32_tiled(const char *s0
 }
 
 // ----------------------------------------------------------------------------------- fused chains
-// Back-to-back nodes of a LLaMA graph in one launch (ggml-hip.cpp defers the producer until its
+// Back-to-back nodes of a LLaMA graph in one launch (ggml-hip-fuse.cpp defers the producer until its
 // consumer arrives).  Each stage computes exactly what its own node's kernel above computes, in
 // the same order, and writes that node's output too unless it shares the final output's buffer
 // (in-place nodes), so every intermediate tensor holds the value ggml.c would give it.

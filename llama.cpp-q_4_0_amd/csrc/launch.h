@@ -30,7 +30,7 @@ bool rec_pending();
 void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, int nargs, void *const *args,
                 const size_t *sizes, const size_t *aligns);
 // submits the recorded launches (no-op when none are pending); every backend HIP call that is not
-// a kernel launch calls it first (GHIP_SYNC in ggml-hip.cpp)
+// a kernel launch calls it first (GHIP_SYNC, ggml-hip-internal.h)
 void rec_flush();
 void rec_flush_at(const char *why);      // the same, naming the caller (GGML_HIP_TRACE_GRAPH=1 prints it)
 // recording on / off for stream s (switching stream or turning it off submits what is pending)

@@ -22,7 +22,7 @@ namespace ghip {
 // segment of recv instead of copying the (stale) landing slot.  A comm with any error bit set is failed
 // for good: every later launch only copies this rank's own slice and fills the peers' segments with NaN
 // (no stores to peers, no waits, the epoch stays), and the host returns an error before launching the
-// next all-gather (ggml-hip.cpp comm_allgather).  Before round 4 a timed-out wait copied the stale slot
+// next all-gather (ggml-hip-comm.cpp comm_allgather).  Before round 4 a timed-out wait copied the stale slot
 // and advanced the epoch, so the peers' epochs drifted apart and every later wait timed out in turn:
 // one late peer became a cascade of bounded waits whose sum outran the caller's join (the 3-rank
 // loopback "deadlock" of the round-3 suite).

@@ -232,7 +232,9 @@ int ggml_hip_comm_destroy(ggml_hip_comm *comm);
 int ggml_hip_comm_init_local(ggml_hip_comm **comms, int nranks, const int *devices);
 /* One process per rank without RCCL: the comm's host collectives (allreduce_host, the P2P handle
  * exchange) go through files in dir, a directory every rank can read and write (rank r writes
- * <dir>/c<seq>_r<r>).  Device all-gathers need the P2P transport (ggml_hip_comm_enable_p2p); the RCCL
+ * <dir>/c<nonce>_<seq>_r<r>).  Init is collective: rank 0 publishes a fresh session nonce as <dir>/session
+ * and refuses a directory where that name exists (a session in progress or a crashed one's leftover), so
+ * files of different sessions never mix.  Device all-gathers need the P2P transport (ggml_hip_comm_enable_p2p); the RCCL
  * transport is unavailable.  It also lets several processes share ONE device (RCCL refuses that),
  * which is how the cross-process IPC path of the P2P all-gather is tested on a one-GPU box. */
 int ggml_hip_comm_init_file(ggml_hip_comm **comm, int nranks, int rank, const char *dir);
@@ -250,12 +252,17 @@ int ggml_hip_comm_rank(const ggml_hip_comm *comm, int *rank, int *nranks);
  * peer's segment (never the stale landing slot), later gathers fill every peer segment with NaN
  * without waiting, and the next split mul_mat / all-gather on the comm returns GGML_HIP_ERR_COMM
  * before enqueueing anything (the reference stops at its first failed copy, CUDA_CHECK,
- * ggml-cuda.cu:22-51).  p2p_status synchronizes the device and returns 0, or the bit mask of peers
- * whose data never arrived (sticky). */
+ * ggml-cuda.cu:22-51).  The rank that sees a failure first notifies every peer (a failure word stored
+ * into each peer's control block over the same mapping), and the peers' waits poll it, so every rank
+ * fails within one poll instead of after its own timeout.  p2p_status synchronizes the device and
+ * returns 0, or the bit mask of peers whose data never arrived or that reported a failure (sticky).
+ * comm_abort fails this rank's comm on purpose and sends the same notice (ncclCommAbort's role; the
+ * timeout is a kernel argument, so gathers captured in a HIP graph keep the value of their capture). */
 int ggml_hip_comm_enable_p2p(ggml_hip_comm *comm, int64_t max_floats);
 int ggml_hip_comm_set_transport(ggml_hip_comm *comm, int transport);
 int ggml_hip_comm_p2p_status(ggml_hip_comm *comm);
 int ggml_hip_comm_set_p2p_timeout(ggml_hip_comm *comm, double ms);
+int ggml_hip_comm_abort(ggml_hip_comm *comm);
 /* All-reduce of n <= 64 host doubles in place (op 0 sum, 1 max, 2 min) over the comm; synchronous,
  * so it is also a barrier (bench harness: max-over-ranks timing without a second runtime). */
 int ggml_hip_comm_allreduce_host(ggml_hip_comm *comm, double *vals, int n, int op);

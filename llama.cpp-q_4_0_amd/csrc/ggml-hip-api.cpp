@@ -136,7 +136,9 @@ int ggml_hip_weight_image_create(const void *dev_w, int64_t K, int64_t M, void *
 int ggml_hip_weight_image_free(const void *dev_w) {
     ensure_init();
     ghip::rec_flush_at("weight image");
-    return (int)wimage_drop(dev_w, 0);
+    const int64_t n = wimage_drop(dev_w, 0);
+    if (n) wcache_image_dropped(dev_w);
+    return (int)n;
 }
 
 }  // extern "C"

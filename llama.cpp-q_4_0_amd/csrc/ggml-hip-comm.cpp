@@ -5,6 +5,7 @@
 using namespace ghh;
 
 #include <rccl/rccl.h>
+#include <unistd.h>
 
 // ------------------------------------------------------------------------------------------
 // multi-GPU (one process per GPU) over RCCL.
@@ -65,10 +66,11 @@ struct ggml_hip_comm {
     ghip::P2PArgs p2p{};
     void *p2p_mine = nullptr;
     std::vector<void *> p2p_opened;   // IPC mappings of the peers' landing buffers
-    uint32_t *p2p_herr = nullptr;     // host-mapped error word the gather kernel sets on a timeout
+    uint32_t *p2p_herr = nullptr;     // host-mapped error word the gather kernel sets on a failure
     double p2p_timeout_ms = -1.0;     // < 0: GGML_HIP_P2P_TIMEOUT_MS (default 10000)
     // file rendezvous transport (ggml_hip_comm_init_file): host collectives through files in fdir
     std::string fdir;
+    std::string fnonce;           // this session's token: every file name carries it
     uint64_t fseq = 0;
 };
 
@@ -83,12 +85,21 @@ namespace ghh {
         }                                                                                            \
     } while (0)
 
-// file rendezvous: rank r writes <dir>/c<seq>_r<r> (tmp + rename), then reads every rank's file of the
-// same sequence number; a rank that sees all R files of seq knows every rank finished reading seq - 1,
-// so it removes its own file of seq - 1.  Bounded wait (GGML_HIP_COMM_FILE_TIMEOUT_S, default 120 s).
+double file_timeout_s() {
+    static const double limit_s = getenv("GGML_HIP_COMM_FILE_TIMEOUT_S") ? atof(getenv("GGML_HIP_COMM_FILE_TIMEOUT_S")) : 120.0;
+    return limit_s;
+}
+
+// file rendezvous: rank r writes <dir>/c<nonce>_<seq>_r<r> (tmp + rename), then reads every rank's file of
+// the same sequence number; a rank that sees all R files of seq knows every rank finished reading seq - 1,
+// so it removes its own file of seq - 1.  Bounded wait (GGML_HIP_COMM_FILE_TIMEOUT_S, default 120 s).  The
+// session nonce (file_join) keeps a reused directory from feeding a dead session's files of the same
+// sequence number into this one; at most one file per rank (its last) outlives a session.
 int file_allgather(ggml_hip_comm *c, const void *mine, size_t n, std::vector<char> &all) {
     const uint64_t seq = c->fseq++;
-    auto name = [&](uint64_t s, int r) { return c->fdir + "/c" + std::to_string(s) + "_r" + std::to_string(r); };
+    auto name = [&](uint64_t s, int r) {
+        return c->fdir + "/c" + c->fnonce + "_" + std::to_string(s) + "_r" + std::to_string(r);
+    };
     const std::string me = name(seq, c->rank);
     {
         FILE *f = fopen((me + ".tmp").c_str(), "wb");
@@ -97,7 +108,7 @@ int file_allgather(ggml_hip_comm *c, const void *mine, size_t n, std::vector<cha
         if (fclose(f) != 0 || !ok) return fail(GGML_HIP_ERR_COMM, "file comm: short write " + me);
         if (rename((me + ".tmp").c_str(), me.c_str()) != 0) return fail(GGML_HIP_ERR_COMM, "file comm: rename " + me);
     }
-    static const double limit_s = getenv("GGML_HIP_COMM_FILE_TIMEOUT_S") ? atof(getenv("GGML_HIP_COMM_FILE_TIMEOUT_S")) : 120.0;
+    const double limit_s = file_timeout_s();
     all.assign(n * c->nranks, 0);
     const auto t0 = std::chrono::steady_clock::now();
     for (int r = 0; r < c->nranks; r++) {
@@ -114,6 +125,65 @@ int file_allgather(ggml_hip_comm *c, const void *mine, size_t n, std::vector<cha
         }
     }
     if (seq > 0) (void)remove(name(seq - 1, c->rank).c_str());
+    return GGML_HIP_OK;
+}
+
+// The session of a file comm (collective, inside ggml_hip_comm_init_file): rank 0 publishes a fresh random
+// nonce as <dir>/session with link(2), which fails when the name exists, so a directory in use or the
+// leftover of a crashed session is refused loudly instead of mixing sessions; the other ranks wait for
+// it (bounded), and the first all-gather of the session (the join) tells rank 0 that every rank has read
+// it, after which it removes <dir>/session so the directory can host the next session.
+int file_join(ggml_hip_comm *c) {
+    const std::string sess = c->fdir + "/session";
+    if (c->rank == 0) {
+        uint64_t v = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() ^ ((uint64_t)getpid() << 32);
+        FILE *ur = fopen("/dev/urandom", "rb");
+        if (ur) {
+            uint64_t r = 0;
+            if (fread(&r, 1, sizeof r, ur) == sizeof r) v ^= r;
+            fclose(ur);
+        }
+        char hex[17];
+        snprintf(hex, sizeof hex, "%016llx", (unsigned long long)v);
+        const std::string tmp = sess + ".tmp" + hex;
+        FILE *f = fopen(tmp.c_str(), "wb");
+        if (!f) return fail(GGML_HIP_ERR_COMM, "file comm: cannot write " + tmp);
+        const bool ok = fwrite(hex, 1, 16, f) == 16;
+        if (fclose(f) != 0 || !ok) return fail(GGML_HIP_ERR_COMM, "file comm: short write " + tmp);
+        const int lrc = link(tmp.c_str(), sess.c_str());
+        (void)remove(tmp.c_str());
+        if (lrc != 0)
+            return fail(GGML_HIP_ERR_COMM, "file comm: " + sess + " exists (a session in progress, or left by a crashed "
+                                           "one): use a fresh directory or remove it");
+        c->fnonce = hex;
+    } else {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            FILE *f = fopen(sess.c_str(), "rb");
+            if (f) {
+                char hex[17] = {0};
+                const size_t got = fread(hex, 1, 16, f);
+                fclose(f);
+                if (got == 16) {
+                    c->fnonce = hex;
+                    break;
+                }
+            }
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > file_timeout_s())
+                return fail(GGML_HIP_ERR_COMM, "file comm: timed out waiting for " + sess);
+            std::this_thread::sleep_for(std::chrono::microseconds(500));
+        }
+    }
+    std::vector<char> all;
+    const int32_t me = c->rank;
+    const int rc = file_allgather(c, &me, sizeof me, all);   // the join: every rank has the nonce
+    if (rc != GGML_HIP_OK) return rc;
+    for (int r = 0; r < c->nranks; r++) {
+        int32_t v;
+        memcpy(&v, all.data() + sizeof v * r, sizeof v);
+        if (v != r) return fail(GGML_HIP_ERR_COMM, "file comm: ranks disagree on the session");
+    }
+    if (c->rank == 0) (void)remove(sess.c_str());
     return GGML_HIP_OK;
 }
 
@@ -154,7 +224,7 @@ int comm_allgather(ggml_hip_comm *c, const float *send, float *recv, size_t coun
     // a P2P wait that timed out failed the comm for good (its gathers fill NaN; p2p_gather.hip): the
     // error surfaces here, at the next all-gather, as the reference's CUDA_CHECK would stop at the first
     // failed copy (ggml-cuda.cu:22-51, 2514-2539)
-    if (p2p_failed(c)) return fail(GGML_HIP_ERR_COMM, "P2P all-gather: a peer wait timed out earlier; the comm is failed");
+    if (p2p_failed(c)) return fail(GGML_HIP_ERR_COMM, "P2P all-gather: the comm failed earlier (a peer wait timed out, or a rank aborted)");
     if (c->transport == 1 && c->p2p_on && (int64_t)count <= c->p2p.cap) {
         HIP_RET(ghip::p2p_allgather(c->p2p, send, (int64_t)count, recv, s));
         return GGML_HIP_OK;
@@ -265,6 +335,11 @@ int ggml_hip_comm_init_file(ggml_hip_comm **comm, int nranks, int rank, const ch
     c->rank = rank;
     c->device = current_device();
     c->fdir = dir;
+    const int rc = file_join(c);
+    if (rc != GGML_HIP_OK) {
+        delete c;
+        return rc;
+    }
     *comm = c;
     return GGML_HIP_OK;
 }
@@ -467,7 +542,14 @@ int ggml_hip_comm_enable_p2p(ggml_hip_comm *c, int64_t max_floats) {
         }
         std::vector<char> all;
         const int grc = host_allgather_blob(c, rec, sizeof rec, all);
-        if (grc != GGML_HIP_OK) return grc;   // the transport itself failed: no further collective can run
+        if (grc != GGML_HIP_OK) {              // the transport itself failed: no further collective can run
+            const std::string msg = g_last_error;
+            if (c->p2p_mine) (void)GHIP_SYNC(hipFree)(c->p2p_mine);
+            c->p2p_mine = nullptr;
+            if (c->p2p_herr) (void)hipHostFree(c->p2p_herr);
+            c->p2p_herr = nullptr;
+            return fail(grc, msg);
+        }
         for (int r = 0; r < R; r++) {
             if (r == me) continue;
             if (!all[(size_t)128 * r + 124]) {
@@ -505,6 +587,7 @@ int ggml_hip_comm_enable_p2p(ggml_hip_comm *c, int64_t max_floats) {
     for (int r = 0; r < R; r++) {
         a.land[r] = (float *)base[r];
         a.flag[r] = (uint64_t *)(base[r] + p2p_flag_off(R, cap));
+        a.pctl[r] = (uint64_t *)(base[r] + p2p_ctl_off(R, cap));
     }
     a.ctl = (uint64_t *)((char *)c->p2p_mine + p2p_ctl_off(R, cap));
     a.herr = herr_dev;
@@ -523,8 +606,21 @@ int ggml_hip_comm_set_p2p_timeout(ggml_hip_comm *c, double ms) {
         const char *e = getenv("GGML_HIP_P2P_TIMEOUT_MS");   // builds, page faults, a descheduled rank)
         ms = e && atof(e) > 0.0 ? atof(e) : 10000.0;
     }
+    // s_memrealtime ticks at 100 MHz; clamped so the conversion stays defined.  The timeout is
+    // a kernel argument: gathers captured in a HIP graph keep the value they were captured with.
+    if (!(ms < 1.0e14)) ms = 1.0e14;           // also NaN / inf
     c->p2p_timeout_ms = ms;
-    c->p2p.timeout = (uint64_t)(ms * 1e5);     // s_memrealtime: 100 MHz
+    c->p2p.timeout = (uint64_t)(ms * 1e5);
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_comm_abort(ggml_hip_comm *c) {
+    if (!c) return fail(GGML_HIP_ERR_INVALID, "null comm");
+    if (!c->p2p_on) return fail(GGML_HIP_ERR_INVALID, "P2P not enabled on this comm");
+    HIP_RET(hipSetDevice(c->device));
+    hipStream_t s = g_dev[c->device].stream;
+    HIP_RET(ghip::p2p_abort(c->p2p, s));
+    HIP_RET(GHIP_SYNC(hipStreamSynchronize)(s));
     return GGML_HIP_OK;
 }
 
@@ -539,9 +635,9 @@ int ggml_hip_comm_p2p_status(ggml_hip_comm *c) {
     if (!c || !c->p2p_on) return fail(GGML_HIP_ERR_INVALID, "P2P not enabled on this comm");
     HIP_RET(hipSetDevice(c->device));
     HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
-    uint64_t err = 0;
-    HIP_RET(GHIP_SYNC(hipMemcpy)(&err, c->p2p.ctl + 2, 8, hipMemcpyDeviceToHost));
-    return (int)err;                           // sticky: a failed comm stays failed
+    uint64_t err[2] = {0, 0};
+    HIP_RET(GHIP_SYNC(hipMemcpy)(err, c->p2p.ctl + 2, 16, hipMemcpyDeviceToHost));
+    return (int)(err[0] | err[1]);             // sticky: a failed comm stays failed
 }
 
 int ggml_hip_comm_rank(const ggml_hip_comm *c, int *rank, int *nranks) {
@@ -578,7 +674,7 @@ int ggml_hip_mul_mat_q4_0_split(ggml_hip_comm *c, const void *dev_w_local, int64
                                 const int64_t *row_begin, const float *dev_x, int64_t N, float *dev_y_full,
                                 void *stream) {
     if (!c || !row_begin || !dev_y_full) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
-    if (p2p_failed(c)) return fail(GGML_HIP_ERR_COMM, "P2P all-gather: a peer wait timed out earlier; the comm is failed");
+    if (p2p_failed(c)) return fail(GGML_HIP_ERR_COMM, "P2P all-gather: the comm failed earlier (a peer wait timed out, or a rank aborted)");
     hipStream_t s = resolve_stream(stream);
     const int R = c->nranks;
     int64_t max_rows = 0;
@@ -632,7 +728,7 @@ int ggml_hip_mul_mat_q4_0_split(ggml_hip_comm *c, const void *dev_w_local, int64
 int ggml_hip_mul_mat_q4_0_split_multi(ggml_hip_comm *c, int n, const void *const *dev_w_local, const int64_t *M_total,
                                       const int64_t *const *row_begin, int64_t K, const float *dev_x, int64_t N,
                                       float *const *dev_y_full, void *stream) {
-    if (c && p2p_failed(c)) return fail(GGML_HIP_ERR_COMM, "P2P all-gather: a peer wait timed out earlier; the comm is failed");
+    if (c && p2p_failed(c)) return fail(GGML_HIP_ERR_COMM, "P2P all-gather: the comm failed earlier (a peer wait timed out, or a rank aborted)");
     if (!c || n < 1 || n > 4 || !dev_w_local || !M_total || !row_begin || !dev_y_full)
         return fail(GGML_HIP_ERR_INVALID, "bad arguments");
     const int R = c->nranks;

@@ -169,7 +169,8 @@ int64_t decode_min_weights();
 uint64_t wcache_next_call_id();
 const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, uint64_t call_id);
 bool wcache_images_enabled();
-void wcache_note_image(int id, const void *dev, size_t img_bytes);
+void wcache_note_image(int id, const void *dev, size_t img_bytes, uint64_t call_id);
+void wcache_image_dropped(const void *dev);
 int64_t wcache_invalidate(const void *host, size_t bytes);
 void wcache_note_host_write(const void *data, size_t bytes);
 

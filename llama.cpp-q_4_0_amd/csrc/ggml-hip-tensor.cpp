@@ -228,7 +228,8 @@ void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst) {
                 (src0_dev || wcache_images_enabled())) {
                 const bool had = wimage_find(id, w, K, rows) != nullptr;
                 if (wimage_ensure(id, w, K, rows, s) && !had && !src0_dev)
-                    wcache_note_image(id, w, image_format() == 9 ? ghip::gemm9_w_bytes(K, rows) : ghip::gemm8_w_bytes(K, rows));
+                    wcache_note_image(id, w, image_format() == 9 ? ghip::gemm9_w_bytes(K, rows) : ghip::gemm8_w_bytes(K, rows),
+                                      call_id);
             }
             // activations
             const float *x;

@@ -183,6 +183,22 @@ uint64_t wcache_fingerprint(const uint8_t *p, size_t n) {
     return h;
 }
 
+// LRU eviction (g_wc_mu held) until `incoming` more bytes fit the budget; entries used by the current
+// call (last_use == call_id) are never evicted (a kernel of this call may read them)
+void wcache_evict_locked(size_t incoming, uint64_t call_id) {
+    while (g_wc_resident + incoming > wcache_budget()) {
+        auto victim = g_wc.end();
+        for (auto e = g_wc.begin(); e != g_wc.end(); ++e)
+            if (e->second.last_use != call_id && (victim == g_wc.end() || e->second.last_use < victim->second.last_use))
+                victim = e;
+        if (victim == g_wc.end()) break;                           // everything is in use: over budget
+        wimage_drop(victim->second.dev, victim->second.bytes);
+        HIP_FATAL(GHIP_SYNC(hipFree)(victim->second.dev));
+        g_wc_resident -= victim->second.bytes + victim->second.img_bytes;
+        g_wc.erase(victim);
+    }
+}
+
 // device copy of host bytes [host, host+bytes) on device id (current device = id), uploaded on
 // stream s on a miss; call_id marks entries in use by the current call (never evicted by it)
 const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, uint64_t call_id) {
@@ -202,17 +218,7 @@ const void *wcache_get(int id, const void *host, size_t bytes, hipStream_t s, ui
         g_wc_resident -= it->second.bytes + it->second.img_bytes;
         g_wc.erase(it);
     }
-    while (g_wc_resident + bytes > wcache_budget()) {             // LRU eviction
-        auto victim = g_wc.end();
-        for (auto e = g_wc.begin(); e != g_wc.end(); ++e)
-            if (e->second.last_use != call_id && (victim == g_wc.end() || e->second.last_use < victim->second.last_use))
-                victim = e;
-        if (victim == g_wc.end()) break;                           // everything is in use: over budget
-        wimage_drop(victim->second.dev, victim->second.bytes);
-        HIP_FATAL(GHIP_SYNC(hipFree)(victim->second.dev));
-        g_wc_resident -= victim->second.bytes + victim->second.img_bytes;
-        g_wc.erase(victim);
-    }
+    wcache_evict_locked(bytes, call_id);
     WCacheEntry e;
     e.bytes = bytes;
     e.fp = fp;
@@ -235,13 +241,24 @@ bool wcache_images_enabled() {
     static const bool on = !getenv("GGML_HIP_WEIGHT_CACHE_IMAGES") || atoi(getenv("GGML_HIP_WEIGHT_CACHE_IMAGES")) != 0;
     return on;
 }
-void wcache_note_image(int id, const void *dev, size_t img_bytes) {
+void wcache_note_image(int id, const void *dev, size_t img_bytes, uint64_t call_id) {
     std::lock_guard<std::mutex> lk(g_wc_mu);
     for (auto &e : g_wc)
         if (e.first.device == id && e.second.dev == dev && e.second.img_bytes == 0) {
             e.second.img_bytes = img_bytes;
-            g_wc_resident += img_bytes;                // evicted from at the next miss that needs room
+            g_wc_resident += img_bytes;
+            wcache_evict_locked(0, call_id);           // back under the budget now, not at the next miss
             return;
+        }
+}
+
+// ggml_hip_weight_image_free dropped the image at dev: a cached copy there no longer carries its bytes
+void wcache_image_dropped(const void *dev) {
+    std::lock_guard<std::mutex> lk(g_wc_mu);
+    for (auto &e : g_wc)
+        if (e.second.dev == dev && e.second.img_bytes) {
+            g_wc_resident -= e.second.img_bytes;
+            e.second.img_bytes = 0;
         }
 }
 

@@ -124,13 +124,17 @@ constexpr int P2P_MAX_RANKS = 8;
 struct P2PArgs {
     float *land[P2P_MAX_RANKS];
     uint64_t *flag[P2P_MAX_RANKS];
-    uint64_t *ctl;                   // [0] epoch, [1] arrivals, [2] error bits (peer q timed out: bit q)
+    uint64_t *ctl;                   // [0] epoch, [1] arrivals, [2] error bits (peer q timed out: bit q),
+                                     // [3] failure notices from peers (peer p failed: bit p, stored by p)
+    uint64_t *pctl[P2P_MAX_RANKS];   // every rank's control block (ctl of rank r, mapped here)
     uint32_t *herr;                  // host-mapped error word (nonzero: the comm failed), or nullptr
     uint64_t timeout;                // peer-wait bound in s_memrealtime ticks (100 MHz)
     int me, R;
     int64_t cap;
 };
 hipError_t p2p_allgather(const P2PArgs &a, const float *send, int64_t count, float *recv, hipStream_t s);
+// fail this rank's comm and notify every peer (bit me in each peer's ctl[3]); stream-ordered on s
+hipError_t p2p_abort(const P2PArgs &a, hipStream_t s);
 
 // Synthetic inputs for the bench (splitmix64 + Box-Muller on device).
 hipError_t fill_gaussian(float *dst, int64_t n, uint64_t seed, float mean, float std, hipStream_t s);

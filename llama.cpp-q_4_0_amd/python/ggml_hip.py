@@ -62,6 +62,7 @@ def _bind(L):
         "ggml_hip_comm_set_transport": ([vp, i32], i32),
         "ggml_hip_comm_p2p_status": ([vp], i32),
         "ggml_hip_comm_set_p2p_timeout": ([vp, ctypes.c_double], i32),
+        "ggml_hip_comm_abort": ([vp], i32),
         "ggml_hip_comm_init_file": ([vp, i32, i32, cp], i32),
         "ggml_hip_weight_image_free": ([vp], i32),
         "ggml_hip_weight_image_bytes": ([], i64),

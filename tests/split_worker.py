@@ -29,6 +29,8 @@ def main():
     gh.check(L.ggml_hip_set_device(rank % L.ggml_hip_device_count()), "set_device")
     if mode == "ipc":
         return main_ipc(L, rank, world, os.path.dirname(idfile))
+    if mode == "abort":
+        return main_abort(L, rank, world, os.path.dirname(idfile))
     uid = ctypes.create_string_buffer(128)
     if rank == 0:
         gh.check(L.ggml_hip_comm_unique_id(uid))
@@ -148,6 +150,51 @@ def main_ipc(L, rank, world, cdir):
     L.ggml_hip_stream_destroy(s)
     gh.check(L.ggml_hip_comm_destroy(comm))
     print(f"P2P_IPC_OK rank {rank}/{world}: {nchecks} checks", flush=True)
+
+
+def main_abort(L, rank, world, cdir):
+    """Active failure propagation across processes: one good split, a barrier, then rank 0 aborts its comm
+    0.3 s later while rank 1 runs the next split; rank 1's gather must be released by the notice."""
+    comm = ctypes.c_void_p()
+    gh.check(L.ggml_hip_comm_init_file(ctypes.byref(comm), world, rank, cdir.encode()), "comm_init_file")
+    s = L.ggml_hip_stream_create()
+    K, M, N = 4096, 1024, 1
+    wq, _ = O.quantize_q4_0(O.gaussian(M * K, 0x5EED6200, 0.0, 0.02).reshape(M, K))
+    x = O.gaussian(N * K, 0x5EED7400, 0.0, 1.0).reshape(N, K)
+    rb = np.array([M * r // world for r in range(world + 1)], np.int64)
+    gh.check(L.ggml_hip_comm_enable_p2p(comm, N * M), "enable_p2p (IPC)")
+    xd = gh.DeviceBuffer.from_array(x)
+    wd = gh.DeviceBuffer.from_array(wq[rb[rank]:rb[rank + 1]])
+    yd = gh.DeviceBuffer(N * M * 4)
+
+    def split():
+        return L.ggml_hip_mul_mat_q4_0_split(comm, wd.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p), xd.ptr, N, yd.ptr, s)
+    gh.check(split(), "good split")
+    gh.check(L.ggml_hip_stream_synchronize(s))
+    assert L.ggml_hip_comm_p2p_status(comm) == 0
+    own = yd.download((N, M), np.float32, stream=s)[:, rb[rank]:rb[rank + 1]].copy()
+    v = (ctypes.c_double * 1)(0.0)
+    gh.check(L.ggml_hip_comm_allreduce_host(comm, v, 1, 0), "barrier")
+    if rank == 0:
+        time.sleep(0.3)
+        gh.check(L.ggml_hip_comm_abort(comm), "abort")
+        assert split() == gh.ERR_COMM
+        print("ABORT_OK rank 0 sent the notice", flush=True)
+    else:
+        L.ggml_hip_memset(yd.ptr, 0, yd.nbytes, s)
+        t0 = time.time()
+        gh.check(split(), "split after the peer's abort")
+        gh.check(L.ggml_hip_stream_synchronize(s))
+        waited = time.time() - t0
+        got = yd.download((N, M), np.float32, stream=s)
+        assert np.array_equal(got[:, rb[1]:rb[2]].view(np.uint32), own.view(np.uint32))
+        assert np.all(np.isnan(got[:, rb[0]:rb[1]])), "rank 0's segment must read NaN"
+        assert L.ggml_hip_comm_p2p_status(comm) & 1
+        assert split() == gh.ERR_COMM
+        assert waited < 2.0, f"rank 1 waited {waited:.3f} s (timeout 10 s): the notice did not release it"
+        print(f"ABORT_OK rank 1 released after {waited:.3f} s (0.3 s abort delay, 10 s timeout)", flush=True)
+    L.ggml_hip_stream_destroy(s)
+    gh.check(L.ggml_hip_comm_destroy(comm))
 
 
 if __name__ == "__main__":

@@ -94,3 +94,42 @@ def test_file_comm_ranks_drive_product_host_code(world):
         for r, (p, o) in enumerate(zip(procs, outs)):
             assert p.returncode == 0, f"rank {r}:\n{o[-3000:]}"
             assert "FILE_COMM_OK" in o, o[-2000:]
+
+
+def test_file_comm_session_nonce_and_reuse():
+    """file-comm names carry a per-session nonce that rank 0 publishes as <dir>/session (link(2),
+    refused when the name exists), so a reused directory never feeds a dead session's file of the same
+    sequence number into a new one.  Two world-2 sessions run back to back in ONE directory (the first
+    leaves its last files behind), and a directory holding a session file is refused loudly."""
+    cases = [(4096, 64, 1, None, 31)]
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "cases.json")
+        json.dump(cases, open(path, "w"))
+        cdir = os.path.join(td, "comm")
+        os.mkdir(cdir)
+        env = dict(os.environ, GGML_HIP_COMM_FILE_TIMEOUT_S="60")
+        for session in range(2):
+            procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "file_comm_worker.py"), str(r), "2", cdir, path],
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+                     for r in range(2)]
+            outs = [p.communicate(timeout=180)[0] for p in procs]
+            for r, (p, o) in enumerate(zip(procs, outs)):
+                assert p.returncode == 0 and "FILE_COMM_OK" in o, f"session {session} rank {r}:\n{o[-3000:]}"
+            left = sorted(os.listdir(cdir))
+            assert "session" not in left, left
+            nonces = {f[1:].split("_")[0] for f in left if f.startswith("c")}
+            assert len(nonces) == session + 1, left          # each session's leftovers carry their own nonce
+        # a directory with a session file (in use, or a crashed session's leftover): refused, not joined
+        L = ggml_hip.load()
+        sdir = os.path.join(td, "stale")
+        os.mkdir(sdir)
+        open(os.path.join(sdir, "session"), "w").write("0123456789abcdef")
+        c = ctypes.c_void_p()
+        assert L.ggml_hip_comm_init_file(ctypes.byref(c), 1, 0, sdir.encode()) == ggml_hip.ERR_COMM
+        assert b"session" in L.ggml_hip_last_error()
+        os.remove(os.path.join(sdir, "session"))
+        ggml_hip.check(L.ggml_hip_comm_init_file(ctypes.byref(c), 1, 0, sdir.encode()))   # one rank: joins itself
+        v = (ctypes.c_double * 1)(3.0)
+        ggml_hip.check(L.ggml_hip_comm_allreduce_host(c, v, 1, 0))
+        assert v[0] == 3.0
+        ggml_hip.check(L.ggml_hip_comm_destroy(c))

@@ -403,6 +403,90 @@ def test_p2p_timeout_fails_the_comm():
         L.ggml_hip_comm_destroy(c1)
 
 
+def test_p2p_abort_notifies_a_waiting_peer():
+    """Verdict r4 item 4: a failure propagates actively.  Rank 1's gather is already waiting for rank 0's
+    data (default 10 s timeout) when rank 0 aborts (ggml_hip_comm_abort: bit 0 stored into rank 1's control
+    block over the P2P mapping); rank 1's wait polls that word, so its launch ends within one poll, not
+    after its own timeout: own rows bitwise, rank 0's segment NaN (never the stale slot), p2p_status names
+    rank 0, and the next split call on either rank returns GGML_HIP_ERR_COMM."""
+    import time
+    K, M, N = 4096, 1024, 1
+    wq, x = make_case(K, M, N, seed=78)
+    rb = split_rows(M, 2)
+    L = ggml_hip.load()
+    xd = DB.from_array(x)
+    wds = [DB.from_array(wq[rb[r]:rb[r + 1]]) for r in range(2)]
+    y = DB(N * M * 4)
+    own = gpu_y(wq[rb[1]:rb[2]], K, x)
+    comms = (ctypes.c_void_p * 2)()
+    ggml_hip.check(L.ggml_hip_comm_init_local(comms, 2, None))
+    c0, c1 = ctypes.c_void_p(comms[0]), ctypes.c_void_p(comms[1])
+    s = L.ggml_hip_stream_create()
+    out = {}
+    try:
+        th = threading.Thread(target=lambda: ggml_hip.check(L.ggml_hip_comm_enable_p2p(c1, N * M)))
+        th.start()
+        ggml_hip.check(L.ggml_hip_comm_enable_p2p(c0, N * M))
+        th.join(timeout=60)
+        L.ggml_hip_memset(y.ptr, 0, y.nbytes, s)
+        ggml_hip.synchronize()
+
+        def rank1():
+            t0 = time.time()
+            out["rc"] = L.ggml_hip_mul_mat_q4_0_split(c1, wds[1].ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p), xd.ptr,
+                                                      N, y.ptr, s)
+            out["sync"] = L.ggml_hip_stream_synchronize(s)
+            out["waited"] = time.time() - t0
+        th = threading.Thread(target=rank1)
+        th.start()
+        time.sleep(0.3)                                            # rank 1 is spinning on rank 0's flag now
+        t_abort = time.time()
+        ggml_hip.check(L.ggml_hip_comm_abort(c0), "abort rank 0")
+        th.join(timeout=60)
+        released = time.time() - t_abort
+        assert not th.is_alive()
+        assert out["rc"] == 0 and out["sync"] == 0, out
+        assert released < 1.0, f"rank 1 released {released:.3f} s after the abort (timeout 10 s)"
+        got = y.download((N, M), np.float32, stream=s)
+        assert np.array_equal(got[:, rb[1]:rb[2]].view(np.uint32), own.view(np.uint32))
+        assert np.all(np.isnan(got[:, rb[0]:rb[1]])), "the aborted peer's segment must read NaN"
+        assert L.ggml_hip_comm_p2p_status(c1) & 1, "rank 1's status must name rank 0"
+        for c, r in ((c1, 1), (c0, 0)):
+            rc = L.ggml_hip_mul_mat_q4_0_split(c, wds[r].ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p), xd.ptr, N,
+                                               y.ptr, s)
+            assert rc == ggml_hip.ERR_COMM, (r, rc)
+        print(f"rank 1 waited {out['waited']:.3f} s, released {released * 1e3:.1f} ms after the abort")
+    finally:
+        L.ggml_hip_stream_destroy(s)
+        L.ggml_hip_comm_destroy(c0)
+        L.ggml_hip_comm_destroy(c1)
+
+
+def test_p2p_abort_across_processes_one_gpu():
+    """The same active failure across the process boundary (IPC mappings, tests/split_worker.py mode abort):
+    after one good split on both ranks, rank 1 starts the next one while rank 0 aborts 0.3 s later; rank 1
+    must finish within 2 s (its timeout is 10 s) with rank 0's segment NaN and then get GGML_HIP_ERR_COMM."""
+    R = 2
+    with tempfile.TemporaryDirectory() as td:
+        idfile = os.path.join(td, "uid")
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "split_worker.py"), str(r), str(R), idfile, "abort"],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                 for r in range(R)]
+        outs = []
+        for p in procs:
+            try:
+                outs.append(p.communicate(timeout=100)[0])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        for r, (p, o) in enumerate(zip(procs, outs)):
+            assert p.returncode == 0, f"rank {r} failed:\n{o[-3000:]}"
+            assert "ABORT_OK" in o, o[-2000:]
+        print(outs[1].strip().splitlines()[-1])
+
+
 def test_p2p_loopback_refusal_is_uniform():
     """Ranks on devices [0, 0, 0, 1] (or all on device 0 on a one-GPU box): every rank refuses P2P,
     including one on a device with fewer ranks (the decision was per rank before)."""

@@ -63,23 +63,75 @@ def log(*a):
 
 
 # ---------------------------------------------------------------------------------------------
-def setup_dist(n_gpus):
-    """torchrun env -> (rank, world, local_rank).  No torch in this process: torch bundles its own
+def launch_ranks(n_gpus):
+    """`bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment): start N fresh child
+    processes of this script, one per rank, before this process loads any GPU library (no exec, no
+    relaunch of a process that touched the GPU).  Rank 0's stdout (the one JSON line) is this process's
+    stdout, the other ranks' go to stderr.  The ranks rendezvous through a fresh directory (RCCL unique
+    id file, or the file comm when ranks share a device).  Returns the exit code (the worst rank's)."""
+    import shutil
+    import socket
+    import subprocess
+    import tempfile
+    work = tempfile.mkdtemp(prefix="ggml_hip_bench_")
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    procs = []
+    try:
+        for r in range(n_gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n_gpus), LOCAL_WORLD_SIZE=str(n_gpus),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GGML_HIP_UID_FILE=os.path.join(work, "uid"),
+                       GGML_HIP_COMM_DIR=os.path.join(work, "comm"), GGML_HIP_BENCH_SELF_LAUNCHED="1")
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                          stdout=None if r == 0 else sys.stderr))
+        rcs = [None] * n_gpus
+        t_fail = None
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    rcs[r] = p.poll()
+                    if rcs[r] not in (None, 0) and t_fail is None:
+                        t_fail = time.time()
+                        log(f"[launcher] rank {r} exited with {rcs[r]}")
+            if t_fail is not None and time.time() - t_fail > 60:     # a failed rank: the others get 60 s
+                for r, p in enumerate(procs):
+                    if rcs[r] is None:
+                        log(f"[launcher] terminating rank {r}")
+                        p.terminate()
+                t_fail = time.time() + 1e9
+            time.sleep(0.05)
+        return max(abs(rc) for rc in rcs)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def setup_dist():
+    """launcher env -> (rank, world, local_rank).  No torch in this process: torch bundles its own
     libamdhip64 / librccl, and a second HIP runtime next to /opt/rocm's (which libggml_hip.so is
-    built against) corrupts the process; ranks talk through RCCL only (comm_allreduce_host)."""
+    built against) corrupts the process; ranks talk through RCCL or the file comm only."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", rank))
-    if n_gpus > 1 and world == 1:
-        log(f"--gpus {n_gpus} without a launcher: running 1 rank (use torch.distributed.run, see bench doc)")
     return rank, world, local
 
 
+def _rendezvous_path(kind):
+    """a path every rank of this node derives alike: the launcher's (self-launch sets it), else one named
+    after torchrun's agent (every worker's parent) and its rendezvous port"""
+    env = {"uid": "GGML_HIP_UID_FILE", "comm": "GGML_HIP_COMM_DIR"}[kind]
+    return os.environ.get(env) or os.path.join(
+        "/tmp", f"ggml_hip_{kind}_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}")
+
+
 def exchange_unique_id(gh, L, rank, world):
-    """RCCL unique id from rank 0 to the other ranks of this node through a file named after the
-    launcher (torchrun's agent is every worker's parent) and its rendezvous port."""
-    path = os.environ.get("GGML_HIP_UID_FILE") or os.path.join(
-        "/tmp", f"ggml_hip_uid_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}")
+    """RCCL unique id from rank 0 to the other ranks of this node through a file."""
+    path = _rendezvous_path("uid")
     uid = ctypes.create_string_buffer(128)
     if rank == 0:
         gh.check(L.ggml_hip_comm_unique_id(uid))
@@ -95,6 +147,13 @@ def exchange_unique_id(gh, L, rank, world):
         time.sleep(0.05)
         uid = ctypes.create_string_buffer(open(path, "rb").read(), 128)
     return uid, path
+
+
+def weight_std(K):
+    """W ~ N(0, 1/sqrt(K)): y = W x keeps x's scale, so the decode chain (each launch reads the previous
+    launch's y) stays O(1) over 32 layers (at N(0, 0.02) it grew ~4.4x per layer and overflowed the fp16
+    q8_0 scale by layer ~10); LLaMA-7B's init scale 0.02 is 1.28/sqrt(4096)"""
+    return 1.0 / float(np.sqrt(K))
 
 
 class Stack:
@@ -115,7 +174,7 @@ class Stack:
                 nbytes = q4_bytes(K, m_loc)
                 buf = gh.DeviceBuffer(max(nbytes, 16))
                 seed = seed_base + li * 16 + mi
-                gh.check(L.ggml_hip_fill_gaussian(tmp.ptr, K * m_loc, seed, 0.0, 0.02, None))
+                gh.check(L.ggml_hip_fill_gaussian(tmp.ptr, K * m_loc, seed, 0.0, weight_std(K), None))
                 gh.check(L.ggml_hip_quantize_q4_0(tmp.ptr, K, m_loc, buf.ptr, None))
                 row.append((name, K, M, m_loc, buf, rb))
                 self.bufs.append(buf)
@@ -125,6 +184,11 @@ class Stack:
         tmp.free()
         self.total_bytes = total
 
+    def free(self):
+        for b in self.bufs:
+            b.free()
+        self.bufs = []
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -132,6 +196,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layers", type=int, default=N_LAYERS)
+    ap.add_argument("--config4-layers", type=int, default=40,
+                    help="N > 1: layers of the LLaMA-13B row-sharded line (BASELINE config 4); 0 skips it")
     ap.add_argument("--prefill-tokens", type=int, default=512)
     ap.add_argument("--no-prefill", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -139,6 +205,9 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no HIP graph (launch-per-call)")
     ap.add_argument("--force-split", action="store_true",
                     help="run the multi-GPU code path (row split + RCCL all-gather) even with one rank")
+    ap.add_argument("--comm", choices=("auto", "rccl", "file"), default="auto",
+                    help="N > 1: RCCL communicator (one rank per GPU), or the file-rendezvous comm with the P2P "
+                         "all-gather only (ranks may share a device); auto = file when ranks outnumber devices")
     ap.add_argument("--no-extra", action="store_true", help="skip the LLaMA-13B / Falcon-7B decode lines")
     ap.add_argument("--no-exact", action="store_true", help="skip the exact-mode (bit-identical) decode line")
     ap.add_argument("--no-p2p", action="store_true",
@@ -147,45 +216,67 @@ def main():
                     help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+
     import ggml_hip as gh
     L = gh.load()                            # /opt/rocm HIP + RCCL (no torch in this process)
-    rank, world, local = setup_dist(args.gpus)
+    rank, world, local = setup_dist()
+    if world > 1 and args.gpus != world:
+        log(f"[rank {rank}] --gpus {args.gpus} but WORLD_SIZE {world}: using {world} ranks")
     ndev = L.ggml_hip_device_count()
     if ndev < 1:
         raise SystemExit("no HIP device")
     gh.check(L.ggml_hip_set_device(local % ndev), "set_device")
     stream = L.ggml_hip_default_stream()
 
-    comm = None
+    comm, comm_kind = None, None
     if world > 1 or args.force_split:
-        uid, uid_path = exchange_unique_id(gh, L, rank, world)
+        comm_kind = args.comm if args.comm != "auto" else ("file" if world > ndev else "rccl")
         comm = ctypes.c_void_p()
-        # RCCL prints a version banner on fd 1 at init: keep stdout to the one JSON line
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            gh.check(L.ggml_hip_comm_init(ctypes.byref(comm), world, rank, uid), "comm_init")
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
-        if rank == 0 and world > 1:
+        if comm_kind == "file":
+            cdir = _rendezvous_path("comm")
+            os.makedirs(cdir, exist_ok=True)
+            gh.check(L.ggml_hip_comm_init_file(ctypes.byref(comm), world, rank, cdir.encode()), "comm_init_file")
+        else:
+            uid, uid_path = exchange_unique_id(gh, L, rank, world)
+            # RCCL prints a version banner on fd 1 at init: keep stdout to the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
             try:
-                os.remove(uid_path)      # every rank has joined (comm init is collective)
-            except OSError:
-                pass
+                gh.check(L.ggml_hip_comm_init(ctypes.byref(comm), world, rank, uid), "comm_init")
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
+            if rank == 0 and world > 1:
+                try:
+                    os.remove(uid_path)      # every rank has joined (comm init is collective)
+                except OSError:
+                    pass
 
     def allreduce(vals, op):
-        """sum (0) / max (1) / min (2) of host doubles over the ranks (RCCL; also a barrier)"""
+        """sum (0) / max (1) / min (2) of host doubles over the ranks (RCCL or files; also a barrier)"""
         if comm is None:
             return list(vals)
         buf = (ctypes.c_double * len(vals))(*vals)
         gh.check(L.ggml_hip_comm_allreduce_host(comm, buf, len(vals), op), "allreduce")
         return list(buf)
 
+    def barrier():
+        gh.check(L.ggml_hip_device_synchronize())
+        allreduce([0.0], 0)
+
+    if comm is not None:
+        result = sharded_main(gh, L, comm, comm_kind, rank, world, args, stream, allreduce, barrier)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        L.ggml_hip_comm_destroy(comm)
+        return
+
     t0 = time.time()
-    stack = Stack(gh, L, rank, world, args.layers)
-    log(f"[rank {rank}] weight stack {stack.total_bytes / 1e9:.3f} GB resident in {time.time() - t0:.1f}s")
+    stack = Stack(gh, L, 0, 1, args.layers)
+    log(f"weight stack {stack.total_bytes / 1e9:.3f} GB resident in {time.time() - t0:.1f}s")
 
     # activations (one x per K; synthetic N(0,1)) and outputs (one y per M)
     xs = {}
@@ -202,59 +293,37 @@ def main():
     # sibling groups that share src1 in the LLaMA graph: (wq, wk, wv) and (w1, w3)
     groups = [[0, 1, 2], [3], [4, 5], [6]] if batch else [[i] for i in range(len(LAYER))]
     yb = {i: gh.DeviceBuffer(LAYER[i][2] * 4) for i in range(len(LAYER))}
-    ysplit = {i: gh.DeviceBuffer(LAYER[i][2] * 4) for i in range(len(LAYER))}   # full-M gathered outputs
-    # one GPU: the decode's real data dependencies (each launch reads the y of the launch before it):
-    # wq|wk|wv read the previous layer's w2 output (layer 0: the fixed input row), wo reads q, w1|w3 read
-    # wo's output, w2 reads w1's output.  Multi-GPU keeps one fixed x per K (split_check reads the slices).
+    # the decode's real data dependencies (each launch reads the y of the launch before it): wq|wk|wv read
+    # the previous layer's w2 output (layer 0: the fixed input row), wo reads q, w1|w3 read wo's output,
+    # w2 reads w1's output
     DEP = {0: 6, 1: 6, 2: 6, 3: 0, 4: 3, 5: 3, 6: 4}
-    def x_of(li, i, use_comm):
+
+    def x_of(li, i):
         K = LAYER[i][1]
-        if use_comm or (li == 0 and DEP[i] == 6):
+        if li == 0 and DEP[i] == 6:
             return xs[K].ptr
         return yb[DEP[i]].ptr
 
-    def build_launch_args(use_comm):
-        out = []
-        for li, row in enumerate(stack.mats):
-            for g in groups:
-                if len(g) == 1 or not batch:
-                    out.append(("one" if use_comm else "local",
-                                tuple(row[g[0]]) + (yb[g[0]], ysplit[g[0]], x_of(li, g[0], use_comm))))
-                elif not use_comm:
-                    n = len(g)
-                    wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
-                    yp = (ctypes.c_void_p * n)(*[yb[i].ptr for i in g])
-                    mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
-                    out.append(("multi", (n, wp, mp, row[g[0]][1], yp, x_of(li, g[0], use_comm))))
-                else:                # split siblings: one GEMV launch + one grouped all-gather
-                    n = len(g)
-                    wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
-                    mt = (ctypes.c_int64 * n)(*[row[i][2] for i in g])
-                    rp = (ctypes.c_void_p * n)(*[row[i][5].ctypes.data for i in g])
-                    yp = (ctypes.c_void_p * n)(*[ysplit[i].ptr for i in g])
-                    out.append(("split_multi", (n, wp, mt, rp, row[g[0]][1], yp)))
-        return out
+    launch_args = []
+    for li, row in enumerate(stack.mats):
+        for g in groups:
+            if len(g) == 1 or not batch:
+                launch_args.append(("local", tuple(row[g[0]]) + (yb[g[0]], None, x_of(li, g[0]))))
+            else:
+                n = len(g)
+                wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
+                yp = (ctypes.c_void_p * n)(*[yb[i].ptr for i in g])
+                mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
+                launch_args.append(("multi", (n, wp, mp, row[g[0]][1], yp, x_of(li, g[0]))))
 
-    launch_args = build_launch_args(comm is not None)
-
-    def decode_step(launch_args=launch_args):
+    def decode_step():
         for kind, a in launch_args:
             if kind == "multi":
                 n, wp, mp, K, yp, xp = a
                 gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xp, 1, yp, stream))
-                continue
-            if kind == "split_multi":
-                n, wp, mt, rp, K, yp = a
-                gh.check(L.ggml_hip_mul_mat_q4_0_split_multi(comm, n, wp, mt, rp, K, xs[K].ptr, 1, yp, stream))
-                continue
-            name, K, M, m_loc, buf, rb, ylocal, yfull, xp = a
-            if kind == "local":      # this rank's slice only, no collective
-                gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xp, 1, ylocal.ptr, m_loc, 0, stream))
-            elif comm is None:
-                gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, M, xs[K].ptr, 1, ys[M].ptr, M, 0, stream))
             else:
-                gh.check(L.ggml_hip_mul_mat_q4_0_split(comm, buf.ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p),
-                                                       xs[K].ptr, 1, yfull.ptr, stream))
+                name, K, M, m_loc, buf, rb, ylocal, _, xp = a
+                gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xp, 1, ylocal.ptr, m_loc, 0, stream))
 
     graph = None
     if not args.eager:
@@ -270,10 +339,6 @@ def main():
         else:
             decode_step()
 
-    def barrier():
-        gh.check(L.ggml_hip_device_synchronize())
-        allreduce([0.0], 0)
-
     for _ in range(args.warmup):
         run_step()
     barrier()
@@ -282,82 +347,225 @@ def main():
         run_step()
     barrier()
     elapsed = time.perf_counter() - t_start
-    elapsed = allreduce([elapsed], 1)[0]     # max over ranks
     ms_per_step = elapsed / args.steps * 1e3
     tok_s = args.steps / elapsed * 32 / args.layers if args.layers else 0.0   # per full 32-layer token
+    last = yb[6].download((LAYER[6][2],), np.float32, stream=stream)          # the step's last output
+    finite = bool(np.all(np.isfinite(last)))
+    if not finite:
+        log("WARNING: the decode chain's last output is not finite")
 
     result = {
-        "metric": METRIC, "value": round(tok_s, 2), "unit": "tok/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC, "value": round(tok_s, 2), "unit": "tok/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "q4_0 x q8_0 (int8 dot, f32 acc)",
-        "data": ("synthetic: W ~ N(0,0.02) -> q4_0 (ggml A3 rule, on device), x ~ N(0,1); random-init, no checkpoint"
-                 + ("; each launch reads the previous launch's y (wo <- q, w1|w3 <- wo, w2 <- w1, next layer <- w2)"
-                    if comm is None else "")),
+        "data": ("synthetic: W ~ N(0, 1/sqrt(K)) -> q4_0 (ggml A3 rule, on device), x ~ N(0,1); random-init, no "
+                 "checkpoint; each launch reads the previous launch's y (wo <- q, w1|w3 <- wo, w2 <- w1, next layer "
+                 f"<- w2); last output finite: {finite}"),
         "config": {"workload": "LLaMA-7B q4_0 decode, 32 layers x 7 mul_mats (wq,wk,wv,wo 4096x4096; w1,w3 "
                                "4096->11008; w2 11008->4096), N=1, q8_0 quantize of x included, lm_head excluded",
                    "layers": args.layers, "weights_bytes_per_rank": stack.total_bytes,
                    "graph": graph is not None, "launches_per_layer": len(groups),
-                   "sibling_batching": ("wq|wk|wv and w1|w3 share src1 -> one launch each"
-                                        + (" + one grouped all-gather each" if comm is not None else ""))
-                   if batch else "off",
-                   "collectives_per_layer": len(groups) if comm is not None else 0,
-                   "parallelism": f"row-split x{world} + RCCL all-gather" if world > 1 else "single GPU"},
+                   "sibling_batching": "wq|wk|wv and w1|w3 share src1 -> one launch each" if batch else "off",
+                   "collectives_per_layer": 0, "parallelism": "single GPU", "activations_finite": finite},
     }
+    result["config"]["runtime_libs"] = gh.mapped_runtime_libs()
+    result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
+    if not args.no_prefill and args.prefill_tokens > 0:
+        result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens,
+                                          groups=[tuple(g) for g in groups])
+    if not args.no_exact:
+        result["exact_mode"] = exact_decode(gh, L, decode_step, stream, args)
+    if not args.no_extra:
+        result["other_configs"] = [extra_decode(gh, L, stream, *c, steps=args.steps, warmup=args.warmup)
+                                   for c in EXTRA_CONFIGS]
+    if not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    print(json.dumps(result), flush=True)
 
-    if comm is not None:
-        # same sharded graph without the all-gathers: what the collectives cost
-        g2 = gh.Graph(stream)
-        with g2:
-            decode_step(build_launch_args(False))
+
+# ---------------------------------------------------------------------------------------------
+LLAMA13B = [("wq", 5120, 5120), ("wk", 5120, 5120), ("wv", 5120, 5120), ("wo", 5120, 5120),
+            ("w1", 5120, 13824), ("w3", 5120, 13824), ("w2", 13824, 5120)]
+
+
+def sharded_main(gh, L, comm, comm_kind, rank, world, args, stream, allreduce, barrier):
+    """N ranks (one process each): every matrix row-sharded N ways (GGML_BACKEND_GPU_SPLIT); per layer 4
+    launches (siblings batched) each followed by one grouped all-gather.  The headline is LLaMA-7B (32
+    layers) over the faster self-checked transport; the BASELINE config-4 line (LLaMA-13B, 40 layers) rides
+    along.  File comm: the RCCL transport is unavailable (ranks may share a device), P2P only."""
+    use_p2p = comm_kind == "file" or (world > 1 and not args.no_p2p)
+    p2p_state = {"on": False, "error": None}
+    if use_p2p:
+        max_floats = max(M for _, K, M in LAYER + LLAMA13B)
+        rc = L.ggml_hip_comm_enable_p2p(comm, max_floats)
+        if allreduce([float(rc)], 2)[0] != 0.0:             # any rank failed (the outcome is collective)
+            p2p_state["error"] = f"enable_p2p rc={rc}: {L.ggml_hip_last_error().decode(errors='replace')}"
+            if comm_kind == "file":
+                raise SystemExit(f"[rank {rank}] file comm needs the P2P transport: {p2p_state['error']}")
+        else:
+            p2p_state["on"] = True
+    batch = not args.no_batch_siblings
+    groups = [[0, 1, 2], [3], [4, 5], [6]] if batch else [[i] for i in range(len(LAYER))]
+    line = sharded_decode(gh, L, comm, comm_kind, rank, world, LAYER, args.layers, groups, args, stream, allreduce,
+                          barrier, p2p_state, 0x5EED0000)
+    tok_s, ms = line["tok_s"], line["ms_per_step"]
+    result = {
+        "metric": METRIC, "value": tok_s, "unit": "tok/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "q4_0 x q8_0 (int8 dot, f32 acc)",
+        "data": "synthetic: W ~ N(0, 1/sqrt(K)) -> q4_0 (ggml A3 rule, on device), x ~ N(0,1); random-init, no checkpoint",
+        "config": {"workload": "LLaMA-7B q4_0 decode, 32 layers x 7 mul_mats (wq,wk,wv,wo 4096x4096; w1,w3 "
+                               "4096->11008; w2 11008->4096), N=1, q8_0 quantize of x included, lm_head excluded",
+                   "layers": args.layers, "weights_bytes_per_rank": line["weights_bytes_per_rank"],
+                   "graph": True, "launches_per_layer": len(groups), "comm": comm_kind,
+                   "sibling_batching": ("wq|wk|wv and w1|w3 share src1 -> one launch + one grouped all-gather each"
+                                        if batch else "off"),
+                   "collectives_per_layer": len(groups),
+                   "parallelism": f"row-split x{world} + {line['transport']} all-gather",
+                   "transport": line["transport"], "transports": line["transports"],
+                   "compute_only_tok_s": line["compute_only_tok_s"], "split_check": line["split_check"],
+                   "self_launched": os.environ.get("GGML_HIP_BENCH_SELF_LAUNCHED") == "1"},
+    }
+    if "rccl" in line["transports"]:
+        r = line["transports"]["rccl"]
+        result["config"]["collective_us_per_token"] = r.get("collective_us_per_token")
+    if "p2p" in line["transports"]:
+        result["config"]["p2p_transport"] = line["transports"]["p2p"]
+    if p2p_state["error"]:
+        result["config"]["p2p_transport"] = {"error": p2p_state["error"]}
+    if args.config4_layers > 0 and world > 1:
+        c4 = sharded_decode(gh, L, comm, comm_kind, rank, world, LLAMA13B, args.config4_layers, groups, args, stream,
+                            allreduce, barrier, p2p_state, 0x5EEF0000, tokens_per=40)
+        result["config4_llama13b_sharded"] = dict(
+            {"config": f"LLaMA-13B q4_0 decode, weight rows sharded {world}-way + all-gather over xGMI (BASELINE "
+                       "config 4): 40 layers x 7 mul_mats (5120x5120 x4, 5120->13824 x2, 13824->5120), 4 grouped "
+                       "all-gathers per layer", "layers": args.config4_layers}, **c4)
+    result["config"]["runtime_libs"] = gh.mapped_runtime_libs()
+    return result
+
+
+def sharded_decode(gh, L, comm, comm_kind, rank, world, spec, n_layers, groups, args, stream, allreduce, barrier,
+                   p2p_state, seed_base, tokens_per=32):
+    """One model's row-sharded decode: the split graph on each available transport (RCCL, P2P), the same
+    shards without collectives (compute only), and the bitwise split self-check.  tok/s per full model
+    (`tokens_per` layers), max over ranks of the timed region."""
+    stack = Stack(gh, L, rank, world, n_layers, seed_base=seed_base, spec=spec)
+    Ks = sorted({K for _, K, _ in spec})
+    xs = {}
+    for K in Ks:
+        xs[K] = gh.DeviceBuffer(K * 4)
+        gh.check(L.ggml_hip_fill_gaussian(xs[K].ptr, K, 0x5EED1000 + K, 0.0, 1.0, None))
+    yb = {i: gh.DeviceBuffer(max(spec[i][2] // world + 1, 1) * 4 + 64) for i in range(len(spec))}
+    ysplit = {i: gh.DeviceBuffer(spec[i][2] * 4) for i in range(len(spec))}     # full-M gathered outputs
+    gh.synchronize()
+    keep = []
+
+    def build(use_comm):
+        out = []
+        for row in stack.mats:
+            for g in groups:
+                n = len(g)
+                K = row[g[0]][1]
+                if not use_comm:
+                    wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
+                    yp = (ctypes.c_void_p * n)(*[yb[i].ptr for i in g])
+                    mp = (ctypes.c_int64 * n)(*[row[i][3] for i in g])
+                    keep.append((wp, yp, mp))
+                    out.append(("multi", (n, wp, mp, K, yp)))
+                else:                # split siblings: one GEMV launch + one grouped all-gather
+                    wp = (ctypes.c_void_p * n)(*[row[i][4].ptr for i in g])
+                    mt = (ctypes.c_int64 * n)(*[row[i][2] for i in g])
+                    rp = (ctypes.c_void_p * n)(*[row[i][5].ctypes.data for i in g])
+                    yp = (ctypes.c_void_p * n)(*[ysplit[i].ptr for i in g])
+                    keep.append((wp, mt, rp, yp))
+                    out.append(("split_multi", (n, wp, mt, rp, K, yp)))
+        return out
+
+    split_args, local_args = build(True), build(False)
+
+    def step(launch_args):
+        for kind, a in launch_args:
+            if kind == "multi":
+                n, wp, mp, K, yp = a
+                gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, 1, yp, stream))
+            else:
+                n, wp, mt, rp, K, yp = a
+                gh.check(L.ggml_hip_mul_mat_q4_0_split_multi(comm, n, wp, mt, rp, K, xs[K].ptr, 1, yp, stream))
+
+    def timed_graph(launch_args):
+        step(launch_args)                    # outside capture first (workspaces, lazy init)
+        gh.check(L.ggml_hip_stream_synchronize(stream))
+        g = gh.Graph(stream)
+        with g:
+            step(launch_args)
         for _ in range(args.warmup):
-            g2.launch()
+            g.launch()
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            g2.launch()
+            g.launch()
         barrier()
-        el = time.perf_counter() - t0
-        el = allreduce([el], 1)[0]
-        result["config"]["compute_only_tok_s"] = round(args.steps / el * 32 / args.layers, 2)
-        result["config"]["collective_us_per_token"] = round((elapsed - el) / args.steps * 1e6 * 32 / args.layers, 1)
+        el = allreduce([time.perf_counter() - t0], 1)[0]     # max over ranks
+        del g
+        return el
 
-    if comm is not None:
-        result["config"]["split_check"] = split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream)
-        if not all(result["config"]["split_check"][k] for k in ("own_rows_bitwise", "gather_checksum")):
-            log(f"[rank {rank}] SPLIT CHECK FAILED: {result['config']['split_check']}")
-        if world > 1 and not args.no_p2p:
-            p2p = p2p_decode(gh, L, comm, decode_step, stack, ysplit, yb, rank, allreduce, barrier, stream, args,
-                             elapsed - el)
-            result["config"]["p2p_transport"] = p2p
-            chk = p2p.get("split_check", {})
-            # value = the faster transport whose run passed its own checks (bitwise own rows, gathered
-            # checksum, no peer-wait timeouts); the RCCL figures stay in the line either way
-            if (p2p.get("status_ok") and chk.get("own_rows_bitwise") and chk.get("gather_checksum")
-                    and p2p.get("tok_s", 0.0) > tok_s):
-                result["config"]["rccl_tok_s"] = result["value"]
-                result["config"]["rccl_ms_per_step"] = result["ms_per_step"]
-                result["value"] = p2p["tok_s"]
-                result["ms_per_step"] = p2p["ms_per_step"]
-                result["config"]["parallelism"] = (f"row-split x{world} + direct-store P2P all-gather over xGMI "
-                                                   "(faster than RCCL here, self-checks passed)")
-    result["config"]["runtime_libs"] = gh.mapped_runtime_libs()
-
-    if rank == 0 and world == 1 and comm is None:
-        result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
-        if not args.no_prefill and args.prefill_tokens > 0:
-            result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens,
-                                              groups=[tuple(g) for g in groups])
-        if not args.no_exact:
-            result["exact_mode"] = exact_decode(gh, L, decode_step, stream, args)
-        if not args.no_extra:
-            result["other_configs"] = [extra_decode(gh, L, stream, *c, steps=args.steps, warmup=args.warmup)
-                                       for c in EXTRA_CONFIGS]
-        if not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if comm is not None:
-        L.ggml_hip_comm_destroy(comm)
+    el_local = timed_graph(local_args)
+    tokens = tokens_per / n_layers
+    out = {"weights_bytes_per_rank": stack.total_bytes,
+           "compute_only_tok_s": round(args.steps / el_local * tokens, 2), "transports": {}}
+    runs = []
+    if comm_kind == "rccl":
+        gh.check(L.ggml_hip_comm_set_transport(comm, 0))
+        el = timed_graph(split_args)
+        chk = split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream)
+        out["transports"]["rccl"] = {"tok_s": round(args.steps / el * tokens, 2),
+                                     "ms_per_step": round(el / args.steps * 1e3, 4), "split_check": chk,
+                                     "collective_us_per_token": round((el - el_local) / args.steps * 1e6 * tokens, 1)}
+        runs.append(("rccl", el, chk, True))
+    if p2p_state["on"]:
+        gh.check(L.ggml_hip_comm_set_transport(comm, 1))
+        try:
+            # one eager step first: a transport that cannot run here (IPC, peer access) is reported, not timed;
+            # a peer wait that times out fails the comm for good and the next split call raises, but every
+            # rank still reaches the allreduce below (the waits are time-bounded)
+            try:
+                step(split_args)
+                local_ok = True
+            except gh.GgmlHipError as e:
+                log(f"[rank {rank}] P2P step failed: {e}")
+                local_ok = False
+            gh.check(L.ggml_hip_device_synchronize(), "device synchronize")
+            st = L.ggml_hip_comm_p2p_status(comm)
+            if allreduce([float(st) if local_ok else 1.0], 1)[0] != 0.0:
+                out["transports"]["p2p"] = {"error": f"peer waits failed (status {st}, this rank's step "
+                                                     f"{'ok' if local_ok else 'failed'})"}
+                p2p_state["on"] = False
+            else:
+                el = timed_graph(split_args)
+                st = L.ggml_hip_comm_p2p_status(comm)
+                ok = allreduce([float(st)], 1)[0] == 0.0
+                chk = split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream)
+                out["transports"]["p2p"] = {"tok_s": round(args.steps / el * tokens, 2),
+                                            "ms_per_step": round(el / args.steps * 1e3, 4), "status_ok": ok,
+                                            "split_check": chk,
+                                            "collective_us_per_token": round((el - el_local) / args.steps * 1e6 * tokens, 1)}
+                runs.append(("p2p", el, chk, ok))
+        finally:
+            if comm_kind == "rccl":
+                L.ggml_hip_comm_set_transport(comm, 0)
+    # the faster transport whose run passed its own checks (bitwise own rows, gathered checksum, no
+    # peer-wait failure); every transport's figures stay in the line
+    good = [r for r in runs if r[3] and r[2]["own_rows_bitwise"] and r[2]["gather_checksum"]]
+    best = min(good or runs, key=lambda r: r[1]) if runs else None
+    if best is None:
+        raise SystemExit(f"[rank {rank}] no all-gather transport ran")
+    out["transport"] = {"rccl": "RCCL", "p2p": "direct-store P2P"}[best[0]]
+    out["tok_s"] = round(args.steps / best[1] * tokens, 2)
+    out["ms_per_step"] = round(best[1] / args.steps * 1e3, 4)
+    out["split_check"] = best[2]
+    out["self_checks_passed"] = bool(good)
+    stack.free()
+    return out
 
 
 # ---------------------------------------------------------------------------------------------
@@ -368,57 +576,10 @@ def _bits_checksum(a, offset):
     return int(np.sum((u + np.uint64(1)) * (pos * np.uint64(2654435761) + np.uint64(97)), dtype=np.uint64))
 
 
-def p2p_decode(gh, L, comm, decode_step, stack, ysplit, yb, rank, allreduce, barrier, stream, args, rccl_coll_s):
-    """The same row-sharded decode with the all-gathers done by direct stores into the peers' landing
-    buffers over xGMI (ggml_hip_comm_enable_p2p, p2p_gather.hip) instead of ncclAllGather: tok/s and
-    the collective cost per token next to RCCL's, plus the bitwise split check.  One eager step and a
-    status check first: a transport that cannot run here (IPC, peer access) is reported, not timed."""
-    max_floats = max(M for row in stack.mats for _, K, M, m, buf, rb in row)
-    rc = L.ggml_hip_comm_enable_p2p(comm, max_floats)
-    if allreduce([float(rc)], 2)[0] != 0.0:              # any rank failed
-        L.ggml_hip_comm_set_transport(comm, 0)
-        return {"error": f"enable_p2p rc={rc}: {L.ggml_hip_last_error().decode(errors='replace')}"}
-    try:
-        # a peer wait that times out fails the comm for good and the next split call returns
-        # GGML_HIP_ERR_COMM (raised by gh.check): every rank still reaches the allreduce below, so the ranks
-        # agree on the failure instead of leaving the others in a collective (the waits are time-bounded)
-        try:
-            decode_step()
-            local_ok = True
-        except gh.GgmlHipError as e:
-            log(f"[rank {rank}] P2P step failed: {e}")
-            local_ok = False
-        gh.check(L.ggml_hip_device_synchronize(), "device synchronize")
-        st = L.ggml_hip_comm_p2p_status(comm)
-        if allreduce([float(st) if local_ok else 1.0], 1)[0] != 0.0:
-            return {"error": f"peer waits timed out (status {st}, this rank's step {'ok' if local_ok else 'failed'})"}
-        g = gh.Graph(stream)
-        with g:
-            decode_step()
-        for _ in range(args.warmup):
-            g.launch()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            g.launch()
-        barrier()
-        el = allreduce([time.perf_counter() - t0], 1)[0]
-        st = L.ggml_hip_comm_p2p_status(comm)
-        ok = allreduce([float(st)], 1)[0] == 0.0
-        chk = split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream)
-        tok = args.steps / el * 32 / args.layers
-        return {"tok_s": round(tok, 2), "ms_per_step": round(el / args.steps * 1e3, 4), "status_ok": ok,
-                "split_check": chk,
-                "rccl_collective_us_per_token": round(rccl_coll_s / args.steps * 1e6 * 32 / args.layers, 1),
-                "note": "collective cost = this line's time minus the compute-only graph's (config)"}
-    finally:
-        L.ggml_hip_comm_set_transport(comm, 0)
-
-
 def split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream):
-    """Self-check of the sharded run (after the timed region): the decode step leaves the last
-    layer's gathered outputs in ysplit and the local-only graph its slices in yb.  (1) this rank's
-    rows of every gathered y equal its own slice bitwise; (2) the exact checksum of every gathered y
+    """Self-check of the sharded run (after its timed region): the split step leaves the last layer's
+    gathered outputs in ysplit and the local-only graph (run before it, same x) its slices in yb.  (1) this
+    rank's rows of every gathered y equal its own slice bitwise; (2) the exact checksum of every gathered y
     equals the sum over ranks of the slice checksums (every rank's slice landed at its rows)."""
     MOD = 1 << 44                            # sums of <= 256 ranks stay exact in a double
     row = stack.mats[-1]

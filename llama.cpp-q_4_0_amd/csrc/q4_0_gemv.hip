@@ -205,7 +205,20 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
     // count vmcnt exactly: the q8_0 math waits for the activations only, not the weights.
     const int total = NT * nb * 8;
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, (uint32_t)total * 16u);
+#ifndef GEMV_XKO
+#define GEMV_XKO 0          // diagnostic builds only (tools/build_variant.sh -DGEMV_XKO=n): x-prologue knockouts
+#endif
     auto quantize_into_lds = [&](const u32x4 &raw, int t) __attribute__((always_inline)) {
+#if GEMV_XKO >= 1           // 1: no quantize VALU (raw bits to LDS), 2: + a quarter of the x loads, 3: no x at all
+        if (t < total) {
+            xq[t] = raw.x ^ raw.w;
+            if ((t & 7) == 0) {
+                xd[t >> 3] = 1.0f;
+                xs[t >> 3] = 0;
+            }
+        }
+        return;
+#endif
         if (t < total) {                                            // whole 8-lane groups agree
             const float4 v = make_float4(__uint_as_float(raw.x), __uint_as_float(raw.y),
                                          __uint_as_float(raw.z), __uint_as_float(raw.w));
@@ -379,7 +392,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
     } else {
         // x-waves: wave < XW load + quantize x (XT threads, PRO float4 each per round), then issue
         // their weight loads; the other waves only issue weight loads
-        const int XW0 = (total + 64 * GEMV_XPRO - 1) / (64 * GEMV_XPRO);
+        const int xtot = GEMV_XKO == 2 ? total / 4 : GEMV_XKO == 3 ? 0 : total;
+        const int XW0 = (xtot + 64 * GEMV_XPRO - 1) / (64 * GEMV_XPRO);
         const int XW = XW0 < WAVES ? XW0 : WAVES;
         const int XT = XW * 64;
         if constexpr (XFIRST) {
@@ -398,7 +412,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             if (wave < XW) {
 #pragma unroll
                 for (int i = 0; i < GEMV_XPRO; i++) quantize_into_lds(xw[i], tid + i * XT);
-                for (int base = GEMV_XPRO * XT; base < total; base += GEMV_XPRO * XT) {
+                for (int base = GEMV_XPRO * XT; base < xtot; base += GEMV_XPRO * XT) {
 #pragma unroll
                     for (int i = 0; i < GEMV_XPRO; i++)
                         xw[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * XT), 0, 0);
@@ -415,7 +429,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             }
         } else if (wave < XW) {
             u32x4 xw[GEMV_XPRO];
-            for (int base = 0; base < total; base += GEMV_XPRO * XT) {
+            for (int base = 0; base < xtot; base += GEMV_XPRO * XT) {
 #pragma unroll
                 for (int i = 0; i < GEMV_XPRO; i++)
                     xw[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (base + tid + i * XT), 0, 0);

@@ -871,6 +871,15 @@ int ggml_hip_debug_graph_stats(long long *out, int clear) {
     return GGML_HIP_OK;
 }
 
+// not in the public header: host cost of eager launches: out[0] launches, out[1] ns inside hipLaunchKernel;
+// enable 1 starts counting (and resets), 0 stops, -1 only reads
+int ggml_hip_debug_launch_stats(long long *out, int enable) {
+    flush_deferred();
+    ghip::launch_prof_read(&out[0], &out[1], enable == 1);
+    if (enable >= 0) ghip::g_launch_prof = enable != 0;
+    return GGML_HIP_OK;
+}
+
 // not in the public header: the decode norm chain folded into the GEMV prologue on (1) / off (0)
 int ggml_hip_debug_set_norm_fold(int on) {
     flush_deferred();

@@ -434,6 +434,21 @@ void rec_stats(long long *runs, long long *kernels, long long *updated, long lon
     *built = r.built;
 }
 
+bool g_launch_prof = false;
+static std::atomic<long long> g_lp_count{0}, g_lp_ns{0};
+long long launch_prof_now() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void launch_prof_add(long long ns) {
+    g_lp_count.fetch_add(1, std::memory_order_relaxed);
+    g_lp_ns.fetch_add(ns, std::memory_order_relaxed);
+}
+void launch_prof_read(long long *count, long long *ns, bool reset) {
+    *count = g_lp_count.load();
+    *ns = g_lp_ns.load();
+    if (reset) g_lp_count.store(0), g_lp_ns.store(0);
+}
+
 void rec_clear_cache() {
     REC_LOCK;
     Recorder &r = rec();

@@ -42,12 +42,23 @@ void rec_set_mode(int mode);
 void rec_stats(long long *runs, long long *kernels, long long *updated, long long *built, long long *submit_ns);
 // submits what is pending and destroys every cached graph
 void rec_clear_cache();
+// host-cost profile of eager launches (ggml_hip_debug_launch_stats): count and ns inside hipLaunchKernel
+extern bool g_launch_prof;
+void launch_prof_add(long long ns);
+long long launch_prof_now();
+void launch_prof_read(long long *count, long long *ns, bool reset);
 
 template <typename... P, typename... A>
 inline void launch_k(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t s, A &&...a) {
     static_assert(sizeof...(P) == sizeof...(A), "launch_k: argument count");
     if (!rec_active(s)) {
         if (rec_pending()) rec_flush_at("eager launch");   // never overtakes recorded launches
+        if (__builtin_expect(g_launch_prof, 0)) {
+            const long long t0 = launch_prof_now();
+            hipLaunchKernelGGL(k, grid, block, lds, s, std::forward<A>(a)...);
+            launch_prof_add(launch_prof_now() - t0);
+            return;
+        }
         hipLaunchKernelGGL(k, grid, block, lds, s, std::forward<A>(a)...);
         return;
     }

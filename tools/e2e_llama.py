@@ -29,6 +29,9 @@ sys.path[:0] = [os.path.join(ROOT, "llama.cpp-q_4_0_amd", "python")]
 CPU_LIB = os.path.join(ROOT, "oracle", "_ref", "libllama_ref_cpu.so")
 HIP_LIB = os.path.join(ROOT, "oracle", "_ref", "libllama_ref_hip.so")
 HP7B = dict(n_vocab=32000, n_embd=4096, n_mult=256, n_head=32, n_layer=32, n_rot=128, ftype=2)
+# the same graph (32 layers, 1,187 nodes per decode eval, head dim 128) with little device work: the host
+# walk of the hook path measured on its own (--shape host)
+HPHOST = dict(n_vocab=32000, n_embd=512, n_mult=256, n_head=4, n_layer=32, n_rot=128, ftype=2)
 
 
 def n_ff(hp):
@@ -112,16 +115,18 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--modes", default="fast,exact")
     ap.add_argument("--out", default="")
+    ap.add_argument("--shape", choices=("7b", "host"), default="7b")
     args = ap.parse_args()
+    hp = HP7B if args.shape == "7b" else HPHOST
     import ggml_hip as gh
     L = gh.load()
     d = tempfile.mkdtemp(prefix="e2e7b_", dir=os.environ.get("E2E_DIR", "/tmp"))
     model = os.path.join(d, "llama7b-q4_0-synthetic.ggjt")
     t0 = time.time()
-    size = write_model(model, HP7B)
+    size = write_model(model, hp)
     print(f"model {size / 1e9:.2f} GB written in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
-    nv = HP7B["n_vocab"]
-    res = {"model": "LLaMA-7B shape, GGJT v3 q4_0, random valid blocks (synthetic)", "model_bytes": size,
+    nv = hp["n_vocab"]
+    res = {"model": ("LLaMA-7B shape" if args.shape == "7b" else f"host-walk shape {hp}") + ", GGJT v3 q4_0, random valid blocks (synthetic)", "model_bytes": size,
            "caller": "reference llama.cpp + ggml.c (oracle/_ref builds, unmodified sources)",
            "n_ctx": max(512, -(-(args.prompt + args.decode) // 512) * 512)}
     try:
@@ -139,8 +144,14 @@ def main():
             L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
             st = np.zeros(69 + 68, np.int64)
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
+            L.ggml_hip_debug_launch_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            ls = np.zeros(2, np.int64)
+            L.ggml_hip_debug_launch_stats(ls.ctypes.data, 1)
             r, lg = bench(HIP_LIB, model, args.prompt, args.decode, args.threads_gpu, 99, 3, nv)
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
+            L.ggml_hip_debug_launch_stats(ls.ctypes.data, 0)
+            r["eager_launches_per_eval"] = round(float(ls[0]) / (3 + args.decode), 1)
+            r["eager_launch_host_ms_per_eval"] = round(float(ls[1]) / 1e6 / (3 + args.decode), 3)
             ntok = 3 * args.prompt + args.decode      # evals: 3 prompt reps + decode steps
             r["backend_nodes_per_eval"] = round(float(st[:68].sum()) / (3 + args.decode), 1)
             r["backend_host_ms_per_eval"] = round(float(st[68]) / 1e6 / (3 + args.decode), 3)

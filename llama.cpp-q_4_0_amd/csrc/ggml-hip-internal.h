@@ -176,8 +176,10 @@ void wcache_note_host_write(const void *data, size_t bytes);
 
 // ---- device ops (ggml-hip-ops.cpp)
 struct OpTables {
-    uint16_t *silu = nullptr;                // table_silu_f16 (ggml.c:4252)
-    uint16_t *exp = nullptr;                 // table_exp_f16  (ggml.c:4253)
+    uint16_t *silu = nullptr;                // table_silu_f16 (ggml.c:4252), as the kernels get it (lut_apply)
+    uint16_t *exp = nullptr;                 // table_exp_f16  (ggml.c:4253), the same
+    uint16_t *silu_raw = nullptr, *exp_raw = nullptr;   // the device tables
+    int silu_bad = -1, exp_bad = -1;         // finite inputs where the direct evaluation differs (device check)
 };
 const OpTables &op_tables(int id, hipStream_t s);
 const float *rope_table(int id, int64_t ne0, int n_dims, int64_t need_pos, hipStream_t s);

@@ -23,13 +23,32 @@ float f16_bits_to_f32(uint16_t b) {
 
 std::mutex g_tab_mu;
 OpTables g_tabs[GGML_HIP_MAX_DEVICES];
+// direct evaluation of the tables' values in the kernels (q4_0_device.h lut_silu / lut_exp) where the device
+// reproduces every finite entry bit for bit; GGML_HIP_LUT_DIRECT=0 or ggml_hip_debug_set_lut_direct(0) keeps
+// the gathers
+std::atomic<int> g_lut_direct{-1};
+bool lut_direct_enabled() {
+    int v = g_lut_direct.load(std::memory_order_relaxed);
+    if (v < 0) {
+        v = (!getenv("GGML_HIP_LUT_DIRECT") || atoi(getenv("GGML_HIP_LUT_DIRECT")) != 0) ? 1 : 0;
+        g_lut_direct.store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+// the pointers the kernels get: the tables, tagged with bit 0 when they may evaluate directly
+void lut_apply(OpTables &t) {
+    auto tag = [](uint16_t *p, bool on) { return (uint16_t *)((uintptr_t)p | (on ? 1u : 0u)); };
+    const bool on = lut_direct_enabled();
+    t.silu = tag(t.silu_raw, on && t.silu_bad == 0);
+    t.exp = tag(t.exp_raw, on && t.exp_bad == 0);
+}
 
 // ggml_init builds them as fp16(silu(f)) and fp16(expf(f)) for every fp16 bit pattern f with the
 // host libm (ggml.c:4246-4254); the same formula with the same libm gives the same 2 x 64 K entries
 const OpTables &op_tables(int id, hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_tab_mu);
     OpTables &t = g_tabs[id];
-    if (!t.silu) {
+    if (!t.silu_raw) {
         std::vector<uint16_t> silu(65536), ex(65536);
 #pragma clang loop vectorize(disable)
         for (int i = 0; i < 65536; i++) {
@@ -37,12 +56,24 @@ const OpTables &op_tables(int id, hipStream_t s) {
             silu[i] = f32_to_f16_bits(f / (1.0f + expf(-f)));
             ex[i] = f32_to_f16_bits(expf(f));
         }
-        HIP_FATAL(hipMalloc(&t.silu, 2 * 65536 * sizeof(uint16_t)));
-        t.exp = t.silu + 65536;
-        HIP_FATAL(GHIP_SYNC(hipMemcpyAsync)(t.silu, silu.data(), 65536 * 2, hipMemcpyHostToDevice, s));
-        HIP_FATAL(GHIP_SYNC(hipMemcpyAsync)(t.exp, ex.data(), 65536 * 2, hipMemcpyHostToDevice, s));
+        HIP_FATAL(hipMalloc(&t.silu_raw, 2 * 65536 * sizeof(uint16_t) + 2 * sizeof(int)));
+        t.exp_raw = t.silu_raw + 65536;
+        int *bad = (int *)(t.exp_raw + 65536);
+        HIP_FATAL(GHIP_SYNC(hipMemcpyAsync)(t.silu_raw, silu.data(), 65536 * 2, hipMemcpyHostToDevice, s));
+        HIP_FATAL(GHIP_SYNC(hipMemcpyAsync)(t.exp_raw, ex.data(), 65536 * 2, hipMemcpyHostToDevice, s));
+        HIP_FATAL(GHIP_SYNC(hipMemsetAsync)(bad, 0, 2 * sizeof(int), s));
+        // the kernels' direct evaluation against every finite entry, once per device
+        HIP_FATAL(ghip::op_lut_check(t.silu_raw, t.exp_raw, bad, s));
+        int hb[2] = {-1, -1};
+        HIP_FATAL(GHIP_SYNC(hipMemcpyAsync)(hb, bad, sizeof hb, hipMemcpyDeviceToHost, s));
         HIP_FATAL(GHIP_SYNC(hipStreamSynchronize)(s));
+        t.silu_bad = hb[0];
+        t.exp_bad = hb[1];
+        if ((hb[0] || hb[1]) && getenv("GGML_HIP_VERBOSE"))
+            fprintf(stderr, "ggml-hip: direct silu / exp differ from the host tables at %d / %d inputs: gathers kept\n",
+                    hb[0], hb[1]);
     }
+    lut_apply(t);
     return t;
 }
 
@@ -315,6 +346,25 @@ void run_device_op(tensor *t, const tensor *fused_cpy) {
 }  // namespace ghh
 
 extern "C" {
+
+// not in the public header: the fp16-table ops' direct evaluation (out[0] silu mode, [1] silu mismatches of the
+// device check, [2] exp mode, [3] exp mismatches; mode 1 = direct, 0 = table gathers); on: 1 / 0 sets the
+// switch, -1 only reads (device 0's tables, built on first use)
+int ggml_hip_debug_lut_direct(int on, int *out) {
+    ensure_init();
+    if (g_device_count == 0) return GGML_HIP_ERR_UNSUPPORTED;
+    flush_deferred();
+    if (on >= 0) g_lut_direct.store(on ? 1 : 0, std::memory_order_relaxed);
+    HIP_FATAL(hipSetDevice(g_main_device));
+    const OpTables &t = op_tables(g_main_device, g_dev[g_main_device].stream);
+    if (out) {
+        out[0] = ((uintptr_t)t.silu & 1) ? 1 : 0;
+        out[1] = t.silu_bad;
+        out[2] = ((uintptr_t)t.exp & 1) ? 1 : 0;
+        out[3] = t.exp_bad;
+    }
+    return GGML_HIP_OK;
+}
 
 // not in the public header: nodes taken by ggml_hip_compute_forward per ggml op (counts[op], op < n);
 // reset when reset != 0 (tests check which ops of a full-offload graph ran on the device)

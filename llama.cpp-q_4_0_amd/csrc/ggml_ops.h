@@ -77,6 +77,9 @@ hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *
                           const uint16_t *table, int64_t nkv, int64_t nhead, const void *vs, int64_t nb01v, int64_t nb02v,
                           int64_t nout, float *kqv, float *merged, hipStream_t s);
 // u = silu(a) -> out = u * b (same shape)
+// mismatches of the direct silu / exp evaluation against the host tables over every finite fp16 input
+// (bad_dev: two zeroed ints on the device; q4_0_device.h lut_silu / lut_exp)
+hipError_t op_lut_check(const uint16_t *silu, const uint16_t *ex, int *bad_dev, hipStream_t s);
 hipError_t op_silu_mul_f32(const float *a, const float *b, float *u, float *out, int64_t n, const uint16_t *table,
                            hipStream_t s);
 // The same chains with the k_gemm9 x image of out written beside it into xws (codes [nb][3][Np][16 B] +

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(TPB) void k_mul_f32(const float *a, const float *b,
 
 __global__ __launch_bounds__(TPB) void k_silu_f32(const float *x, float *d, int64_t n, const uint16_t *table) {
     const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (i < n) d[i] = h2f_bits(table[f2h_bits(x[i])]);
+    if (i < n) d[i] = h2f_bits(lut_silu(table, f2h_bits(x[i])));
 }
 
 __global__ __launch_bounds__(TPB) void k_scale_f32(const float *x, float *d, float v, int64_t n) {
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(TPB) void k_soft_max_f32(const float *x, float *d, 
         const float v = xr[i];
         float e = 0.0f;
         if (v != -INFINITY) {
-            e = h2f_bits(table[f2h_bits(v - mx)]);
+            e = h2f_bits(lut_exp(table, f2h_bits(v - mx)));
             s += (double)e;
         }
         dr[i] = e;
@@ -615,7 +615,7 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max(const float *x, flo
         if (masked) masked[o + i] = m;
         float e = 0.0f;
         if (m != -INFINITY) {
-            e = h2f_bits(table[f2h_bits(m - mx)]);
+            e = h2f_bits(lut_exp(table, f2h_bits(m - mx)));
             s += (double)e;
         }
         d[o + i] = e;
@@ -660,7 +660,7 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max_reg(const float *x,
     mx = wave_max_f(mx);
     uint16_t tv[NV];
 #pragma unroll
-    for (int k = 0; k < NV; k++) tv[k] = table[f2h_bits(m[k] - mx)];   // -inf - mx: a valid index, unused
+    for (int k = 0; k < NV; k++) tv[k] = lut_exp(table, f2h_bits(m[k] - mx));   // -inf - mx: a valid index, unused
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < NV; k++) {
@@ -726,7 +726,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
         const float m = i > n_past ? -INFINITY : sv;
         float e = 0.0f;
         if (m != -INFINITY) {
-            e = h2f_bits(table[f2h_bits(m - mx)]);
+            e = h2f_bits(lut_exp(table, f2h_bits(m - mx)));
             ssum += (double)e;
         }
         row[i] = e;
@@ -989,7 +989,7 @@ __global__ __launch_bounds__(TPB) void k_silu_mul(const float *a, const float *b
                                                   const uint16_t *table) {
     const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
     if (i >= n) return;
-    const float s = h2f_bits(table[f2h_bits(a[i])]);
+    const float s = h2f_bits(lut_silu(table, f2h_bits(a[i])));
     if (u) u[i] = s;
     out[i] = s * b[i];
 }
@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(TPB) void k_silu_mul_x9(const float *a, const float
         // the four table indices first, then the four lookups back to back (interleaved with the
         // conversions they were issued and waited for one at a time)
         const uint16_t h0 = f2h_bits(av.x), h1 = f2h_bits(av.y), h2 = f2h_bits(av.z), h3 = f2h_bits(av.w);
-        const uint16_t t0 = table[h0], t1 = table[h1], t2 = table[h2], t3 = table[h3];
+        const uint16_t t0 = lut_silu(table, h0), t1 = lut_silu(table, h1), t2 = lut_silu(table, h2), t3 = lut_silu(table, h3);
         const float4 sv = make_float4(h2f_bits(t0), h2f_bits(t1), h2f_bits(t2), h2f_bits(t3));
         if (u) reinterpret_cast<float4 *>(u)[i4] = sv;
         r = make_float4(sv.x * bv.x, sv.y * bv.y, sv.z * bv.z, sv.w * bv.w);
@@ -1097,6 +1097,20 @@ hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *
     const int splits = (int)((nout + SM_OUT - 1) / SM_OUT);
     launch_k(k_softmax_kqv, dim3((unsigned)(nhead * splits)), dim3(SM_THREADS), (size_t)nkv * 4, s, kq, scaled,
                        masked, sm, v, n_past, table, nkv, (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged);
+    return hipGetLastError();
+}
+
+// every finite fp16 input: the direct evaluation against the host-built table (bad[0] silu, bad[1] exp)
+__global__ __launch_bounds__(TPB) void k_lut_check(const uint16_t *silu, const uint16_t *ex, int *bad) {
+    const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= 65536u || (i & 0x7C00u) == 0x7C00u) return;
+    if (silu_direct(i) != silu[i]) atomicAdd(bad, 1);
+    if (exp_direct(i) != ex[i]) atomicAdd(bad + 1, 1);
+}
+
+hipError_t op_lut_check(const uint16_t *silu, const uint16_t *ex, int *bad_dev, hipStream_t s) {
+    (void)hipGetLastError();
+    launch_k(k_lut_check, dim3(65536 / TPB), dim3(TPB), 0, s, silu, ex, bad_dev);
     return hipGetLastError();
 }
 

@@ -717,24 +717,34 @@ struct G9Mats {
     int M[4];
     int tb[5];
     int n, ny, xcd;
+    int nfull;                  // tiles [0, nfull) run whole; each later tile runs as two 64-row halves
 };
 
+// HALF: the workgroup computes rows [64 hsel, 64 hsel + 64) of its 128-row tile, one 32 x 32 tile per compute
+// wave (the same per-output arithmetic: bitwise the whole tile's values for those rows).  Tile order: see
+// G9Mats; the HALF instantiation runs the tiles from mats.nfull on, two workgroups per tile (gemm9_run_multi:
+// the last partial round of a multi-round launch, e.g. LLaMA-7B w1|w3 at N = 512 = 5 rounds of 256 + 96).
+// (One kernel with both forms behind a workgroup-uniform branch spilled 200 bytes: two instantiations.)
+template <bool HALF>
 __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats, int nb,
                                                                const uint8_t *__restrict__ ximg,
                                                                const uint16_t *__restrict__ xd16, int64_t Np, int N) {
+    const int Mt = mats.tb[mats.n];
+    int j = (int)blockIdx.x, hsel = 0;
+    if constexpr (HALF) {
+        hsel = j & 1;
+        j = mats.nfull + (j >> 1);
+    } else if (mats.xcd) {
+        const int C = (int)gridDim.x >> 3;
+        if (j < 8 * C) j = (j & 7) * C + (j >> 3);
+    }
+    const int rtg = mats.xcd ? j / mats.ny : j % Mt, ty = mats.xcd ? j - rtg * mats.ny : j / Mt;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *zero = smem + G9_NS * G9_STAGE;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 31, h = lane >> 5;
-    const int G = (int)gridDim.x, Mt = mats.tb[mats.n];
-    int j = (int)blockIdx.x;
-    if (mats.xcd) {
-        const int C = G >> 3;
-        if (j < 8 * C) j = (j & 7) * C + (j >> 3);
-    }
-    const int rtg = mats.xcd ? j / mats.ny : j % Mt, ty = mats.xcd ? j - rtg * mats.ny : j / Mt;
     // matrix of row tile rtg (selects, no dynamic kernarg indexing)
     const int mi = (mats.n > 1 && rtg >= mats.tb[1]) + (mats.n > 2 && rtg >= mats.tb[2]) + (mats.n > 3 && rtg >= mats.tb[3]);
     const uint8_t *wimg = mi == 0 ? mats.wimg[0] : mi == 1 ? mats.wimg[1] : mi == 2 ? mats.wimg[2] : mats.wimg[3];
@@ -783,7 +793,8 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
     };
     const int g = (wave >> 2) & 1, q = wave & 3;
     const int tt = 32 * (q & 1) + c;                       // this lane's token (A operand row) in the tile
-    const int r0 = 64 * (q >> 1) + c, r1 = r0 + 32;        // this lane's weight rows (B operand columns)
+    const int r0 = HALF ? 64 * hsel + 32 * (q >> 1) + c : 64 * (q >> 1) + c;   // this lane's weight rows
+    const int r1 = r0 + 32;                                                   // (B operand columns)
     const int xo16 = h * 1024 + tt * 16, xo8 = 2048 + tt * 16 + 8 * (h ^ ((tt >> 4) & 1));
     const int sa = h ? G9_SCALE_1 : G9_SCALE_5;
     const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -813,12 +824,12 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
         // the previous block's epilogues, then this block's four MFMAs back to back: the two fp6 MFMAs,
         // then the two fp16 ones (two format switches per burst, not four)
         epi(acc0, S0, P0);
-        epi(acc1, S1, P1);
+        if constexpr (!HALF) epi(acc1, S1, P1);
         __builtin_amdgcn_sched_barrier(0);
         S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw0, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
-        S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw1, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+        if constexpr (!HALF) S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw1, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
         P0 = scale_rank1(as, bs0);
-        P1 = scale_rank1(as, bs1);
+        if constexpr (!HALF) P1 = scale_rank1(as, bs1);
         __builtin_amdgcn_sched_barrier(0);
     };
     auto sync = [&]() __attribute__((always_inline)) {
@@ -849,7 +860,8 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
                 Ops o;
                 o.ax = rd24(smem + xa + j * G9_XB, smem + xb8 + j * G9_XB);
                 o.bw0 = rd24(smem + wa0 + j * G9_WB, smem + w80 + j * G9_WB);
-                o.bw1 = rd24(smem + wa1 + j * G9_WB, smem + w81 + j * G9_WB);
+                if constexpr (HALF) o.bw1 = o.bw0;
+                else o.bw1 = rd24(smem + wa1 + j * G9_WB, smem + w81 + j * G9_WB);
                 o.sw0 = *reinterpret_cast<const uint16_t *>(smem + da + j * 256);
                 o.sw1 = *reinterpret_cast<const uint16_t *>(smem + da + j * 256 + 64);
                 o.sx = *reinterpret_cast<const uint16_t *>(smem + xd + j * 128);
@@ -864,7 +876,7 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
         sync();
     }
     epi(acc0, S0, P0);
-    epi(acc1, S1, P1);
+    if constexpr (!HALF) epi(acc1, S1, P1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     float *red = reinterpret_cast<float *>(smem);
@@ -872,7 +884,8 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
 #pragma unroll
         for (int i = 0; i < 16; i += 4) {
             *reinterpret_cast<float4 *>(red + ((i / 4) * 256 + q * 64 + lane) * 4) = {acc0[i], acc0[i + 1], acc0[i + 2], acc0[i + 3]};
-            *reinterpret_cast<float4 *>(red + ((4 + i / 4) * 256 + q * 64 + lane) * 4) = {acc1[i], acc1[i + 1], acc1[i + 2], acc1[i + 3]};
+            if constexpr (!HALF)
+                *reinterpret_cast<float4 *>(red + ((4 + i / 4) * 256 + q * 64 + lane) * 4) = {acc1[i], acc1[i + 1], acc1[i + 2], acc1[i + 3]};
         }
     }
     __syncthreads();
@@ -880,9 +893,11 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
 #pragma unroll
         for (int i = 0; i < 16; i += 4) {
             const float4 o0 = *reinterpret_cast<const float4 *>(red + ((i / 4) * 256 + q * 64 + lane) * 4);
-            const float4 o1 = *reinterpret_cast<const float4 *>(red + ((4 + i / 4) * 256 + q * 64 + lane) * 4);
             acc0[i] += o0.x; acc0[i + 1] += o0.y; acc0[i + 2] += o0.z; acc0[i + 3] += o0.w;
-            acc1[i] += o1.x; acc1[i + 1] += o1.y; acc1[i + 2] += o1.z; acc1[i + 3] += o1.w;
+            if constexpr (!HALF) {
+                const float4 o1 = *reinterpret_cast<const float4 *>(red + ((4 + i / 4) * 256 + q * 64 + lane) * 4);
+                acc1[i] += o1.x; acc1[i + 1] += o1.y; acc1[i + 2] += o1.z; acc1[i + 3] += o1.w;
+            }
         }
         const int row0 = m0 + r0, row1 = m0 + r1;
 #pragma unroll
@@ -890,11 +905,12 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
             const int tk = n0 + 32 * (q & 1) + (i & 3) + 8 * (i >> 2) + 4 * h;
             if (tk < N) {
                 if (row0 < M) y[(int64_t)tk * ldy + row0] = acc0[i];
-                if (row1 < M) y[(int64_t)tk * ldy + row1] = acc1[i];
+                if (!HALF && row1 < M) y[(int64_t)tk * ldy + row1] = acc1[i];
             }
         }
     }
 }
+
 
 int64_t gemm9_np(int64_t N) { return (N + 3) & ~(int64_t)3; }
 size_t gemm9_x_bytes(int64_t K, int64_t N) { return (size_t)(K / QK) * gemm9_np(N) * 50; }
@@ -954,17 +970,37 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     // GGML_HIP_GEMM9_XCD=0 restores the row-tile-fastest order (A/B)
     static const int xcd = env_int("GGML_HIP_GEMM9_XCD", 1);
     mats.xcd = xcd ? 1 : 0;
+    // a last partial round of at most half the CUs runs as twice as many 64-row half tiles, each about half
+    // a tile's time (one workgroup per CU: 154 KB of LDS); GGML_HIP_GEMM9_HALF=0 runs it whole
+    static const int half_on = env_int("GGML_HIP_GEMM9_HALF", 1);
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            cus = v;
+        if (cus <= 0) cus = 256;
+    }
+    const int64_t rem = tiles % cus;
+    const bool halves = half_on && tiles > cus && rem > 0 && 2 * rem <= cus;
+    mats.nfull = (int)(halves ? tiles - rem : tiles);
+    const int64_t grid = halves ? tiles + rem : tiles;
     const uint8_t *ximg = (const uint8_t *)xws;
     const uint16_t *xd16 = (const uint16_t *)((const char *)xws + (size_t)nb * Np * 48);
     if ((int64_t)nb * Np * 48 >= ((int64_t)1 << 31) || (int64_t)nb * G9_WB >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_gemm9_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
+        hipError_t e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
         if (e != hipSuccess) return e;
         attr = true;
     }
     (void)hipGetLastError();
-    launch_k(k_gemm9_q4_0, dim3((unsigned)tiles), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
+    if (mats.nfull > 0)
+        launch_k(k_gemm9_q4_0<false>, dim3((unsigned)mats.nfull), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
+    if (grid > mats.nfull)
+        launch_k(k_gemm9_q4_0<true>, dim3((unsigned)(grid - mats.nfull)), dim3(G9_THREADS), G9_LDS, s, mats, nb, ximg, xd16,
+                 Np, (int)N);
     return hipGetLastError();
 }
 

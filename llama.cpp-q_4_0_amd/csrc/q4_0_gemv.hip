@@ -276,7 +276,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
 #pragma unroll
                 for (int d = 0; d < DEPTH; d++) buf[d] = issue(d);
             }
-            typedef __attribute__((address_space(1))) const uint16_t g_u16;
             const bool store = blockIdx.x == 0;
 #pragma unroll
             for (int i = 0; i < GEMV_XPRO; i++) {
@@ -289,7 +288,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
 #pragma unroll
                     for (int c = 0; c < 4; c++) hi[c] = f2h(__uint_as_float(av[c]));
 #pragma unroll
-                    for (int c = 0; c < 4; c++) tv[c] = ((g_u16 *)nrm.table)[hi[c]];
+                    for (int c = 0; c < 4; c++) tv[c] = lut_silu(nrm.table, hi[c]);
 #pragma unroll
                     for (int c = 0; c < 4; c++) {    // as k_silu_mul: s = table[fp16(a)], out = s * b
                         u[c] = h2f(tv[c]);

@@ -45,6 +45,18 @@ bool x9_fold_enabled() {
     return v == 1;
 }
 
+// GGML_HIP_GEMV_EPI=0: the elementwise nodes held behind a decode q|k|v norm group (rope K -> K cache,
+// V -> V cache, rope Q) run as their own batched launch; on (default), in the GEMV's epilogue
+std::atomic<int> g_epi_fold{-1};
+bool epi_fold_enabled() {
+    int v = g_epi_fold.load(std::memory_order_relaxed);
+    if (v < 0) {
+        v = (!getenv("GGML_HIP_GEMV_EPI") || atoi(getenv("GGML_HIP_GEMV_EPI")) != 0) ? 1 : 0;
+        g_epi_fold.store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
 std::atomic<int> g_fuse{-1};
 bool fuse_enabled() {
     int v = g_fuse.load(std::memory_order_relaxed);
@@ -702,6 +714,139 @@ bool flush_group_x9(const Group &g) {
     return true;
 }
 
+// f32 elements of t at byte offset 4 * (linear element index) from its data (a contiguous, or a
+// transposed single-row / single-column, view)
+bool linear_f32(const tensor *t) {
+    if (t->type != gabi::TYPE_F32) return false;
+    int64_t want = 4;
+    for (int i = 0; i < 4; i++) {
+        if (t->ne[i] > 1 && t->nb[i] != want) return false;
+        want *= t->ne[i];
+    }
+    return true;
+}
+
+// The prefix of a decode norm group's held nodes that the GEMV finishes in its epilogue (ghip::GemvEpi):
+// each one reads exactly one member's whole output as linear elements (rope mode 0 on one token, with its
+// K-cache copy, or a copy such as V into the transposed V cache), at most one per member, and writes
+// nothing any member, the norm chain or another of them reads or writes.  Returns how many held nodes
+// that is (0: no epilogue).
+int epi_prefix(const Group &g, ghip::GemvEpi &ep) {
+    if (!fuse_enabled() || !epi_fold_enabled() || g.norm.kind != 1 || g.na == 0) return 0;
+    ep = ghip::GemvEpi{};
+    struct Range {
+        const char *p;
+        size_t n;
+    };
+    std::vector<Range> wr;                 // what the epilogue writes besides the members' outputs
+    int owner[4] = {-1, -1, -1, -1};
+    auto member_of = [&](const tensor *x) {
+        for (int i = 0; i < g.n; i++)
+            if (dptr(x) == dptr(g.mm[i]) && x->ne[0] * x->ne[1] * x->ne[2] * x->ne[3] == g.mm[i]->src0->ne[1] &&
+                g.mm[i]->src0->ne[1] < ((int64_t)1 << 20) && linear_f32(x))
+                return owner[i] < 0 ? i : -1;
+        return -1;
+    };
+    auto add_copy = [&](int i, const tensor *b) {
+        // the kernel's index math: extents below 2^20 (udiv20), byte strides in int32
+        if (b->ne[0] >= ((int64_t)1 << 20) || b->ne[1] >= ((int64_t)1 << 20) || b->nb[0] > INT32_MAX || b->nb[1] > INT32_MAX ||
+            b->nb[2] > INT32_MAX)
+            return false;
+        ep.c[i] = dptr(b);
+        ep.f16[i] = b->type == gabi::TYPE_F16;
+        ep.ne10[i] = (int)b->ne[0], ep.ne11[i] = (int)b->ne[1];
+        ep.nb10[i] = (int)b->nb[0], ep.nb11[i] = (int)b->nb[1], ep.nb12[i] = (int)b->nb[2];
+        wr.push_back({dptr(b), span_bytes(b)});
+        return true;
+    };
+    int used = 0, nops = 0;
+    while (used < g.na) {
+        const tensor *t = g.after[used];
+        ghip::ElemOp op;
+        int i = -1, take = 0;
+        if (rope_elem(t, op)) {
+            i = member_of(t->src0);
+            if (i < 0 || t->src0->ne[2] != 1 || !linear_f32(t) || op.ne0 % 2 || op.npairs * 2 != op.ne0) break;
+            ep.kind[i] = 1;
+            ep.d[i] = (float *)dptr(t);
+            ep.cs[i] = op.cs;
+            ep.ne0[i] = (int)op.ne0;
+            if (dptr(t) != dptr(g.mm[i])) wr.push_back({dptr(t), span_bytes(t)});
+            take = 1;
+            if (used + 1 < g.na && g.after[used + 1]->src0 == t && cpy_target_ok(g.after[used + 1]) &&
+                add_copy(i, g.after[used + 1]->src1))
+                take = 2;
+        } else if (cpy_target_ok(t)) {
+            i = member_of(t->src0);
+            if (i < 0) break;
+            ep.kind[i] = 2;
+            if (!add_copy(i, t->src1)) break;
+            take = 1;
+        } else {
+            break;
+        }
+        owner[i] = used;
+        used += take;
+        nops++;
+    }
+    if (nops == 0) return 0;
+    // nothing written overlaps another write, a member's output, or the norm chain's operands
+    const size_t row = (size_t)g.norm.ncols * 4;
+    std::vector<Range> rd;
+    for (int i = 0; i < g.n; i++) rd.push_back({dptr(g.mm[i]), span_bytes(g.mm[i])});
+    for (const void *q : {(const void *)g.norm.a, (const void *)g.norm.b, (const void *)g.norm.w,
+                          (const void *)g.norm.sum, (const void *)g.norm.norm, (const void *)g.norm.out})
+        if (q) rd.push_back({(const char *)q, row});
+    auto hit = [](const Range &a, const Range &b) { return a.p < b.p + b.n && b.p < a.p + a.n; };
+    for (size_t a = 0; a < wr.size(); a++) {
+        for (size_t b = a + 1; b < wr.size(); b++)
+            if (hit(wr[a], wr[b])) return 0;
+        for (const Range &r : rd)
+            if (hit(wr[a], r)) return 0;
+    }
+    for (int i = 0; i < g.n; i++) {        // rows of members without an op: plain stores
+        if (owner[i] >= 0) continue;
+        ep.kind[i] = 0;
+    }
+    return used;
+}
+
+// w1 | w3 followed by silu(w1) -> mul(silu, w3) (the LLaMA FFN, held behind the group): the GEMV runs
+// the two matrices as interleaved (gate, up) rows and finishes silu -> mul in its epilogue (GemvEpi
+// glu).  Returns 2 (the held nodes it takes) and the gate's member index, or 0.
+int glu_prefix(const Group &g, ghip::GemvEpi &ep, int *gate) {
+    if (!fuse_enabled() || !epi_fold_enabled() || !silu_fold_enabled() || g.norm.kind != 1 || g.n != 2 || g.na < 2)
+        return 0;
+    const tensor *sl = g.after[0], *ml = g.after[1];
+    if (sl->op != gabi::OP_SILU || ml->op != gabi::OP_MUL || !same_tensor(ml->src0, sl) || !dev_f32(sl) || !dev_f32(ml))
+        return 0;
+    const int64_t M = g.mm[0]->src0->ne[1];
+    if (g.mm[1]->src0->ne[1] != M || M >= ((int64_t)1 << 30)) return 0;
+    int ga = -1;
+    for (int i = 0; i < 2; i++)
+        if (dptr(sl->src0) == dptr(g.mm[i])) ga = i;
+    if (ga < 0 || dptr(ml->src1) != dptr(g.mm[1 - ga])) return 0;
+    for (const tensor *x : {(const tensor *)sl->src0, (const tensor *)ml->src1, sl, ml})
+        if (x->type != gabi::TYPE_F32 || x->ne[0] * gabi::nrows(x) != M || !linear_f32(x)) return 0;
+    // the two stores write nothing the GEMV, its norm prologue or the other stores touch
+    const size_t row = (size_t)g.norm.ncols * 4;
+    for (const tensor *o : {(const tensor *)sl, (const tensor *)ml}) {
+        for (int i = 0; i < 2; i++)
+            if (dev_overlap(o, g.mm[i])) return 0;
+        for (const void *q : {(const void *)g.norm.a, (const void *)g.norm.b, (const void *)g.norm.w,
+                              (const void *)g.norm.sum, (const void *)g.norm.norm, (const void *)g.norm.out})
+            if (q && (const char *)q < dptr(o) + span_bytes(o) && dptr(o) < (const char *)q + row) return 0;
+    }
+    if (dev_overlap(sl, ml)) return 0;
+    ep = ghip::GemvEpi{};
+    ep.glu = 1;
+    ep.table = op_tables(g_main_device, g_dev[g_main_device].stream).silu;
+    ep.d[0] = (float *)dptr(sl);
+    ep.d[1] = (float *)dptr(ml);
+    *gate = ga;
+    return 2;
+}
+
 void flush_group() {
     const Group g = g_grp;
     g_grp = Group{};
@@ -725,14 +870,34 @@ void flush_group() {
         }
         const ghip::GemvNorm nrm{g.norm.a, g.norm.w, g.norm.sum, g.norm.norm, g.norm.out, g.norm.kind, g.norm.table};
         HIP_FATAL(hipSetDevice(g_main_device));
-        HIP_FATAL(ghip::gemv_q4_0_multi_norm(g.n, w, m, g.norm.ncols, g.norm.b, nrm, y, ldy,
-                                             g_dev[g_main_device].info, g_dev[g_main_device].stream));
+        ghip::GemvEpi ep;
+        int gate = 0;
+        int ne = glu_prefix(g, ep, &gate);
+        if (ne > 0 && gate == 1) {        // the gate first
+            std::swap(w[0], w[1]);
+            std::swap(m[0], m[1]);
+            std::swap(ldy[0], ldy[1]);
+            std::swap(y[0], y[1]);
+        }
+        if (ne == 0) ne = epi_prefix(g, ep);
+        hipError_t e = hipErrorInvalidValue;
+        if (ne > 0) {                     // the launch shape may refuse the epilogue (nothing launched)
+            e = ghip::gemv_q4_0_multi_norm(g.n, w, m, g.norm.ncols, g.norm.b, nrm, y, ldy, g_dev[g_main_device].info,
+                                           g_dev[g_main_device].stream, &ep);
+            if (e == hipErrorInvalidValue) ne = 0;
+            else HIP_FATAL(e);
+        }
+        if (ne == 0)
+            HIP_FATAL(ghip::gemv_q4_0_multi_norm(g.n, w, m, g.norm.ncols, g.norm.b, nrm, y, ldy,
+                                                 g_dev[g_main_device].info, g_dev[g_main_device].stream));
         for (int i = 0; i < g.norm.nn; i++) count_node(g.norm.node[i]);
         for (int i = 0; i < g.n; i++) count_node(g.mm[i]);
+        for (int i = 0; i < ne; i++) count_node(g.after[i]);
         g_fused[g.norm.kind == 2 ? 2 : 0].fetch_add(1, std::memory_order_relaxed);
         g_fused[g.norm.kind == 2 ? 10 : 9].fetch_add(1, std::memory_order_relaxed);
         if (g.n > 1) g_fused[6].fetch_add(1, std::memory_order_relaxed);
-        const int done = run_elem_prefix(g.after, g.na);
+        if (ne > 0) g_fused[ep.glu ? 13 : 12].fetch_add(1, std::memory_order_relaxed);
+        const int done = ne + run_elem_prefix(g.after + ne, g.na - ne);
         for (int i = done; i < g.na; i++) execute_node(g.after[i]);
         return;
     }
@@ -884,6 +1049,13 @@ int ggml_hip_debug_launch_stats(long long *out, int enable) {
 int ggml_hip_debug_set_norm_fold(int on) {
     flush_deferred();
     g_norm_fold.store(on < 0 || on > 2 ? 1 : on);
+    return GGML_HIP_OK;
+}
+
+// not in the public header: the decode q|k|v GEMV epilogue (held rope / copy nodes) on (1) / off (0)
+int ggml_hip_debug_set_epi_fold(int on) {
+    flush_deferred();
+    g_epi_fold.store(on ? 1 : 0);
     return GGML_HIP_OK;
 }
 

@@ -305,7 +305,13 @@ void async_drain() {
     Launcher &L = launcher();
     if (!L.started) return;
     const uint64_t h = L.head.load(std::memory_order_relaxed);
-    while (L.tail.load(std::memory_order_acquire) != h) std::this_thread::yield();
+    if (L.tail.load(std::memory_order_acquire) != h) {     // counted as runs / submit ns (rec_stats)
+        const auto t0 = std::chrono::steady_clock::now();
+        while (L.tail.load(std::memory_order_acquire) != h) std::this_thread::yield();
+        rec().runs++;
+        rec().submit_ns +=
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    }
     if (const int e = L.err.exchange(0)) fatal((hipError_t)e, "hipLaunchKernel (launcher thread)");
 }
 }  // namespace
@@ -350,7 +356,7 @@ void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s
 void rec_flush_at(const char *why) {
     REC_LOCK;
     static const bool trace = getenv("GGML_HIP_TRACE_GRAPH") != nullptr;
-    if (trace && !rec().cur.items.empty())
+    if (trace && rec_pending())
         fprintf(stderr, "rec_flush: %zu launches, by %s\n", rec().cur.items.size(), why);
     rec_flush();
 }

@@ -188,7 +188,7 @@ extern std::atomic<int64_t> g_op_count[gabi::OP_COUNT];      // device nodes run
 extern std::atomic<int64_t> g_host_ns;                        // host time inside the taken nodes
 extern std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of the node that arrived
 // fused launches by chain (index list at the definition, ggml-hip-ops.cpp)
-constexpr int N_FUSED = 12;
+constexpr int N_FUSED = 14;
 extern std::atomic<int64_t> g_fused[N_FUSED];
 
 // ---- the hook's node scheduler (ggml-hip-fuse.cpp)

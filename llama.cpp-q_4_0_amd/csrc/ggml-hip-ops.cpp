@@ -173,9 +173,10 @@ std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of th
 // fused launches by chain: add/rms_norm/mul, scale/mask/soft_max, silu/mul, rope/cpy, KQV/merge cpy,
 // q4_0 mul_mat run under a pending silu, sibling q4_0 GEMVs (wq|wk|wv, w1|w3) run as one group,
 // independent rope / rope->cpy / cpy nodes held behind a group run as one launch, the decode
-// soft_max chain with its KQV and merged copy as one launch
 // soft_max chain with its KQV and merged copy as one launch, the decode norm / silu chains in the GEMV
-// prologue (9, 10), the prefill chains that wrote the k_gemm9 x image of their output (11)
+// prologue (9, 10), the prefill chains that wrote the k_gemm9 x image of their output (11), the decode
+// q|k|v GEMVs that ran the held rope / copy nodes in their epilogue (12), the decode w1|w3 GEMVs that ran
+// silu -> mul in theirs (13)
 std::atomic<int64_t> g_fused[N_FUSED];
 
 // fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)

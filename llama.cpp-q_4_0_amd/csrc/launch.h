@@ -38,7 +38,7 @@ void rec_enable(hipStream_t s, bool on);
 // 1: runs submitted as cached HIP graphs; 2: a launcher thread issues the launches in order
 void rec_set_mode(int mode);
 // counters: submitted runs, kernels in them, nodes updated in place, graphs instantiated, host ns
-// spent submitting
+// spent submitting (mode 2: waits for the launcher thread to drain, and the ns spent waiting)
 void rec_stats(long long *runs, long long *kernels, long long *updated, long long *built, long long *submit_ns);
 // submits what is pending and destroys every cached graph
 void rec_clear_cache();

@@ -84,6 +84,20 @@ struct GemvTail {
     int64_t ldy[GEMV_MAXMAT];
     GemvNorm nrm;                         // NORM instantiations only
 };
+// a / b for a < 2^20, 1 <= b < 2^20 (the epilogue's element indices): a float reciprocal estimate and
+// one correction (the estimate is within 1 of the quotient there)
+__device__ __forceinline__ uint32_t udiv20(uint32_t a, uint32_t b) {
+    int q = (int)((float)a * __builtin_amdgcn_rcpf((float)b));
+    const int rem = (int)a - q * (int)b;
+    q += rem < 0 ? -1 : (rem >= (int)b ? 1 : 0);
+    return (uint32_t)q;
+}
+struct GemvTailEpi : GemvTail {
+    GemvEpi epi;                          // EPI instantiations (q4_0_kernels.h)
+};
+template <int EPI> struct GemvTailOf { using type = GemvTail; };
+template <> struct GemvTailOf<1> { using type = GemvTailEpi; };
+template <> struct GemvTailOf<2> { using type = GemvTailEpi; };
 // geom = nb | map << 16 | grid << 18  (nb < 2^16, grid < 2^14; checked by the launcher)
 
 // Weight loads are plain global loads with clamped lane addresses; only the first XW waves load and
@@ -120,11 +134,11 @@ __device__ __forceinline__ double wave_sum_d64(double v) {   // every lane gets 
 __device__ uint64_t *g_gemv_stamps = nullptr;
 __device__ int g_gemv_stamp_m = -1;
 #endif
-template <int NT, int WAVES, int DEPTH, int VAR, int PPL = 0, int PRO = 0, int BAL = 0>
+template <int NT, int WAVES, int DEPTH, int VAR, int PPL = 0, int PRO = 0, int BAL = 0, int EPI = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restrict__ x_, const uint8_t *W0,
                                                           const uint8_t *W1, const uint8_t *W2, int rb1_, int rb2_,
                                                           int rb3_, int rowbytes_, int geom, int M_,
-                                                          const GemvTail tail) {
+                                                          const typename GemvTailOf<EPI>::type tail) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 #ifdef GEMV_STAMPS
     const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
@@ -170,8 +184,14 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
     // multiple of grid*WAVES.
     int row0, rstride, rend;
     if (map == 2) {                                                 // grid * M < 2^32 (launcher)
-        row0 = (int)(((uint32_t)blockIdx.x * (uint32_t)M) / (uint32_t)grid) + wave;
-        rend = (int)(((uint32_t)(blockIdx.x + 1) * (uint32_t)M) / (uint32_t)grid);
+        if constexpr (EPI == 2) {                                   // whole (gate, up) pairs per workgroup
+            const uint32_t P = (uint32_t)M >> 1;
+            row0 = 2 * (int)(((uint32_t)blockIdx.x * P) / (uint32_t)grid) + wave;
+            rend = 2 * (int)(((uint32_t)(blockIdx.x + 1) * P) / (uint32_t)grid);
+        } else {
+            row0 = (int)(((uint32_t)blockIdx.x * (uint32_t)M) / (uint32_t)grid) + wave;
+            rend = (int)(((uint32_t)(blockIdx.x + 1) * (uint32_t)M) / (uint32_t)grid);
+        }
         rstride = WAVES;
     } else {
         row0 = map == 1 ? wave * grid + blockIdx.x : blockIdx.x * WAVES + wave;
@@ -187,6 +207,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
 
     static_assert(GEMV_MAXMAT == 4, "matrix selection below is written for 4 siblings");
     auto row_ptr = [&](int r) __attribute__((always_inline)) {     // wave-uniform
+        if constexpr (EPI == 2)     // (gate, up) interleaved: row r is row r / 2 of matrix r & 1
+            return reinterpret_cast<const uint8_t *>((uint64_t)w0 + ((r & 1) ? wd1 : 0)) + (int64_t)(r >> 1) * rowbytes;
         // sums of selected deltas (a ternary chain over the pointers becomes a scratch lookup table)
         const bool g1 = r >= rb1, g2 = r >= rb2;
         uint64_t w = (uint64_t)w0 + (g1 ? wd1 : 0) + (g2 ? wd2 : 0);
@@ -454,6 +476,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
 #pragma unroll
     for (int n = 0; n < NT; n++) acc[n] = 0.0f;
     float *const part = reinterpret_cast<float *>(xs + NT * nb);   // BAL: [rows of the WG][nchunk]
+    // EPI: [row item][wave] outputs of the workgroup (after PRO 1's per-wave double sums)
+    float *const epl = reinterpret_cast<float *>(xs + NT * nb) + (PRO == 1 ? 2 * WAVES : 0);
     auto process = [&](const ItemRegs &vi, int it) __attribute__((always_inline)) {
         const int chunk = item_chunk(it);
 #pragma unroll
@@ -502,7 +526,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
                 out = (lane == n) ? tn : out;
                 acc[n] = 0.0f;
             }
-            if (lane < NT) yo[(int64_t)lane * ld] = out;
+            if constexpr (EPI) {                                    // parked for the epilogue (NT == 1)
+                if (lane == 0) epl[(it / nchunk) * WAVES + wave] = out;
+            } else {
+                if (lane < NT) yo[(int64_t)lane * ld] = out;
+            }
         }
     };
     for (int it = 0; it < nitems; it += DEPTH) {
@@ -511,6 +539,76 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             if (it + d >= nitems) break;
             process(buf[d], it + d);
             buf[d] = issue(it + d + DEPTH);
+        }
+    }
+    if constexpr (EPI == 2) {
+        // silu(gate) * up of the interleaved pairs, as k_silu_mul (its fp16 table value, then the product):
+        // the even row's lane stores the gate output and silu(gate), the odd row's the up output and the product
+        __syncthreads();
+        if (lane < nrows_w) {
+            typedef __attribute__((address_space(1))) float gfloat;
+            const int k = lane;
+            const int r = row0 + k * rstride;
+            const float v = epl[k * WAVES + wave], pv = epl[k * WAVES + (wave ^ 1)];
+            const bool odd = (r & 1) != 0;
+            const float gate = odd ? pv : v, up = odd ? v : pv;
+            const float u = h2f(lut_silu(tail.epi.table, f2h(gate)));
+            const int e = r >> 1;
+            float *const ym = reinterpret_cast<float *>(odd ? y0 + yd1 : y0);
+            ((gfloat *)ym)[e] = v;
+            float *const dst = odd ? tail.epi.d[1] : tail.epi.d[0];
+            ((gfloat *)dst)[e] = odd ? u * up : u;
+        }
+    } else if constexpr (EPI) {
+        // every output of the workgroup is in LDS: lane k of each wave finishes the wave's row k, pairing
+        // row r with r ^ 1 (the same item of wave ^ 1 under the strided mapping, which the launcher enforces)
+        static_assert(NT == 1 && PPL > 0 && !BAL, "epilogue: decode row items only");
+        __syncthreads();
+        if (lane < nrows_w) {
+            typedef __attribute__((address_space(1))) float gfloat;
+            typedef __attribute__((address_space(1))) uint16_t gu16;
+            const int k = lane;
+            const int r = row0 + k * rstride;
+            const float v = epl[k * WAVES + wave], pv = epl[k * WAVES + (wave ^ 1)];
+            const bool g1 = r >= rb1, g2 = r >= rb2, g3 = r >= rb3;
+            const int mi = (int)g1 + (int)g2 + (int)g3;
+            const int rb = (g1 ? rb1 : 0) + (g2 ? rb2 - rb1 : 0) + (g3 ? rb3 - rb2 : 0);
+            const uint32_t e = (uint32_t)(r - rb);
+            float *const ym = reinterpret_cast<float *>(y0 + (g1 ? yd1 : 0) + (g2 ? yd2 : 0) + (g3 ? yd3 : 0));
+            // this matrix's epilogue (constant-index field reads, selected per lane)
+            const GemvEpi &ep = tail.epi;
+            int kind = ep.kind[0], f16 = ep.f16[0], ne0 = ep.ne0[0], ne10 = ep.ne10[0], ne11 = ep.ne11[0];
+            int nb10 = ep.nb10[0], nb11 = ep.nb11[0], nb12 = ep.nb12[0];
+            float *d = ep.d[0];
+            const float2 *cs = ep.cs[0];
+            char *cc = ep.c[0];
+#define GEMV_EPI_SEL(I)                                                                                      \
+            if (mi == I) {                                                                                   \
+                kind = ep.kind[I], f16 = ep.f16[I], ne0 = ep.ne0[I], ne10 = ep.ne10[I], ne11 = ep.ne11[I];   \
+                nb10 = ep.nb10[I], nb11 = ep.nb11[I], nb12 = ep.nb12[I], d = ep.d[I], cs = ep.cs[I];          \
+                cc = ep.c[I];                                                                                \
+            }
+            GEMV_EPI_SEL(1)
+            GEMV_EPI_SEL(2)
+            GEMV_EPI_SEL(3)
+#undef GEMV_EPI_SEL
+            float o = v;
+            if (kind == 1) {                                        // rope mode 0, as k_elem_batch kind 0
+                const uint32_t i0 = e - udiv20(e, (uint32_t)ne0) * (uint32_t)ne0;
+                const float2 t = cs[i0 >> 1];
+                o = (i0 & 1) ? pv * t.y + v * t.x : v * t.x - pv * t.y;
+                ((gfloat *)d)[e] = o;
+            }
+            if (kind != 1 || d != ym) ((gfloat *)ym)[e] = v;        // the mul_mat's own output
+            if (cc) {                                               // linear element e of the copy's view
+                const uint32_t q10 = udiv20(e, (uint32_t)ne10), i10 = e - q10 * (uint32_t)ne10;
+                const uint32_t i12 = udiv20(q10, (uint32_t)ne11), i11 = q10 - i12 * (uint32_t)ne11;
+                char *dst = cc + (int64_t)i10 * nb10 + (int64_t)i11 * nb11 + (int64_t)i12 * nb12;
+                if (f16)
+                    *(gu16 *)dst = (uint16_t)f2h(o);
+                else
+                    *(gfloat *)dst = o;
+            }
         }
     }
     if constexpr (BAL) {                                            // rows' chunk sums, in chunk order
@@ -575,9 +673,9 @@ int gemv_max_tokens(int64_t K) {
 }
 
 
-template <int NT, int WAVES, int DEPTH, int VAR, int PPL = 0, int PRO = 0, int BAL = 0>
+template <int NT, int WAVES, int DEPTH, int VAR, int PPL = 0, int PRO = 0, int BAL = 0, int EPI = 0>
 static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, const DeviceInfo &dev, hipStream_t s,
-                                const GemvNorm *nrm = nullptr) {
+                                const GemvNorm *nrm = nullptr, const GemvEpi *epi = nullptr) {
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     size_t lds = (size_t)NT * nb * 40 + (PRO == 1 ? WAVES * sizeof(double) : 0);
@@ -590,7 +688,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     static int occ = 0;                    // resident workgroups per CU for this instantiation
     if (occ == 0) {
         int nb_occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, WAVES, DEPTH, VAR, PPL, PRO, BAL>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_occ, k_gemv_q4_0<NT, WAVES, DEPTH, VAR, PPL, PRO, BAL, EPI>,
                                                          WAVES * 64, lds) != hipSuccess || nb_occ < 1)
             nb_occ = 1;
         occ = nb_occ;
@@ -615,8 +713,24 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
         lds += (size_t)((M + grid - 1) / grid) * nchunk * sizeof(float);
         if (lds > GEMV_LDS_MAX) return hipErrorInvalidValue;   // launch_gemv checks before choosing BAL
     }
+    if (EPI) {
+        // strided rows (row r ^ 1 is the same item of wave ^ 1 in the same workgroup) or, for the
+        // interleaved (gate, up) rows, blocked whole pairs per workgroup; every output of the workgroup
+        // parked in LDS, pairs never straddling two matrices
+        static const int glu_map = env_int("GGML_HIP_GEMV_GLU_MAP", 2);
+        map = EPI == 2 && glu_map == 2 ? 2 : 0;
+        if (EPI == 2 && (m.n != 2 || 2 * m.row_begin[1] != m.row_begin[2])) return hipErrorInvalidValue;
+        for (int i = 1; i <= m.n; i++)
+            if (m.row_begin[i] & 1) return hipErrorInvalidValue;
+        if (map == 2 && (int64_t)grid * M >= (int64_t)1 << 32) return hipErrorInvalidValue;
+        const int64_t rows_w = map == 2 ? (2 * ((M / 2 + grid - 1) / grid) + WAVES - 1) / WAVES
+                                        : (M + (int64_t)grid * WAVES - 1) / ((int64_t)grid * WAVES);
+        lds += (size_t)rows_w * WAVES * sizeof(float);
+        if (lds > GEMV_LDS_MAX || rows_w > 64) return hipErrorInvalidValue;   // one lane per row of a wave
+    }
     if (nb >= (1 << 16) || grid >= (1u << 14) || rowbytes > INT_MAX || M > INT_MAX) return hipErrorInvalidValue;
-    GemvTail tail{};
+    typename GemvTailOf<EPI>::type tail{};
+    if constexpr (EPI) tail.epi = *epi;
     if (nrm) tail.nrm = *nrm;
     tail.W3 = m.W[3];
     for (int i = 0; i < GEMV_MAXMAT; i++) {
@@ -625,7 +739,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
     }
     const int geom = nb | map << 16 | (int)(grid << 18);
     (void)hipGetLastError();  // report only this launch's error
-    launch_k((k_gemv_q4_0<NT, WAVES, DEPTH, VAR, PPL, PRO, BAL>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
+    launch_k((k_gemv_q4_0<NT, WAVES, DEPTH, VAR, PPL, PRO, BAL, EPI>), dim3(grid), dim3(WAVES * 64), lds, s, x, m.W[0],
                        m.W[1], m.W[2], m.row_begin[1], m.row_begin[2], m.row_begin[3], (int)rowbytes, geom, (int)M, tail);
     return hipGetLastError();
 }
@@ -730,7 +844,12 @@ hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_
 
 template <int VAR, int PPL>
 static hipError_t launch_gemv_norm(const GemvMats &m, int64_t K, const float *b, const DeviceInfo &dev, hipStream_t s,
-                                   const GemvNorm &nrm, int rd) {
+                                   const GemvNorm &nrm, int rd, const GemvEpi *epi) {
+    if (epi) {                           // the q|k|v or w1|w3 epilogue: rms_norm prologue, ring depth 1 (same y)
+        if (nrm.kind != 1) return hipErrorInvalidValue;
+        return epi->glu ? launch_gemv_w<1, GEMV_WAVES, 1, VAR, PPL, 1, 0, 2>(m, K, b, dev, s, &nrm, epi)
+                        : launch_gemv_w<1, GEMV_WAVES, 1, VAR, PPL, 1, 0, 1>(m, K, b, dev, s, &nrm, epi);
+    }
     if (nrm.kind == 2)
         return rd == 2 ? launch_gemv_w<1, GEMV_WAVES, 2, VAR, PPL, 2>(m, K, b, dev, s, &nrm)
                        : launch_gemv_w<1, GEMV_WAVES, 1, VAR, PPL, 2>(m, K, b, dev, s, &nrm);
@@ -740,7 +859,7 @@ static hipError_t launch_gemv_norm(const GemvMats &m, int64_t K, const float *b,
 
 hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *b,
                                 const GemvNorm &nrm, float *const *y, const int64_t *ldy, const DeviceInfo &dev,
-                                hipStream_t s) {
+                                hipStream_t s, const GemvEpi *epi) {
     // one round of x-waves holds the row: K / 4 float4 <= 16 waves * 64 lanes * GEMV_XPRO
     if (nmat < 1 || nmat > GEMV_MAXMAT || K % 64 != 0 || K / 4 > 16 * 64 * GEMV_XPRO || !b ||
         (nrm.kind == 1 && !nrm.w) || (nrm.kind == 2 && (!nrm.a || !nrm.table)) || (nrm.kind != 1 && nrm.kind != 2))
@@ -768,13 +887,13 @@ hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M
     const int rd = depth_env == 2 ? 2 : 1;
     const int ppl = (int)((K / 64 + 63) / 64);
     if (var == 15) {
-        if (ppl == 1) return launch_gemv_norm<15, 1>(m, K, b, dev, s, nrm, rd);
-        if (ppl == 2) return launch_gemv_norm<15, 2>(m, K, b, dev, s, nrm, rd);
-        if (ppl == 3) return launch_gemv_norm<15, 3>(m, K, b, dev, s, nrm, rd);
+        if (ppl == 1) return launch_gemv_norm<15, 1>(m, K, b, dev, s, nrm, rd, epi);
+        if (ppl == 2) return launch_gemv_norm<15, 2>(m, K, b, dev, s, nrm, rd, epi);
+        if (ppl == 3) return launch_gemv_norm<15, 3>(m, K, b, dev, s, nrm, rd, epi);
     } else {
-        if (ppl == 1) return launch_gemv_norm<3, 1>(m, K, b, dev, s, nrm, rd);
-        if (ppl == 2) return launch_gemv_norm<3, 2>(m, K, b, dev, s, nrm, rd);
-        if (ppl == 3) return launch_gemv_norm<3, 3>(m, K, b, dev, s, nrm, rd);
+        if (ppl == 1) return launch_gemv_norm<3, 1>(m, K, b, dev, s, nrm, rd, epi);
+        if (ppl == 2) return launch_gemv_norm<3, 2>(m, K, b, dev, s, nrm, rd, epi);
+        if (ppl == 3) return launch_gemv_norm<3, 3>(m, K, b, dev, s, nrm, rd, epi);
     }
     return hipErrorInvalidValue;        // K > 12288: chunked items are not instantiated with the prologue
 }

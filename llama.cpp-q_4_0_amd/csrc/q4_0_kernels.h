@@ -55,9 +55,29 @@ struct GemvNorm {
     int kind = 1;
     const uint16_t *table = nullptr;     // kind 2: ggml's silu table (65536 fp16 bit patterns)
 };
+// Decode epilogue of a sibling GEMV (hook path, one token): the elementwise nodes ggml emits right after the
+// q|k|v mul_mats (rope mode 0 of K and Q in place, K into the K cache, V into the transposed V cache) done by
+// the GEMV on its own output element e of matrix i, with the arithmetic of k_elem_batch (ggml_ops.hip) bit
+// for bit.  kind 0: y[e] = v; 1: d[e] = rope(v, partner e ^ 1) with (cos, sin) cs[(e % ne0) / 2] (and
+// y[e] = v unless d is y), then the copy of d[e]; 2: y[e] = v, then the copy of v.  The copy writes
+// linear element e of its target view (ne10, ne11, strides in bytes) as F16 or F32 when c != nullptr.
+//   glu != 0 instead (two matrices of M rows, gate then up, launched as 2M interleaved rows): the silu -> mul
+// that follows w1 | w3, d[0][e] = silu(gate[e]) and d[1][e] = d[0][e] * up[e] as k_silu_mul computes them
+// (table: table_silu_f16 as the kernels take it), beside the two outputs
+struct GemvEpi {
+    int glu;
+    const uint16_t *table;
+    float *d[GEMV_MULTI_MAX];
+    const float2 *cs[GEMV_MULTI_MAX];
+    char *c[GEMV_MULTI_MAX];
+    int kind[GEMV_MULTI_MAX], f16[GEMV_MULTI_MAX], ne0[GEMV_MULTI_MAX];
+    int ne10[GEMV_MULTI_MAX], ne11[GEMV_MULTI_MAX], nb10[GEMV_MULTI_MAX], nb11[GEMV_MULTI_MAX], nb12[GEMV_MULTI_MAX];
+};
+// epi: nullptr, or the epilogue of every matrix (strided row mapping; returns hipErrorInvalidValue where the
+// launch shape cannot pair rows e and e ^ 1 inside one workgroup)
 hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M, int64_t K, const float *b,
                                 const GemvNorm &nrm, float *const *y, const int64_t *ldy, const DeviceInfo &dev,
-                                hipStream_t s);
+                                hipStream_t s, const GemvEpi *epi = nullptr);
 
 // test hook: force the GEMV launch policy (row mapping 0/1/2, ring depth 1/2, row items 0/1,
 // workgroups per CU); -1 / 0 = automatic

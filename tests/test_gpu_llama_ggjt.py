@@ -31,7 +31,7 @@ pytestmark = [pytest.mark.gpu,
 OPS = json.load(open(os.path.join(GOLD, "ggml_op_enum.json")))
 
 
-N_FUSED = 12  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
+N_FUSED = 14  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
 
 
 def op_stats(L, reset=True, fused=False):
@@ -217,8 +217,11 @@ def test_norm_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode):
     lib.refllama_bench.restype = ctypes.c_int
     lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
     L.ggml_hip_debug_set_norm_fold.argtypes = [ctypes.c_int]
+    L.ggml_hip_debug_set_epi_fold.argtypes = [ctypes.c_int]
     prev = L.ggml_hip_get_exact()
     ggml_hip.check(L.ggml_hip_set_exact(0), "set_exact")
+    # the GEMV epilogues off: w1|w3 would take silu -> mul before the w2 prologue sees it
+    ggml_hip.check(L.ggml_hip_debug_set_epi_fold(0), "set_epi_fold")
     out = {}
     try:
         for fold in (1, 0):
@@ -231,6 +234,7 @@ def test_norm_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode):
     finally:
         L.ggml_hip_set_exact(prev)
         L.ggml_hip_debug_set_norm_fold(1)
+        L.ggml_hip_debug_set_epi_fold(1)
     assert np.isfinite(out[1][0]).all()
     assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
     assert out[1][1][9] >= (2 * hp["n_layer"] - 1) * n_decode, out[1][1]
@@ -238,6 +242,46 @@ def test_norm_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode):
     assert out[0][1][9] == 0 and out[0][1][10] == 0, out[0][1]
     for k in (0, 2):                                                 # every chain still counted once
         assert out[1][1][k] == out[0][1][k], (out[1][1], out[0][1])
+
+
+@pytest.mark.parametrize("hp,n_prompt,n_decode", [(HP128, 40, 60), (G.HP, 8, 40)], ids=["head128", "head64"])
+def test_gemv_epilogue_bitwise_vs_elem_batch(tmp_path, hp, n_prompt, n_decode):
+    """The decode GEMVs finish the nodes ggml holds behind them in their epilogue (ghip::GemvEpi): q|k|v
+    the rope K -> the F16 K cache, V -> the transposed V cache, rope Q; w1|w3 (as interleaved gate / up
+    rows) silu -> mul.  The same logits bit for bit as the batched elementwise launch after the GEMV
+    (k_elem_batch) and silu -> mul in the w2 GEMV's prologue, and the epilogues fire for every device
+    group of a decode eval (layer 0's q|k|v reads the host embedding row: no device norm chain, no group
+    with a prologue, so its nodes stay in the batch)."""
+    L = ggml_hip.load()
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp, hp=hp)
+    nv = hp["n_vocab"]
+    lib = ctypes.CDLL(HIP_LIB)
+    lib.refllama_bench.restype = ctypes.c_int
+    lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    L.ggml_hip_debug_set_epi_fold.argtypes = [ctypes.c_int]
+    prev = L.ggml_hip_get_exact()
+    ggml_hip.check(L.ggml_hip_set_exact(0), "set_exact")
+    out = {}
+    try:
+        for epi in (1, 0):
+            ggml_hip.check(L.ggml_hip_debug_set_epi_fold(epi), "set_epi_fold")
+            op_stats(L)
+            lg = np.zeros(nv, np.float32)
+            res = np.zeros(3, np.float64)
+            assert lib.refllama_bench(mp.encode(), n_prompt, n_decode, 1, 99, 1024, 1, res.ctypes.data, lg.ctypes.data) == nv
+            out[epi] = (lg, op_stats(L, reset=False, fused=True))
+    finally:
+        L.ggml_hip_set_exact(prev)
+        L.ggml_hip_debug_set_epi_fold(1)
+    assert np.isfinite(out[1][0]).all()
+    assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
+    (ran1, f1), (ran0, f0) = out[1][1], out[0][1]
+    assert f1[12] >= (hp["n_layer"] - 1) * n_decode, f1
+    assert f1[13] >= hp["n_layer"] * n_decode, f1
+    assert f0[12] == 0 and f0[13] == 0, f0
+    assert f0[7] - f1[7] >= (hp["n_layer"] - 1) * n_decode, (f1, f0)   # the batches it replaced
+    assert np.array_equal(ran1, ran0)                                  # every node still counted once
 
 
 @pytest.mark.parametrize("n_prompt", [300, 97])

@@ -116,6 +116,7 @@ def main():
     ap.add_argument("--modes", default="fast,exact")
     ap.add_argument("--out", default="")
     ap.add_argument("--shape", choices=("7b", "host"), default="7b")
+    ap.add_argument("--hostprof", default="", help="sample the host walk of each mode (tools/hostprof.c) into PATH.<mode>")
     args = ap.parse_args()
     hp = HP7B if args.shape == "7b" else HPHOST
     import ggml_hip as gh
@@ -135,19 +136,31 @@ def main():
             print("cpu", res["cpu"], file=sys.stderr, flush=True)
         L.ggml_hip_debug_graph_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
         for mode in args.modes.split(","):
-            # modes: fast, exact; suffix "-graph": launch recorder with HIP graphs (GGML_HIP_GRAPH=1),
+            # modes: fast, exact; "-noepi" (below); suffix "-graph": launch recorder with HIP graphs (GGML_HIP_GRAPH=1),
             # "-thread": launcher thread (GGML_HIP_GRAPH=2)
             gh.check(L.ggml_hip_set_exact(1 if mode.startswith("exact") else 0))
             gh.check(L.ggml_hip_debug_set_graph(1 if mode.endswith("-graph") else 2 if mode.endswith("-thread") else 0))
+            # "-noepi": the decode q|k|v GEMV epilogue off (the held rope / copy nodes as their own batch)
+            L.ggml_hip_debug_set_epi_fold.argtypes = [ctypes.c_int]
+            gh.check(L.ggml_hip_debug_set_epi_fold(0 if "-noepi" in mode else 1))
             g0 = np.zeros(5, np.int64)
             L.ggml_hip_debug_graph_stats(g0.ctypes.data, 0)
             L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-            st = np.zeros(69 + 68, np.int64)
+            st = np.zeros(2 * 68 + 1 + 14, np.int64)
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
             L.ggml_hip_debug_launch_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
             ls = np.zeros(2, np.int64)
             L.ggml_hip_debug_launch_stats(ls.ctypes.data, 1)
+            if args.hostprof:
+                # a warm run first: the sampler's signals must not interrupt the HIP runtime's start-up
+                # (device discovery, code-object loads), which then finds no device
+                bench(HIP_LIB, model, args.prompt, 4, args.threads_gpu, 99, 1, nv)
+                hp_lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhostprof.so"))
+                hp_lib.hostprof_stop.argtypes = [ctypes.c_char_p]
+                hp_lib.hostprof_start(50)
             r, lg = bench(HIP_LIB, model, args.prompt, args.decode, args.threads_gpu, 99, 3, nv)
+            if args.hostprof:
+                r["hostprof_samples"] = hp_lib.hostprof_stop(f"{args.hostprof}.{mode}".encode())
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
             L.ggml_hip_debug_launch_stats(ls.ctypes.data, 0)
             r["eager_launches_per_eval"] = round(float(ls[0]) / (3 + args.decode), 1)

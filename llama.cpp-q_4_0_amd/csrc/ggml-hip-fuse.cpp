@@ -57,6 +57,18 @@ bool epi_fold_enabled() {
     return v == 1;
 }
 
+// GGML_HIP_KQ_FOLD=0: the decode KQ runs as its own launch before the soft_max -> KQV chain; on (default)
+// the chain's launch computes it
+std::atomic<int> g_kq_fold{-1};
+bool kq_fold_enabled() {
+    int v = g_kq_fold.load(std::memory_order_relaxed);
+    if (v < 0) {
+        v = (!getenv("GGML_HIP_KQ_FOLD") || atoi(getenv("GGML_HIP_KQ_FOLD")) != 0) ? 1 : 0;
+        g_kq_fold.store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
 std::atomic<int> g_fuse{-1};
 bool fuse_enabled() {
     int v = g_fuse.load(std::memory_order_relaxed);
@@ -153,6 +165,15 @@ struct Pending {
     tensor *node[4] = {};
 };
 Pending g_pend;
+// The decode KQ (f16 K view . f32 q, one query row per head), held for the scale -> diag_mask_inf ->
+// soft_max -> KQV -> merge chain that follows it: the chain's launch computes it first (op_kq_softmax_kqv).
+// Run on its own (run_device_op) when anything else comes first.
+tensor *g_kq = nullptr;
+void flush_kq() {
+    tensor *t = g_kq;
+    g_kq = nullptr;
+    if (t) run_device_op(t);
+}
 
 // ---- a completed chain of one row (decode) that produces the src1 of q4_0 mul_mats, held for them:
 // they run it in their x prologue (ghip::gemv_q4_0_multi_norm), one launch less per chain; anything
@@ -229,6 +250,7 @@ bool softmax_chain(const Pending &p) {
 }
 
 void flush_pending() {
+    flush_kq();                         // the chain reads its output
     const Pending p = g_pend;
     g_pend = Pending{};
     int i = 0;
@@ -246,6 +268,21 @@ size_t span_bytes(const tensor *t);
 bool x9_chain_ok(int64_t ncols, int64_t nrows) {
     return x9_fold_enabled() && !exact_mode() && gemm_version() == 10 && nrows > IMG_MIN_N && ghip::op_x9_ok(ncols, nrows) &&
            nrows * ncols < ((int64_t)1 << 31);
+}
+
+// a decode KQ that op_kq_softmax_kqv can compute: K (f16, element stride 2) and q (f32, contiguous head
+// rows) on the device, one query row per head, head dimension <= 256, a contiguous [nkv][1][heads] output
+bool kq_holdable(const tensor *t) {
+    if (!fuse_enabled() || !kq_fold_enabled() || t->op != gabi::OP_MUL_MAT || !dev_f32(t)) return false;
+    const tensor *K = t->src0, *Q = t->src1;
+    return K && Q && K->type == gabi::TYPE_F16 && K->backend == gabi::BACKEND_GPU && K->extra && Q->type == gabi::TYPE_F32 &&
+           Q->backend == gabi::BACKEND_GPU && Q->extra && K->nb[0] == 2 && Q->nb[0] == 4 && K->ne[3] == 1 && Q->ne[3] == 1 &&
+           Q->ne[1] == 1 && K->ne[0] == Q->ne[0] && K->ne[0] >= 1 && K->ne[0] <= 256 && K->ne[2] == Q->ne[2] &&
+           t->ne[0] == K->ne[1] && t->ne[1] == 1 && t->ne[2] == K->ne[2] && t->ne[3] == 1 && (Q->nb[2] & 3) == 0;
+}
+// ... whose output the held soft_max chain reads row for row (sm: the chain's soft_max node)
+bool kq_chain_ok(const tensor *kqn, const tensor *sm) {
+    return sm->ne[0] == kqn->ne[0] && sm->ne[1] == 1 && sm->ne[2] == kqn->ne[2];
 }
 
 // t arrives while a chain is pending: extend the chain, complete it in one launch, or let a q4_0
@@ -346,9 +383,31 @@ bool try_fuse(tensor *t) {
             auto out = [&](const tensor *x) { return overlaps(x, sc->src0) ? nullptr : (float *)dptr(x); };
             const OpTables &tb = op_tables(id, s);
             HIP_FATAL(hipSetDevice(id));
-            HIP_FATAL(ghip::op_softmax_kqv((const float *)kq, out(sc), out(mk), out(sm), *(const float *)sc->src1->data,
-                                           ((const int32_t *)mk->src1->data)[0], tb.exp, sm->ne[0], sm->ne[2], dptr(vv),
-                                           vv->nb[1], vv->nb[2], vv->ne[1], (float *)dptr(kqv), (float *)dptr(cb), s));
+            tensor *kqn = g_kq;
+            if (kqn && same_tensor(sc->src0, kqn) && kq_chain_ok(kqn, sm)) {
+                // KQ in the same launch: no workgroup reads kq from memory, so every buffer of the chain is
+                // stored once, by the last tensor of the chain that owns it (in-place scale / mask / soft_max)
+                const tensor *chain[4] = {kqn, sc, mk, sm};
+                float *st[4];
+                for (int i = 0; i < 4; i++) {
+                    st[i] = (float *)dptr(chain[i]);
+                    for (int k = i + 1; k < 4; k++)
+                        if (dev_overlap(chain[i], chain[k])) st[i] = nullptr;
+                }
+                const tensor *K = kqn->src0, *Q = kqn->src1;
+                g_kq = nullptr;
+                HIP_FATAL(ghip::op_kq_softmax_kqv(dptr(K), K->nb[1], K->nb[2], (const float *)dptr(Q), Q->nb[2], (int)K->ne[0],
+                                                  st[0], st[1], st[2], st[3], *(const float *)sc->src1->data,
+                                                  ((const int32_t *)mk->src1->data)[0], tb.exp, sm->ne[0], sm->ne[2], dptr(vv),
+                                                  vv->nb[1], vv->nb[2], vv->ne[1], (float *)dptr(kqv), (float *)dptr(cb), s));
+                count_node(kqn);
+                g_fused[14].fetch_add(1, std::memory_order_relaxed);
+            } else {
+                flush_kq();
+                HIP_FATAL(ghip::op_softmax_kqv((const float *)kq, out(sc), out(mk), out(sm), *(const float *)sc->src1->data,
+                                               ((const int32_t *)mk->src1->data)[0], tb.exp, sm->ne[0], sm->ne[2], dptr(vv),
+                                               vv->nb[1], vv->nb[2], vv->ne[1], (float *)dptr(kqv), (float *)dptr(cb), s));
+            }
             for (int i = 0; i < p.n; i++) count_node(p.node[i]);
             count_node(t);
             g_fused[8].fetch_add(1, std::memory_order_relaxed);
@@ -932,6 +991,17 @@ void execute_node(tensor *t) {
         count_node(t);                      // no data touched: a pending chain stays pending
         return;
     }
+    if (g_kq) {                             // only the scale of the held KQ may start the chain behind it
+        if (g_pend.n == 0 && t->op == gabi::OP_SCALE && same_tensor(t->src0, g_kq) && deferrable(t)) {
+            g_pend.node[g_pend.n++] = hold(t);
+            return;
+        }
+        if (g_pend.n == 0) flush_kq();
+    }
+    if (!g_kq && g_pend.n == 0 && g_grp.n == 0 && !g_norm.on && kq_holdable(t)) {
+        g_kq = hold(t);
+        return;
+    }
     // a held norm chain: a GEMV that consumes it opens a group that runs it in its prologue
     auto open_norm_group = [&]() {
         if (!g_norm.on || g_grp.n != 0 || g_pend.n != 0 || !group_mm_ok(t) || !norm_feeds(g_norm, t)) return false;
@@ -1005,20 +1075,22 @@ std::atomic<int> &graph_flag() {
     return f;
 }
 bool graph_enabled() { return graph_flag().load(std::memory_order_relaxed) != 0; }
-void graph_apply_mode() {          // 1: HIP graphs, 2: launcher thread (launch.h)
+int graph_apply_mode() {           // 1: HIP graphs, 2: launcher thread (launch.h); returns the mode
     static int applied = -1;
     const int m = graph_flag().load(std::memory_order_relaxed);
     if (m != applied && m != 0) ghip::rec_set_mode(m);
     applied = m;
+    return m == 2 ? 2 : (m != 0 ? 1 : 0);
 }
 
-bool hook_holding() { return g_grp.n != 0 || g_pend.n != 0 || g_norm.on; }
+bool hook_holding() { return g_grp.n != 0 || g_pend.n != 0 || g_norm.on || g_kq; }
 bool hook_seen(const tensor *t) { return g_snaps.memo.count(t) != 0; }
 
 void flush_deferred() {
     if (g_grp.n > 0) flush_group();
     if (g_norm.on) flush_norm();
     if (g_pend.n > 0) flush_pending();
+    flush_kq();
     ghip::rec_flush_at("entry point");        // and submit the recorded launches (launch.h)
 }
 
@@ -1056,6 +1128,13 @@ int ggml_hip_debug_set_norm_fold(int on) {
 int ggml_hip_debug_set_epi_fold(int on) {
     flush_deferred();
     g_epi_fold.store(on ? 1 : 0);
+    return GGML_HIP_OK;
+}
+
+// not in the public header: the decode KQ computed by the soft_max -> KQV launch on (1) / off (0)
+int ggml_hip_debug_set_kq_fold(int on) {
+    flush_deferred();
+    g_kq_fold.store(on ? 1 : 0);
     return GGML_HIP_OK;
 }
 

@@ -107,7 +107,9 @@ void launcher_main(Launcher *L) {
             (void)hipSetDevice(cur_dev);
         }
         for (int a = 0; a < sl.nargs; a++) argv[a] = sl.blob + sl.off[a];
+        const long long t0 = g_launch_prof ? launch_prof_now() : 0;
         const hipError_t e = hipLaunchKernel(sl.fn, sl.grid, sl.block, argv, sl.lds, L->stream);
+        if (g_launch_prof) launch_prof_add(launch_prof_now() - t0);     // the worker's hipLaunchKernel cost
         if (e != hipSuccess) L->err.store((int)e, std::memory_order_relaxed);
         L->tail.store(t + 1, std::memory_order_release);
     }

@@ -188,7 +188,7 @@ extern std::atomic<int64_t> g_op_count[gabi::OP_COUNT];      // device nodes run
 extern std::atomic<int64_t> g_host_ns;                        // host time inside the taken nodes
 extern std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of the node that arrived
 // fused launches by chain (index list at the definition, ggml-hip-ops.cpp)
-constexpr int N_FUSED = 14;
+constexpr int N_FUSED = 15;
 extern std::atomic<int64_t> g_fused[N_FUSED];
 
 // ---- the hook's node scheduler (ggml-hip-fuse.cpp)
@@ -199,7 +199,7 @@ bool hook_seen(const tensor *t);        // t was snapshotted while held (a new g
 void snap_reset();
 size_t span_bytes(const tensor *t);
 bool graph_enabled();
-void graph_apply_mode();
+int graph_apply_mode();
 
 // ---- the tensor ABI (ggml-hip-tensor.cpp)
 void mul_mat_node(const tensor *src0, const tensor *src1, tensor *dst);

@@ -176,7 +176,7 @@ std::atomic<int64_t> g_op_ns[gabi::OP_COUNT];          // the same, per op of th
 // soft_max chain with its KQV and merged copy as one launch, the decode norm / silu chains in the GEMV
 // prologue (9, 10), the prefill chains that wrote the k_gemm9 x image of their output (11), the decode
 // q|k|v GEMVs that ran the held rope / copy nodes in their epilogue (12), the decode w1|w3 GEMVs that ran
-// silu -> mul in theirs (13)
+// silu -> mul in theirs (13), the decode soft_max -> KQV launches that computed KQ too (14)
 std::atomic<int64_t> g_fused[N_FUSED];
 
 // fused_cpy: a CPY node consuming t (rope -> cpy into the K cache; f16 mul_mat -> permute(0,2,1,3)
@@ -410,6 +410,52 @@ int ggml_hip_debug_x9_producer(int kind, const float *a, const float *b, const f
         HIP_RET(ghip::op_silu_mul_f32(a, b, nullptr, out_ref, ncols * nrows, tb.silu, s));
     }
     HIP_RET(ghip::gemm9_prep_x(out, ncols, nrows, img_ref, s));
+    HIP_FATAL(GHIP_SYNC(hipStreamSynchronize)(s));
+    return GGML_HIP_OK;
+}
+
+// debug: the decode sibling GEMV with its x prologue (kind 0 plain x = b, 1 [a +] b -> rms_norm -> * w, 2 silu(a)
+// * b) and optionally an epilogue (epi: a ghip::GemvEpi, its table filled here for glu), on device pointers.
+// reps > 0: the launch is repeated reps times between two events and *us receives the mean (tools/gemv_epi_ab.py);
+// the outputs are those of the last launch.
+int ggml_hip_debug_gemv_norm(int nmat, const void *const *W, const int64_t *M, int64_t K, int kind, const float *a,
+                             const float *b, const float *w, float *sum, float *norm, float *out, float *const *y,
+                             const void *epi, int reps, float *us) {
+    ensure_init();
+    if (g_device_count == 0) return GGML_HIP_ERR_UNSUPPORTED;
+    if (nmat < 1 || nmat > 4 || kind < 0 || kind > 2) return fail(GGML_HIP_ERR_INVALID, "bad gemv_norm case");
+    flush_deferred();
+    const int id = g_main_device;
+    HIP_FATAL(hipSetDevice(id));
+    hipStream_t s = g_dev[id].stream;
+    const OpTables &tb = op_tables(id, s);
+    ghip::GemvEpi ep{};
+    if (epi) {
+        memcpy(&ep, epi, sizeof ep);
+        if (ep.glu) ep.table = tb.silu;
+    }
+    int64_t ldy[4];
+    for (int i = 0; i < nmat; i++) ldy[i] = M[i];
+    const ghip::GemvNorm nrm{a, w, sum, norm, out, kind, kind == 2 ? tb.silu : nullptr};
+    auto run = [&]() -> hipError_t {
+        if (kind == 0) return ghip::gemv_q4_0_multi(nmat, W, M, K, b, 1, y, ldy, g_dev[id].info, s);
+        return ghip::gemv_q4_0_multi_norm(nmat, W, M, K, b, nrm, y, ldy, g_dev[id].info, s, epi ? &ep : nullptr);
+    };
+    HIP_RET(run());
+    if (reps > 0) {
+        hipEvent_t e0, e1;
+        HIP_FATAL(GHIP_SYNC(hipEventCreate)(&e0));
+        HIP_FATAL(GHIP_SYNC(hipEventCreate)(&e1));
+        HIP_FATAL(GHIP_SYNC(hipEventRecord)(e0, s));
+        for (int r = 0; r < reps; r++) HIP_RET(run());
+        HIP_FATAL(GHIP_SYNC(hipEventRecord)(e1, s));
+        HIP_FATAL(GHIP_SYNC(hipEventSynchronize)(e1));
+        float ms = 0.0f;
+        HIP_FATAL(hipEventElapsedTime(&ms, e0, e1));
+        if (us) *us = 1000.0f * ms / (float)reps;
+        HIP_FATAL(hipEventDestroy(e0));
+        HIP_FATAL(hipEventDestroy(e1));
+    }
     HIP_FATAL(GHIP_SYNC(hipStreamSynchronize)(s));
     return GGML_HIP_OK;
 }

@@ -539,14 +539,15 @@ bool ggml_hip_compute_forward(struct ggml_compute_params *params_, struct ggml_t
     } else if (hook_seen(t)) {
         flush_deferred();                  // t arrives again: a new graph at the old addresses
     }
-    // with the recorder on, the node's launches on the main stream are recorded and submitted as HIP
-    // graphs (launch.h)
+    // with the recorder on, the node's launches on the main stream are recorded (launch.h): mode 1 submits
+    // them as HIP graphs when the node returns; mode 2's launcher thread issues them on its own, so the ring
+    // stays open across nodes (the main thread never waits for it between nodes: every entry point and
+    // every other HIP call of the backend drains it first, GHIP_SYNC / flush_deferred)
     g_eval_computed = true;
-    const bool use_graph = graph_enabled();
-    if (use_graph) graph_apply_mode();
-    if (use_graph) ghip::rec_enable(g_dev[g_main_device].stream, true);
+    const int gmode = graph_enabled() ? graph_apply_mode() : 0;
+    ghip::rec_enable(g_dev[g_main_device].stream, gmode != 0);
     execute_node(t);
-    if (use_graph) ghip::rec_enable(g_dev[g_main_device].stream, false);
+    if (gmode == 1) ghip::rec_enable(g_dev[g_main_device].stream, false);
     const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     g_host_ns.fetch_add(ns, std::memory_order_relaxed);
     g_op_ns[t->op].fetch_add(ns, std::memory_order_relaxed);

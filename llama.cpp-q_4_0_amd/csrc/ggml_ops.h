@@ -76,6 +76,14 @@ hipError_t op_scale_mask_soft_max_f32(const float *x, float *scaled, float *mask
 hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm, float v, int n_past,
                           const uint16_t *table, int64_t nkv, int64_t nhead, const void *vs, int64_t nb01v, int64_t nb02v,
                           int64_t nout, float *kqv, float *merged, hipStream_t s);
+// the whole decode attention of one query row per head: KQ = K.fp16(q) per head (as op_mul_mat_f16_f32 with
+// N = 1: K rows f16 at nb01k, heads at nb02k; q heads at nb02q, hd <= 256) into LDS, then as op_softmax_kqv;
+// kq / scaled / masked / sm stored by each head's first workgroup unless nullptr (pass one pointer per
+// buffer: the last tensor of an in-place chain)
+hipError_t op_kq_softmax_kqv(const void *ks, int64_t nb01k, int64_t nb02k, const float *q, int64_t nb02q, int hd,
+                             float *kq, float *scaled, float *masked, float *sm, float v, int n_past, const uint16_t *table,
+                             int64_t nkv, int64_t nhead, const void *vs, int64_t nb01v, int64_t nb02v, int64_t nout,
+                             float *kqv, float *merged, hipStream_t s);
 // u = silu(a) -> out = u * b (same shape)
 // mismatches of the direct silu / exp evaluation against the host tables over every finite fp16 input
 // (bad_dev: two zeroed ints on the device; q4_0_device.h lut_silu / lut_exp)

@@ -687,11 +687,25 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max_reg(const float *x,
 // 32 of the head's KQV outputs, 32 lanes per output as k_mul_mat_f16_f32 does.  Workgroup 0 of a
 // head stores the softmax row (and scaled / masked) unless nullptr: the caller passes nullptr for a
 // buffer that aliases kq (the in-place chain), which the other workgroups are still reading.
-constexpr int SM_THREADS = 1024, SM_OUT = SM_THREADS / 32, SM_PF = 16;
+// KQ: the head's KQ row first, in LDS (the whole decode attention in one launch): key j of head i2 is
+// ggml_vec_dot_f16 of K row j (f16, element stride 2 bytes) and fp16(q), the arithmetic of
+// k_mul_mat_f16_f32 (lane l of 32 takes elements l + 32 m in order, the same reduction tree and double
+// tail), one 32-lane group per key; workgroup 0 of the head stores it to kq_out unless nullptr.
+struct AttnKQ {
+    const char *ks;            // K view: key j of head h at ks + h * nb02k + j * nb01k
+    int64_t nb01k, nb02k;
+    const float *q;            // q of head h at q + h * nb02q / 4 (contiguous hd floats)
+    int64_t nb02q;
+    int hd;                    // head dimension, <= SM_HD
+    float *kq_out;
+};
+constexpr int SM_THREADS = 1024, SM_OUT = SM_THREADS / 32, SM_PF = 16, SM_HD = 256;
+// KQM: 0 (kq read from memory) or the K-row elements per lane, ceil(hd / 32) rounded up to 2, 4 or 8
+template <int KQM>
 __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm,
                                                             float v, int n_past, const uint16_t *table, int64_t nkv,
                                                             const char *vs, int64_t nb01v, int64_t nb02v, int64_t nout,
-                                                            int splits, float *kqv, float *merged) {
+                                                            int splits, float *kqv, float *merged, const AttnKQ aq) {
     extern __shared__ float row[];                     // [nkv]
     __shared__ float redf[SM_THREADS / 64];
     __shared__ double redd[SM_THREADS / 64];
@@ -713,8 +727,46 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
 #pragma unroll
     for (int j = 0; j < SM_PF; j++) vpre[j] = xr[min(l + 32 * j, K - 1)];
     const uint16_t vtail = xr[min(np + l, K - 1)];
+    constexpr bool KQ = KQM > 0;
+    if constexpr (KQ) {
+        const int hd = aq.hd, hnp = hd & ~31, htl = hd - hnp, hkl = hd - 1;
+        const float *qr = reinterpret_cast<const float *>(reinterpret_cast<const char *>(aq.q) + i2 * aq.nb02q);
+        float qh[KQM];                                 // fp16(q) of this lane's elements
+#pragma unroll
+        for (int m = 0; m < KQM; m++) qh[m] = h2f_bits(f2h_bits(qr[min(l + 32 * m, hkl)]));
+        const float qt = h2f_bits(f2h_bits(qr[min(hnp + l, hkl)]));
+        for (int64_t j = g; j < nkv; j += SM_THREADS / 32) {
+            const uint16_t *kr = reinterpret_cast<const uint16_t *>(aq.ks + i2 * aq.nb02k + j * aq.nb01k);
+            uint16_t kb[KQM];
+#pragma unroll
+            for (int m = 0; m < KQM; m++) kb[m] = kr[min(l + 32 * m, hkl)];
+            const uint16_t kt = kr[min(hnp + l, hkl)];
+            float acc = 0.0f;
+#pragma unroll
+            for (int m = 0; m < KQM; m++)
+                if (32 * m < hnp) acc = fmaf(h2f_bits(kb[m]), qh[m], acc);
+            const float pt = l < htl ? h2f_bits(kt) * qt : 0.0f;
+            const float p16 = __shfl_xor(acc, 16, 32);
+            const float a = acc + p16;
+            const float p8 = __shfl_xor(a, 8, 32);
+            const float c = a + p8;
+            const float c4 = __shfl_xor(c, 4, 32);
+            const float t0 = c + c4;
+            const float t01 = t0 + __shfl_xor(t0, 1, 32);
+            const float t23 = __shfl(t01, 2, 32);
+            const float res = t01 + t23;
+            double sum = (double)res;
+            for (int e = 0; e < htl; e++) sum += (double)__shfl(pt, e, 32);
+            if (l == 0) {
+                row[j] = (float)sum;
+                if (store && aq.kq_out) aq.kq_out[o + j] = (float)sum;
+            }
+        }
+        __syncthreads();
+    }
+    auto kq_at = [&](int64_t i) { return KQ ? row[i] : kq[o + i]; };
     float mx = -INFINITY;
-    for (int64_t i = tid; i < nkv; i += SM_THREADS) mx = fmaxf(mx, i > n_past ? -INFINITY : kq[o + i] * v);
+    for (int64_t i = tid; i < nkv; i += SM_THREADS) mx = fmaxf(mx, i > n_past ? -INFINITY : kq_at(i) * v);
     mx = wave_max_f(mx);
     if (lane == 0) redf[wave] = mx;
     __syncthreads();
@@ -722,7 +774,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     for (int w = 1; w < SM_THREADS / 64; w++) mx = fmaxf(mx, redf[w]);
     double ssum = 0.0;
     for (int64_t i = tid; i < nkv; i += SM_THREADS) {
-        const float sv = kq[o + i] * v;
+        const float sv = kq_at(i) * v;
         const float m = i > n_past ? -INFINITY : sv;
         float e = 0.0f;
         if (m != -INFINITY) {
@@ -1095,8 +1147,30 @@ hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *
                           int64_t nout, float *kqv, float *merged, hipStream_t s) {
     if (nhead <= 0 || nkv <= 0 || nout <= 0) return hipSuccess;
     const int splits = (int)((nout + SM_OUT - 1) / SM_OUT);
-    launch_k(k_softmax_kqv, dim3((unsigned)(nhead * splits)), dim3(SM_THREADS), (size_t)nkv * 4, s, kq, scaled,
-                       masked, sm, v, n_past, table, nkv, (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged);
+    launch_k(k_softmax_kqv<0>, dim3((unsigned)(nhead * splits)), dim3(SM_THREADS), (size_t)nkv * 4, s, kq, scaled,
+             masked, sm, v, n_past, table, nkv, (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, AttnKQ{});
+    return hipGetLastError();
+}
+
+hipError_t op_kq_softmax_kqv(const void *ks, int64_t nb01k, int64_t nb02k, const float *q, int64_t nb02q, int hd,
+                             float *kq, float *scaled, float *masked, float *sm, float v, int n_past, const uint16_t *table,
+                             int64_t nkv, int64_t nhead, const void *vs, int64_t nb01v, int64_t nb02v, int64_t nout,
+                             float *kqv, float *merged, hipStream_t s) {
+    if (nhead <= 0 || nkv <= 0 || nout <= 0) return hipSuccess;
+    if (hd < 1 || hd > SM_HD) return hipErrorInvalidValue;
+    const int splits = (int)((nout + SM_OUT - 1) / SM_OUT);
+    const AttnKQ aq{(const char *)ks, nb01k, nb02k, q, nb02q, hd, kq};
+    const dim3 grid((unsigned)(nhead * splits));
+    const size_t lds = (size_t)nkv * 4;
+    if (hd <= 64)
+        launch_k(k_softmax_kqv<2>, grid, dim3(SM_THREADS), lds, s, nullptr, scaled, masked, sm, v, n_past, table, nkv,
+                 (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, aq);
+    else if (hd <= 128)
+        launch_k(k_softmax_kqv<4>, grid, dim3(SM_THREADS), lds, s, nullptr, scaled, masked, sm, v, n_past, table, nkv,
+                 (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, aq);
+    else
+        launch_k(k_softmax_kqv<8>, grid, dim3(SM_THREADS), lds, s, nullptr, scaled, masked, sm, v, n_past, table, nkv,
+                 (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, aq);
     return hipGetLastError();
 }
 

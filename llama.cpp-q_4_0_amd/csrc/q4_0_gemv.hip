@@ -717,8 +717,7 @@ static hipError_t launch_gemv_w(const GemvMats &m, int64_t K, const float *x, co
         // strided rows (row r ^ 1 is the same item of wave ^ 1 in the same workgroup) or, for the
         // interleaved (gate, up) rows, blocked whole pairs per workgroup; every output of the workgroup
         // parked in LDS, pairs never straddling two matrices
-        static const int glu_map = env_int("GGML_HIP_GEMV_GLU_MAP", 2);
-        map = EPI == 2 && glu_map == 2 ? 2 : 0;
+        map = EPI == 2 && map_env != 0 ? 2 : 0;     // GGML_HIP_GEMV_MAP=0: strided pairs for w1|w3 too
         if (EPI == 2 && (m.n != 2 || 2 * m.row_begin[1] != m.row_begin[2])) return hipErrorInvalidValue;
         for (int i = 1; i <= m.n; i++)
             if (m.row_begin[i] & 1) return hipErrorInvalidValue;

@@ -31,7 +31,7 @@ pytestmark = [pytest.mark.gpu,
 OPS = json.load(open(os.path.join(GOLD, "ggml_op_enum.json")))
 
 
-N_FUSED = 14  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
+N_FUSED = 15  # ggml-hip.h, ggml_hip_debug_op_stats: fused launches per chain in the last slots
 
 
 def op_stats(L, reset=True, fused=False):
@@ -163,6 +163,7 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode
         assert fused[3] + fused[7] >= evals * hp["n_layer"], fused   # rope->cpy alone or in a batch
         assert fused[6] >= 2 * n_decode * hp["n_layer"], fused
         assert fused[7] >= n_decode * hp["n_layer"], fused      # rope K->cache, V->cache, rope Q
+        assert fused[14] >= n_decode * hp["n_layer"], fused     # KQ inside the soft_max -> KQV launch
     else:
         assert (fused == 0).all(), fused
 
@@ -284,6 +285,42 @@ def test_gemv_epilogue_bitwise_vs_elem_batch(tmp_path, hp, n_prompt, n_decode):
     assert np.array_equal(ran1, ran0)                                  # every node still counted once
 
 
+@pytest.mark.parametrize("exact", [0, 1], ids=["fast", "exact"])
+@pytest.mark.parametrize("hp,n_prompt,n_decode", [(HP128, 40, 60), (G.HP, 8, 40)], ids=["head128", "head64"])
+def test_kq_fold_bitwise_vs_own_launch(tmp_path, hp, n_prompt, n_decode, exact):
+    """The decode KQ (f16 K cache view . fp16(q), one query row per head) computed by the scale ->
+    diag_mask_inf -> soft_max -> KQV -> merge launch (op_kq_softmax_kqv, the head's KQ row in LDS): the
+    same logits bit for bit as KQ's own launch (k_mul_mat_f16_f32) before the chain, in both modes, and
+    the fold fires for every layer of every decode eval."""
+    L = ggml_hip.load()
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp, hp=hp)
+    nv = hp["n_vocab"]
+    lib = ctypes.CDLL(HIP_LIB)
+    lib.refllama_bench.restype = ctypes.c_int
+    lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    L.ggml_hip_debug_set_kq_fold.argtypes = [ctypes.c_int]
+    prev = L.ggml_hip_get_exact()
+    ggml_hip.check(L.ggml_hip_set_exact(exact), "set_exact")
+    out = {}
+    try:
+        for fold in (1, 0):
+            ggml_hip.check(L.ggml_hip_debug_set_kq_fold(fold), "set_kq_fold")
+            op_stats(L)
+            lg = np.zeros(nv, np.float32)
+            res = np.zeros(3, np.float64)
+            assert lib.refllama_bench(mp.encode(), n_prompt, n_decode, 1, 99, 1024, 1, res.ctypes.data, lg.ctypes.data) == nv
+            out[fold] = (lg, op_stats(L, reset=False, fused=True))
+    finally:
+        L.ggml_hip_set_exact(prev)
+        L.ggml_hip_debug_set_kq_fold(1)
+    assert np.isfinite(out[1][0]).all()
+    assert np.array_equal(out[1][0].view(np.uint32), out[0][0].view(np.uint32))
+    (ran1, f1), (ran0, f0) = out[1][1], out[0][1]
+    assert f1[14] >= hp["n_layer"] * n_decode and f0[14] == 0, (f1, f0)
+    assert np.array_equal(ran1, ran0)
+
+
 @pytest.mark.parametrize("n_prompt", [300, 97])
 def test_prefill_x_image_fold_bitwise_vs_prep(tmp_path, n_prompt):
     """Prefill (N > 64 tokens) at full offload: the [add ->] rms_norm -> mul and silu -> mul chains whose
@@ -363,6 +400,6 @@ def test_launch_recorder_bitwise_vs_eager(tmp_path, exact, mode):
     if mode == 2:
         return
     runs, kernels, updated, built = stats[1][:4]
-    assert runs >= 120 and kernels >= 120 * 10 * hp["n_layer"], stats[1]
+    assert runs >= 120 and kernels >= 120 * 5 * hp["n_layer"], stats[1]   # >= 5 launches per decode layer
     assert updated > 0, stats[1]                  # n_past-dependent nodes change every step
     assert built * 10 < runs, stats[1]            # replayed, not re-instantiated per run

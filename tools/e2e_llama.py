@@ -143,10 +143,13 @@ def main():
             # "-noepi": the decode q|k|v GEMV epilogue off (the held rope / copy nodes as their own batch)
             L.ggml_hip_debug_set_epi_fold.argtypes = [ctypes.c_int]
             gh.check(L.ggml_hip_debug_set_epi_fold(0 if "-noepi" in mode else 1))
+            # "-nokq": the decode KQ as its own launch
+            L.ggml_hip_debug_set_kq_fold.argtypes = [ctypes.c_int]
+            gh.check(L.ggml_hip_debug_set_kq_fold(0 if "-nokq" in mode else 1))
             g0 = np.zeros(5, np.int64)
             L.ggml_hip_debug_graph_stats(g0.ctypes.data, 0)
             L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-            st = np.zeros(2 * 68 + 1 + 14, np.int64)
+            st = np.zeros(2 * 68 + 1 + 15, np.int64)
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)
             L.ggml_hip_debug_launch_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
             ls = np.zeros(2, np.int64)

@@ -460,6 +460,48 @@ int ggml_hip_debug_gemv_norm(int nmat, const void *const *W, const int64_t *M, i
     return GGML_HIP_OK;
 }
 
+// debug: the decode attention of one query row per head on device pointers: fused = 1 the one launch
+// (op_kq_softmax_kqv), 0 KQ's own launch (op_mul_mat_f16_f32) then op_softmax_kqv; kq receives KQ (fused = 0) or
+// the softmax row (both: sm), kqv the [nhead][nout] output.  reps > 0: timed as ggml_hip_debug_gemv_norm.
+int ggml_hip_debug_attn_decode(int fused, const void *ks, int64_t nb01k, int64_t nb02k, const float *q, int64_t nb02q,
+                               int hd, const void *vs, int64_t nb01v, int64_t nb02v, int64_t nkv, int64_t nhead,
+                               int64_t nout, int n_past, float scale, float *kq, float *sm, float *kqv, int reps, float *us) {
+    ensure_init();
+    if (g_device_count == 0) return GGML_HIP_ERR_UNSUPPORTED;
+    flush_deferred();
+    const int id = g_main_device;
+    HIP_FATAL(hipSetDevice(id));
+    hipStream_t s = g_dev[id].stream;
+    const OpTables &tb = op_tables(id, s);
+    auto run = [&]() -> hipError_t {
+        if (fused)
+            return ghip::op_kq_softmax_kqv(ks, nb01k, nb02k, q, nb02q, hd, nullptr, nullptr, nullptr, sm, scale, n_past,
+                                           tb.exp, nkv, nhead, vs, nb01v, nb02v, nout, kqv, nullptr, s);
+        hipError_t e = ghip::op_mul_mat_f16_f32(ks, q, kq, hd, nkv, 1, nhead, nb01k, nb02k, nb02q, nb02q, s, nullptr,
+                                                 exact_mode() ? -1 : -2);
+        if (e != hipSuccess) return e;
+        return ghip::op_softmax_kqv(kq, nullptr, nullptr, sm, scale, n_past, tb.exp, nkv, nhead, vs, nb01v, nb02v, nout,
+                                    kqv, nullptr, s);
+    };
+    HIP_RET(run());
+    if (reps > 0) {
+        hipEvent_t e0, e1;
+        HIP_FATAL(GHIP_SYNC(hipEventCreate)(&e0));
+        HIP_FATAL(GHIP_SYNC(hipEventCreate)(&e1));
+        HIP_FATAL(GHIP_SYNC(hipEventRecord)(e0, s));
+        for (int r = 0; r < reps; r++) HIP_RET(run());
+        HIP_FATAL(GHIP_SYNC(hipEventRecord)(e1, s));
+        HIP_FATAL(GHIP_SYNC(hipEventSynchronize)(e1));
+        float ms = 0.0f;
+        HIP_FATAL(hipEventElapsedTime(&ms, e0, e1));
+        if (us) *us = 1000.0f * ms / (float)reps;
+        HIP_FATAL(hipEventDestroy(e0));
+        HIP_FATAL(hipEventDestroy(e1));
+    }
+    HIP_FATAL(GHIP_SYNC(hipStreamSynchronize)(s));
+    return GGML_HIP_OK;
+}
+
 // debug: the f16 x f32 mul_mat of the attention on device pointers (tests/test_gpu_f16_mul_mat.py):
 // tiled 0 = one 32-lane group per output, 1 = the LDS-tiled kernel, -1 = the backend's choice (bitwise
 // kernels), 2 = the fast-mode MFMA kernel, -2 = the backend's fast-mode choice

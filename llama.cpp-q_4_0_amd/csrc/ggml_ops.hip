@@ -735,31 +735,43 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
 #pragma unroll
         for (int m = 0; m < KQM; m++) qh[m] = h2f_bits(f2h_bits(qr[min(l + 32 * m, hkl)]));
         const float qt = h2f_bits(f2h_bits(qr[min(hnp + l, hkl)]));
-        for (int64_t j = g; j < nkv; j += SM_THREADS / 32) {
-            const uint16_t *kr = reinterpret_cast<const uint16_t *>(aq.ks + i2 * aq.nb02k + j * aq.nb01k);
-            uint16_t kb[KQM];
+        // KQ_U keys per group in flight: every key's K-row loads (unconditional, clamped indices) are issued
+        // before the first key's products, so a group waits for one memory round trip per KQ_U keys
+        constexpr int KQ_U = 4, G = SM_THREADS / 32;
+        for (int64_t j0 = g; j0 < nkv; j0 += KQ_U * G) {
+            uint16_t kb[KQ_U][KQM], kt[KQ_U];
 #pragma unroll
-            for (int m = 0; m < KQM; m++) kb[m] = kr[min(l + 32 * m, hkl)];
-            const uint16_t kt = kr[min(hnp + l, hkl)];
-            float acc = 0.0f;
+            for (int u = 0; u < KQ_U; u++) {
+                const int64_t jc = min(j0 + (int64_t)u * G, nkv - 1);
+                const uint16_t *kr = reinterpret_cast<const uint16_t *>(aq.ks + i2 * aq.nb02k + jc * aq.nb01k);
 #pragma unroll
-            for (int m = 0; m < KQM; m++)
-                if (32 * m < hnp) acc = fmaf(h2f_bits(kb[m]), qh[m], acc);
-            const float pt = l < htl ? h2f_bits(kt) * qt : 0.0f;
-            const float p16 = __shfl_xor(acc, 16, 32);
-            const float a = acc + p16;
-            const float p8 = __shfl_xor(a, 8, 32);
-            const float c = a + p8;
-            const float c4 = __shfl_xor(c, 4, 32);
-            const float t0 = c + c4;
-            const float t01 = t0 + __shfl_xor(t0, 1, 32);
-            const float t23 = __shfl(t01, 2, 32);
-            const float res = t01 + t23;
-            double sum = (double)res;
-            for (int e = 0; e < htl; e++) sum += (double)__shfl(pt, e, 32);
-            if (l == 0) {
-                row[j] = (float)sum;
-                if (store && aq.kq_out) aq.kq_out[o + j] = (float)sum;
+                for (int m = 0; m < KQM; m++) kb[u][m] = kr[min(l + 32 * m, hkl)];
+                kt[u] = kr[min(hnp + l, hkl)];
+            }
+#pragma unroll
+            for (int u = 0; u < KQ_U; u++) {
+                const int64_t j = j0 + (int64_t)u * G;
+                if (j >= nkv) break;                   // uniform per 32-lane group
+                float acc = 0.0f;
+#pragma unroll
+                for (int m = 0; m < KQM; m++)
+                    if (32 * m < hnp) acc = fmaf(h2f_bits(kb[u][m]), qh[m], acc);
+                const float pt = l < htl ? h2f_bits(kt[u]) * qt : 0.0f;
+                const float p16 = __shfl_xor(acc, 16, 32);
+                const float a = acc + p16;
+                const float p8 = __shfl_xor(a, 8, 32);
+                const float c = a + p8;
+                const float c4 = __shfl_xor(c, 4, 32);
+                const float t0 = c + c4;
+                const float t01 = t0 + __shfl_xor(t0, 1, 32);
+                const float t23 = __shfl(t01, 2, 32);
+                const float res = t01 + t23;
+                double sum = (double)res;
+                for (int e = 0; e < htl; e++) sum += (double)__shfl(pt, e, 32);
+                if (l == 0) {
+                    row[j] = (float)sum;
+                    if (store && aq.kq_out) aq.kq_out[o + j] = (float)sum;
+                }
             }
         }
         __syncthreads();

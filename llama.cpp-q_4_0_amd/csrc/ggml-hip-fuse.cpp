@@ -280,9 +280,13 @@ bool kq_holdable(const tensor *t) {
            Q->ne[1] == 1 && K->ne[0] == Q->ne[0] && K->ne[0] >= 1 && K->ne[0] <= 256 && K->ne[2] == Q->ne[2] &&
            t->ne[0] == K->ne[1] && t->ne[1] == 1 && t->ne[2] == K->ne[2] && t->ne[3] == 1 && (Q->nb[2] & 3) == 0;
 }
-// ... whose output the held soft_max chain reads row for row (sm: the chain's soft_max node)
+// ... whose output the held soft_max chain reads row for row (sm: the chain's soft_max node), for rows up to
+// GGML_HIP_KQ_FOLD_MAX keys (default 192): each of a head's workgroups computes the whole KQ row, so past a
+// few hundred keys KQ's own launch over every CU is faster (tools/attn_ab.py: 7.3 vs 7.5 us at 136 keys,
+// 8.3 vs 7.6 at 256, 12.2 vs 9.3 at 512)
 bool kq_chain_ok(const tensor *kqn, const tensor *sm) {
-    return sm->ne[0] == kqn->ne[0] && sm->ne[1] == 1 && sm->ne[2] == kqn->ne[2];
+    static const int64_t max_kv = getenv("GGML_HIP_KQ_FOLD_MAX") ? atoll(getenv("GGML_HIP_KQ_FOLD_MAX")) : 192;
+    return sm->ne[0] == kqn->ne[0] && sm->ne[1] == 1 && sm->ne[2] == kqn->ne[2] && kqn->ne[0] <= max_kv;
 }
 
 // t arrives while a chain is pending: extend the chain, complete it in one launch, or let a q4_0

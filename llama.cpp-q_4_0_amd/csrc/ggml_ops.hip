@@ -700,6 +700,9 @@ struct AttnKQ {
     float *kq_out;
 };
 constexpr int SM_THREADS = 1024, SM_OUT = SM_THREADS / 32, SM_PF = 16, SM_HD = 256;
+#ifndef ATTN_KQ_U
+#define ATTN_KQ_U 4         // keys in flight per 32-lane group in the fused KQ phase
+#endif
 // KQM: 0 (kq read from memory) or the K-row elements per lane, ceil(hd / 32) rounded up to 2, 4 or 8
 template <int KQM>
 __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm,
@@ -737,7 +740,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
         const float qt = h2f_bits(f2h_bits(qr[min(hnp + l, hkl)]));
         // KQ_U keys per group in flight: every key's K-row loads (unconditional, clamped indices) are issued
         // before the first key's products, so a group waits for one memory round trip per KQ_U keys
-        constexpr int KQ_U = 4, G = SM_THREADS / 32;
+        constexpr int KQ_U = ATTN_KQ_U, G = SM_THREADS / 32;
         for (int64_t j0 = g; j0 < nkv; j0 += KQ_U * G) {
             uint16_t kb[KQ_U][KQM], kt[KQ_U];
 #pragma unroll

@@ -21,7 +21,11 @@ namespace ghip {
 // items) in launch_gemv_w / launch_gemv; every policy gives bitwise-identical results.
 
 static constexpr int GEMV_LDS_MAX = 64 * 1024;
-static constexpr int GEMV_XPRO = 4;         // x float4 loads in flight per x-wave thread in the prologue
+static constexpr int GEMV_XPRO = 4;
+#ifndef GEMV_XPRO_N
+#define GEMV_XPRO_N 2       // the same for the norm prologue (PRO 1): x-waves = K / (256 * GEMV_XPRO_N); 2: 8 x-waves at
+                            // K = 4096 (profiles/r05_gemv_norm_xwaves_ab.txt: q|k|v 0.3 us faster than 4)
+#endif         // x float4 loads in flight per x-wave thread in the prologue
 static constexpr int GEMV_WAVES = 16;       // waves per workgroup
 static constexpr int GEMV_MAXMAT = 4;       // sibling matrices per launch
 
@@ -334,24 +338,24 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
         }
     } else if constexpr (PRO == 1) {
         // [add ->] rms_norm -> mul fused into the x prologue (NT == 1, one round of x-waves: the
-        // launcher checks K <= 16 * 64 * 4 * GEMV_XPRO).  The x-waves hold the row in registers, sum
+        // launcher checks K <= 16 * 64 * 4 * GEMV_XPRO_N).  The x-waves hold the row in registers, sum
         // its squares in double (order-free in practice, as k_row_norm4's), exchange the per-wave
         // sums through LDS (one extra workgroup barrier), then scale, multiply by the norm weight and
         // quantize; workgroup 0 also stores the chain's tensors.
         static_assert(NT == 1, "norm prologue: decode x-wave form only");
         double *npart = reinterpret_cast<double *>(xs + NT * nb);
-        const int XW = (total + 64 * GEMV_XPRO - 1) / (64 * GEMV_XPRO);
+        const int XW = (total + 64 * GEMV_XPRO_N - 1) / (64 * GEMV_XPRO_N);
         const int XT = XW * 64;
         const GemvNorm nrm = tail.nrm;
-        float4 v[GEMV_XPRO];
-        u32x4 rg[GEMV_XPRO];                                   // the norm weight, loaded with x
+        float4 v[GEMV_XPRO_N];
+        u32x4 rg[GEMV_XPRO_N];                                   // the norm weight, loaded with x
         if (wave < XW) {
             const __amdgpu_buffer_rsrc_t ar = make_rsrc(nrm.a ? (const void *)nrm.a : (const void *)x,
                                                         nrm.a ? (uint32_t)total * 16u : 0u);
             const __amdgpu_buffer_rsrc_t gr = make_rsrc(nrm.w, (uint32_t)total * 16u);
-            u32x4 rb[GEMV_XPRO], ra[GEMV_XPRO];
+            u32x4 rb[GEMV_XPRO_N], ra[GEMV_XPRO_N];
 #pragma unroll
-            for (int i = 0; i < GEMV_XPRO; i++) {
+            for (int i = 0; i < GEMV_XPRO_N; i++) {
                 rb[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * (tid + i * XT), 0, 0);
                 ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ar, 16 * (tid + i * XT), 0, 0);
                 rg[i] = __builtin_amdgcn_raw_buffer_load_b128(gr, 16 * (tid + i * XT), 0, 0);
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
             }
             double ss = 0.0;
 #pragma unroll
-            for (int i = 0; i < GEMV_XPRO; i++) {
+            for (int i = 0; i < GEMV_XPRO_N; i++) {
                 float4 b4 = make_float4(__uint_as_float(rb[i].x), __uint_as_float(rb[i].y), __uint_as_float(rb[i].z),
                                         __uint_as_float(rb[i].w));
                 if (nrm.a)                                     // a + b, as k_add_f32 / k_row_norm4
@@ -860,7 +864,7 @@ hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M
                                 const GemvNorm &nrm, float *const *y, const int64_t *ldy, const DeviceInfo &dev,
                                 hipStream_t s, const GemvEpi *epi) {
     // one round of x-waves holds the row: K / 4 float4 <= 16 waves * 64 lanes * GEMV_XPRO
-    if (nmat < 1 || nmat > GEMV_MAXMAT || K % 64 != 0 || K / 4 > 16 * 64 * GEMV_XPRO || !b ||
+    if (nmat < 1 || nmat > GEMV_MAXMAT || K % 64 != 0 || K / 4 > 16 * 64 * (nrm.kind == 1 ? GEMV_XPRO_N : GEMV_XPRO) || !b ||
         (nrm.kind == 1 && !nrm.w) || (nrm.kind == 2 && (!nrm.a || !nrm.table)) || (nrm.kind != 1 && nrm.kind != 2))
         return hipErrorInvalidValue;
     GemvMats m{};

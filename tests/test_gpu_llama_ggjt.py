@@ -163,7 +163,9 @@ def test_long_decode_full_offload_exact_bitwise(tmp_path, hp, n_prompt, n_decode
         assert fused[3] + fused[7] >= evals * hp["n_layer"], fused   # rope->cpy alone or in a batch
         assert fused[6] >= 2 * n_decode * hp["n_layer"], fused
         assert fused[7] >= n_decode * hp["n_layer"], fused      # rope K->cache, V->cache, rope Q
-        assert fused[14] >= n_decode * hp["n_layer"], fused     # KQ inside the soft_max -> KQV launch
+        # KQ inside the soft_max -> KQV launch while the row has <= 192 keys (GGML_HIP_KQ_FOLD_MAX), own launch after
+        short = sum(1 for i in range(n_decode) if n_prompt + i + 1 <= 192)
+        assert fused[14] >= short * hp["n_layer"], fused
     else:
         assert (fused == 0).all(), fused
 

@@ -13,11 +13,14 @@ step() {   # step <name> <seconds> <cmd...>  (counter passes: SIGKILL at the lim
   echo "$name rc=$rc"
   case $rc in 0|1) return 0;; *) exit $rc;; esac
 }
-if [ -z "$SKIP_TESTS" ]; then
+# PART=tests | bench | e2e (one gpurun call each; default: all)
+PART=${PART:-all}
+if [ $PART = all -o $PART = tests ]; then
   step gputest 900 python -u -m pytest tests -m gpu -v -rs --timeout 300 --timeout-method thread
   tail -3 $O/gputest.log
   step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 fi
+if [ $PART = all -o $PART = bench ]; then
 step bench 480 python bench.py
 tail -1 $O/bench.log | cut -c1-300
 step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-extra
@@ -50,6 +53,9 @@ if "GRBM_GUI_ACTIVE" in g and "SQ_VALU_MFMA_BUSY_CYCLES" in g:
           f"WAIT_INST_ANY / WAVE_CYCLES {g.get('SQ_WAIT_INST_ANY', 0) / max(1, g.get('SQ_WAVE_CYCLES', 1)):.3f}")
 PY
 cat $O/gemm9_pmc.txt
+fi
+if [ $PART = all -o $PART = e2e ]; then
 # the hook path end to end: the reference llama.cpp at full offload (LLaMA-7B shape), fast / exact, with a kernel trace
 step e2e 700 python tools/e2e_llama.py --decode 128 --modes fast,exact --out $O/e2e_7b.json
 step e2e_prof 600 rocprofv3 --kernel-trace --stats -d $O/prof_e2e -o e2e --output-format csv -- python3 tools/e2e_llama.py --decode 64 --no-cpu --modes fast
+fi

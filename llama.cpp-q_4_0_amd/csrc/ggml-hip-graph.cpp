@@ -12,6 +12,7 @@
 //   * the nodes of a run form one dependency chain: the same order as the stream would execute them.
 // The results are the kernels' own, so every bitwise test of the eager path holds for the recorded one.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <atomic>
 #include <chrono>
@@ -84,7 +85,33 @@ Launcher &launcher() {
     static Launcher *l = new Launcher;   // never destroyed: the worker may outlive static destructors
     return *l;
 }
-void launcher_main(Launcher *L) {
+// the launcher's CPU: GGML_HIP_LAUNCHER_CPU=n pins it to CPU n, -1 leaves it to the scheduler; by default
+// the first allowed CPU that is neither the starting thread's nor its SMT sibling (tools/launch_thread_cost.hip:
+// 2.75 vs 2.87 us per hipLaunchKernel pinned vs free)
+void launcher_pin(int main_cpu) {
+    const char *e = getenv("GGML_HIP_LAUNCHER_CPU");
+    const int want = e ? atoi(e) : -2;
+    if (want == -1) return;
+    cpu_set_t allowed, one;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+    int sib[2] = {-1, -1};
+    char path[128];
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", main_cpu);
+    if (FILE *f = fopen(path, "r")) {
+        if (fscanf(f, "%d%*[,-]%d", &sib[0], &sib[1]) < 1) sib[0] = -1;
+        fclose(f);
+    }
+    for (int c = 0; c < CPU_SETSIZE; c++) {
+        const bool ok = want >= 0 ? c == want : (CPU_ISSET(c, &allowed) && c != main_cpu && c != sib[0] && c != sib[1]);
+        if (!ok) continue;
+        CPU_ZERO(&one);
+        CPU_SET(c, &one);
+        (void)sched_setaffinity(0, sizeof one, &one);
+        return;
+    }
+}
+void launcher_main(Launcher *L, int main_cpu) {
+    launcher_pin(main_cpu);
     int cur_dev = L->device;
     (void)hipSetDevice(cur_dev);
     void *argv[MAX_ARGS];
@@ -270,7 +297,7 @@ void async_push(const void *fn, dim3 grid, dim3 block, size_t lds, int nargs, vo
         L.stream = r.stream;
         (void)hipGetDevice(&L.device);
         L.started = true;
-        std::thread(launcher_main, &L).detach();
+        std::thread(launcher_main, &L, sched_getcpu()).detach();
     }
     if (L.stream != r.stream) {                // the worker serves one stream: drain, then switch
         while (L.tail.load(std::memory_order_acquire) != L.head.load(std::memory_order_relaxed)) std::this_thread::yield();

@@ -691,6 +691,16 @@ __global__ __launch_bounds__(TPB) void k_scale_mask_soft_max_reg(const float *x,
 // ggml_vec_dot_f16 of K row j (f16, element stride 2 bytes) and fp16(q), the arithmetic of
 // k_mul_mat_f16_f32 (lane l of 32 takes elements l + 32 m in order, the same reduction tree and double
 // tail), one 32-lane group per key; workgroup 0 of the head stores it to kq_out unless nullptr.
+#ifdef ATTN_STAMPS       // diagnostic builds only: per workgroup s_memrealtime at the phase boundaries
+__device__ uint64_t *g_attn_stamps = nullptr;
+#define ATTN_STAMP(k)                                                                                 \
+    if (g_attn_stamps && threadIdx.x == 0) {                                                          \
+        volatile uint64_t *st_ = g_attn_stamps + (uint64_t)blockIdx.x * 8;                            \
+        st_[k] = __builtin_amdgcn_s_memrealtime();                                                    \
+    }
+#else
+#define ATTN_STAMP(k)
+#endif
 struct AttnKQ {
     const char *ks;            // K view: key j of head h at ks + h * nb02k + j * nb01k
     int64_t nb01k, nb02k;
@@ -717,6 +727,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     const int tid = threadIdx.x, g = tid >> 5, l = tid & 31, wave = tid >> 6, lane = tid & 63;
     const int64_t o = i2 * nkv;
     const bool store = part == 0;
+    ATTN_STAMP(0)
     // this lane's first SM_PF V^T values and the row's tail (K % 32 values, one per lane) are loaded
     // before the softmax, so their latency runs under it: unconditional loads of clamped (valid)
     // addresses, so they issue back to back (a load under a branch waits at the join); the products
@@ -726,6 +737,9 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     const uint16_t *xr = (const uint16_t *)(vs + i2 * nb02v + (live ? r : 0) * nb01v);
     const int K = (int)nkv;
     const int np = K & ~31, tl = K - np;
+    // (measured, tools/attn_stamps.py: issued after the K row or after the KQ barrier instead, the fused
+    // launch is 0.3-0.4 us longer; the row's max folded into the KQ phase saves its softmax pass but costs
+    // as much in the KQ phase)
     uint16_t vpre[SM_PF];
 #pragma unroll
     for (int j = 0; j < SM_PF; j++) vpre[j] = xr[min(l + 32 * j, K - 1)];
@@ -779,6 +793,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
         }
         __syncthreads();
     }
+    ATTN_STAMP(1)
     auto kq_at = [&](int64_t i) { return KQ ? row[i] : kq[o + i]; };
     float mx = -INFINITY;
     for (int64_t i = tid; i < nkv; i += SM_THREADS) mx = fmaxf(mx, i > n_past ? -INFINITY : kq_at(i) * v);
@@ -814,6 +829,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
         if (store && sm) sm[o + i] = pv;
     }
     __syncthreads();
+    ATTN_STAMP(2)
     // KQV output r of this head: V^T row r (nkv f16) . fp16(softmax row)
     if (!live) return;
     float acc = 0.0f;
@@ -849,6 +865,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
         kqv[i2 * nout + r] = (float)sum;
         if (merged) merged[i2 * nout + r] = (float)sum;
     }
+    ATTN_STAMP(3)
 }
 
 // row of workgroup i for the image producers: the 8 rows of octet q = 8 * (j / 8) + i % 8 (j = i / 8)
@@ -1166,6 +1183,12 @@ hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *
              masked, sm, v, n_past, table, nkv, (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, AttnKQ{});
     return hipGetLastError();
 }
+
+#ifdef ATTN_STAMPS
+extern "C" int ggml_hip_debug_attn_stamps(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t op_kq_softmax_kqv(const void *ks, int64_t nb01k, int64_t nb02k, const float *q, int64_t nb02q, int hd,
                              float *kq, float *scaled, float *masked, float *sm, float v, int n_past, const uint16_t *table,

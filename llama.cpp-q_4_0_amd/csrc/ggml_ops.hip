@@ -748,15 +748,17 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     if constexpr (KQ) {
         const int hd = aq.hd, hnp = hd & ~31, htl = hd - hnp, hkl = hd - 1;
         const float *qr = reinterpret_cast<const float *>(reinterpret_cast<const char *>(aq.q) + i2 * aq.nb02q);
-        float qh[KQM];                                 // fp16(q) of this lane's elements
+        // q's raw values and the first KQ_U keys' K-row loads are all issued before q's fp16 conversion
+        // (f2h_bits' opaque barrier waits for its operand): one memory round trip, not two
+        float qv[KQM];
 #pragma unroll
-        for (int m = 0; m < KQM; m++) qh[m] = h2f_bits(f2h_bits(qr[min(l + 32 * m, hkl)]));
-        const float qt = h2f_bits(f2h_bits(qr[min(hnp + l, hkl)]));
+        for (int m = 0; m < KQM; m++) qv[m] = qr[min(l + 32 * m, hkl)];
+        const float qtv = qr[min(hnp + l, hkl)];
         // KQ_U keys per group in flight: every key's K-row loads (unconditional, clamped indices) are issued
         // before the first key's products, so a group waits for one memory round trip per KQ_U keys
         constexpr int KQ_U = ATTN_KQ_U, G = SM_THREADS / 32;
-        for (int64_t j0 = g; j0 < nkv; j0 += KQ_U * G) {
-            uint16_t kb[KQ_U][KQM], kt[KQ_U];
+        uint16_t kb[KQ_U][KQM], kt[KQ_U];
+        auto load_keys = [&](int64_t j0) __attribute__((always_inline)) {
 #pragma unroll
             for (int u = 0; u < KQ_U; u++) {
                 const int64_t jc = min(j0 + (int64_t)u * G, nkv - 1);
@@ -765,6 +767,14 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
                 for (int m = 0; m < KQM; m++) kb[u][m] = kr[min(l + 32 * m, hkl)];
                 kt[u] = kr[min(hnp + l, hkl)];
             }
+        };
+        load_keys(g);
+        float qh[KQM];                                 // fp16(q) of this lane's elements
+#pragma unroll
+        for (int m = 0; m < KQM; m++) qh[m] = h2f_bits(f2h_bits(qv[m]));
+        const float qt = h2f_bits(f2h_bits(qtv));
+        for (int64_t j0 = g; j0 < nkv; j0 += KQ_U * G) {
+            if (j0 != g) load_keys(j0);
 #pragma unroll
             for (int u = 0; u < KQ_U; u++) {
                 const int64_t j = j0 + (int64_t)u * G;

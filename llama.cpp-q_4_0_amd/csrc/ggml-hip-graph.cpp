@@ -117,10 +117,18 @@ void launcher_main(Launcher *L, int main_cpu) {
     void *argv[MAX_ARGS];
     for (;;) {
         uint64_t t = L->tail.load(std::memory_order_relaxed);
+        // spin (pause, no syscalls) through an eval and the caller's ~0.7 ms between evals, then sleep:
+        // (profiles/r05_e2e_launcher_spin_ab.txt: the thread mode as a whole stays box-dependent, eager is the default)
+        static const long spin_us = getenv("GGML_HIP_LAUNCHER_SPIN_US") ? atol(getenv("GGML_HIP_LAUNCHER_SPIN_US")) : 2000;
+        const auto t_idle = std::chrono::steady_clock::now();
         int spins = 0;
         while (L->head.load(std::memory_order_acquire) == t) {
-            if (++spins < 20000) {
-                std::this_thread::yield();
+            if ((++spins & 63) != 0 ||
+                std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t_idle).count() <
+                    spin_us) {
+#if defined(__x86_64__)
+                __builtin_ia32_pause();
+#endif
                 continue;
             }
             std::unique_lock<std::mutex> lk(L->mu);

@@ -47,8 +47,10 @@ EXTRA_CONFIGS = [
     ("LLaMA-13B decode (config 4 shapes, 1 GPU)", 40,
      [("wq", 5120, 5120), ("wk", 5120, 5120), ("wv", 5120, 5120), ("wo", 5120, 5120),
       ("w1", 5120, 13824), ("w3", 5120, 13824), ("w2", 13824, 5120)], [[0, 1, 2], [3], [4, 5], [6]]),
+    # Falcon-7B runs attention and MLP in parallel (parallel_attn = 1, arch/falcon/falcon.cpp:1334-1355): the
+    # fused qkv and the MLP's fc both read the layer's one layer-norm output (outLN), so they are siblings
     ("Falcon-7B decode (config 5 shapes, arch/falcon)", 32,
-     [("wqkv", 4544, 4672), ("wo", 4544, 4544), ("w1", 4544, 18176), ("w2", 18176, 4544)], [[0], [1], [2], [3]]),
+     [("wqkv", 4544, 4672), ("wo", 4544, 4544), ("w1", 4544, 18176), ("w2", 18176, 4544)], [[0, 2], [1], [3]]),
     ("GPT-NeoX-20B decode (config 5 shapes, arch/gptneox: n_embd 6144, n_ff 24576)", 44,
      [("wqkv", 6144, 18432), ("wo", 6144, 6144), ("w1", 6144, 24576), ("w2", 24576, 6144)], [[0], [1], [2], [3]]),
 ]

@@ -709,19 +709,23 @@ struct AttnKQ {
     int hd;                    // head dimension, <= SM_HD
     float *kq_out;
 };
-constexpr int SM_THREADS = 1024, SM_OUT = SM_THREADS / 32, SM_PF = 16, SM_HD = 256;
+// threads per decode-attention workgroup: 32 KQV outputs per 1024 threads, 512 for short rows (the head's
+// outputs over twice the workgroups; tools/attn_ab.py: fused 5.5 / 6.1 vs 6.2 / 6.4 us at 40 / 72 keys, slower
+// from ~130 keys on, where each workgroup's KQ phase gets longer)
+constexpr int SM_PF = 16, SM_HD = 256;
+constexpr int64_t ATTN_SMALL_WG_MAX_KV = 100;
 #ifndef ATTN_KQ_U
 #define ATTN_KQ_U 4         // keys in flight per 32-lane group in the fused KQ phase
 #endif
 // KQM: 0 (kq read from memory) or the K-row elements per lane, ceil(hd / 32) rounded up to 2, 4 or 8
-template <int KQM>
-__global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm,
+template <int KQM, int T>
+__global__ __launch_bounds__(T) void k_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm,
                                                             float v, int n_past, const uint16_t *table, int64_t nkv,
                                                             const char *vs, int64_t nb01v, int64_t nb02v, int64_t nout,
                                                             int splits, float *kqv, float *merged, const AttnKQ aq) {
     extern __shared__ float row[];                     // [nkv]
-    __shared__ float redf[SM_THREADS / 64];
-    __shared__ double redd[SM_THREADS / 64];
+    __shared__ float redf[T / 64];
+    __shared__ double redd[T / 64];
     const int64_t i2 = blockIdx.x / splits;
     const int part = blockIdx.x % splits;
     const int tid = threadIdx.x, g = tid >> 5, l = tid & 31, wave = tid >> 6, lane = tid & 63;
@@ -732,7 +736,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     // before the softmax, so their latency runs under it: unconditional loads of clamped (valid)
     // addresses, so they issue back to back (a load under a branch waits at the join); the products
     // below use the same values in the same order
-    const int64_t r = (int64_t)part * SM_OUT + g;
+    const int64_t r = (int64_t)part * (T / 32) + g;
     const bool live = r < nout;
     const uint16_t *xr = (const uint16_t *)(vs + i2 * nb02v + (live ? r : 0) * nb01v);
     const int K = (int)nkv;
@@ -756,7 +760,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
         const float qtv = qr[min(hnp + l, hkl)];
         // KQ_U keys per group in flight: every key's K-row loads (unconditional, clamped indices) are issued
         // before the first key's products, so a group waits for one memory round trip per KQ_U keys
-        constexpr int KQ_U = ATTN_KQ_U, G = SM_THREADS / 32;
+        constexpr int KQ_U = ATTN_KQ_U, G = T / 32;
         uint16_t kb[KQ_U][KQM], kt[KQ_U];
         auto load_keys = [&](int64_t j0) __attribute__((always_inline)) {
 #pragma unroll
@@ -806,14 +810,14 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     ATTN_STAMP(1)
     auto kq_at = [&](int64_t i) { return KQ ? row[i] : kq[o + i]; };
     float mx = -INFINITY;
-    for (int64_t i = tid; i < nkv; i += SM_THREADS) mx = fmaxf(mx, i > n_past ? -INFINITY : kq_at(i) * v);
+    for (int64_t i = tid; i < nkv; i += T) mx = fmaxf(mx, i > n_past ? -INFINITY : kq_at(i) * v);
     mx = wave_max_f(mx);
     if (lane == 0) redf[wave] = mx;
     __syncthreads();
     mx = redf[0];
-    for (int w = 1; w < SM_THREADS / 64; w++) mx = fmaxf(mx, redf[w]);
+    for (int w = 1; w < T / 64; w++) mx = fmaxf(mx, redf[w]);
     double ssum = 0.0;
-    for (int64_t i = tid; i < nkv; i += SM_THREADS) {
+    for (int64_t i = tid; i < nkv; i += T) {
         const float sv = kq_at(i) * v;
         const float m = i > n_past ? -INFINITY : sv;
         float e = 0.0f;
@@ -831,9 +835,9 @@ __global__ __launch_bounds__(SM_THREADS) void k_softmax_kqv(const float *kq, flo
     if (lane == 0) redd[wave] = ssum;
     __syncthreads();
     ssum = 0.0;
-    for (int w = 0; w < SM_THREADS / 64; w++) ssum += redd[w];
+    for (int w = 0; w < T / 64; w++) ssum += redd[w];
     const float inv = (float)(1.0 / ssum);
-    for (int64_t i = tid; i < nkv; i += SM_THREADS) {
+    for (int64_t i = tid; i < nkv; i += T) {
         const float pv = row[i] * inv;
         row[i] = pv;
         if (store && sm) sm[o + i] = pv;
@@ -1184,13 +1188,25 @@ hipError_t op_scale_mask_soft_max_f32(const float *x, float *scaled, float *mask
     return hipGetLastError();
 }
 
+template <int KQM, int T>
+static void launch_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm, float v, int n_past,
+                               const uint16_t *table, int64_t nkv, int64_t nhead, const void *vs, int64_t nb01v,
+                               int64_t nb02v, int64_t nout, float *kqv, float *merged, const AttnKQ &aq, hipStream_t s) {
+    const int splits = (int)((nout + T / 32 - 1) / (T / 32));
+    launch_k(k_softmax_kqv<KQM, T>, dim3((unsigned)(nhead * splits)), dim3(T), (size_t)nkv * 4, s, kq, scaled, masked, sm,
+             v, n_past, table, nkv, (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, aq);
+}
+
 hipError_t op_softmax_kqv(const float *kq, float *scaled, float *masked, float *sm, float v, int n_past,
                           const uint16_t *table, int64_t nkv, int64_t nhead, const void *vs, int64_t nb01v, int64_t nb02v,
                           int64_t nout, float *kqv, float *merged, hipStream_t s) {
     if (nhead <= 0 || nkv <= 0 || nout <= 0) return hipSuccess;
-    const int splits = (int)((nout + SM_OUT - 1) / SM_OUT);
-    launch_k(k_softmax_kqv<0>, dim3((unsigned)(nhead * splits)), dim3(SM_THREADS), (size_t)nkv * 4, s, kq, scaled,
-             masked, sm, v, n_past, table, nkv, (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, AttnKQ{});
+    if (nkv <= ATTN_SMALL_WG_MAX_KV)
+        launch_softmax_kqv<0, 512>(kq, scaled, masked, sm, v, n_past, table, nkv, nhead, vs, nb01v, nb02v, nout, kqv,
+                                   merged, AttnKQ{}, s);
+    else
+        launch_softmax_kqv<0, 1024>(kq, scaled, masked, sm, v, n_past, table, nkv, nhead, vs, nb01v, nb02v, nout, kqv,
+                                    merged, AttnKQ{}, s);
     return hipGetLastError();
 }
 
@@ -1206,19 +1222,24 @@ hipError_t op_kq_softmax_kqv(const void *ks, int64_t nb01k, int64_t nb02k, const
                              float *kqv, float *merged, hipStream_t s) {
     if (nhead <= 0 || nkv <= 0 || nout <= 0) return hipSuccess;
     if (hd < 1 || hd > SM_HD) return hipErrorInvalidValue;
-    const int splits = (int)((nout + SM_OUT - 1) / SM_OUT);
     const AttnKQ aq{(const char *)ks, nb01k, nb02k, q, nb02q, hd, kq};
-    const dim3 grid((unsigned)(nhead * splits));
-    const size_t lds = (size_t)nkv * 4;
+    const bool small = nkv <= ATTN_SMALL_WG_MAX_KV;
+#define ATTN_FUSED(M)                                                                                           \
+    do {                                                                                                        \
+        if (small)                                                                                              \
+            launch_softmax_kqv<M, 512>(nullptr, scaled, masked, sm, v, n_past, table, nkv, nhead, vs, nb01v, nb02v, \
+                                       nout, kqv, merged, aq, s);                                               \
+        else                                                                                                    \
+            launch_softmax_kqv<M, 1024>(nullptr, scaled, masked, sm, v, n_past, table, nkv, nhead, vs, nb01v,     \
+                                        nb02v, nout, kqv, merged, aq, s);                                       \
+    } while (0)
     if (hd <= 64)
-        launch_k(k_softmax_kqv<2>, grid, dim3(SM_THREADS), lds, s, nullptr, scaled, masked, sm, v, n_past, table, nkv,
-                 (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, aq);
+        ATTN_FUSED(2);
     else if (hd <= 128)
-        launch_k(k_softmax_kqv<4>, grid, dim3(SM_THREADS), lds, s, nullptr, scaled, masked, sm, v, n_past, table, nkv,
-                 (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, aq);
+        ATTN_FUSED(4);
     else
-        launch_k(k_softmax_kqv<8>, grid, dim3(SM_THREADS), lds, s, nullptr, scaled, masked, sm, v, n_past, table, nkv,
-                 (const char *)vs, nb01v, nb02v, nout, splits, kqv, merged, aq);
+        ATTN_FUSED(8);
+#undef ATTN_FUSED
     return hipGetLastError();
 }
 

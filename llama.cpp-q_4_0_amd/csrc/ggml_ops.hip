@@ -1149,7 +1149,7 @@ bool op_x9_ok(int64_t ncols, int64_t nrows) {
 
 hipError_t op_add_rms_norm_mul_f32_x9(const float *a, const float *b, float *sum, float *norm, const float *w, float *out,
                                       int64_t ncols, int64_t nrows, void *xws, int64_t Np, hipStream_t s) {
-    if (!op_x9_ok(ncols, nrows) || !out || !xws || Np < nrows || !row_norm4_ok(ncols, a, b, sum, norm, w, out))
+    if (!op_x9_ok(ncols, nrows) || !out || !xws || Np < nrows || !x9_fits(ncols, Np) || !row_norm4_ok(ncols, a, b, sum, norm, w, out))
         return hipErrorInvalidValue;
     uint8_t *ximg = (uint8_t *)xws;
     uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)(ncols / 32) * Np * 48);
@@ -1160,7 +1160,7 @@ hipError_t op_add_rms_norm_mul_f32_x9(const float *a, const float *b, float *sum
 
 hipError_t op_silu_mul_f32_x9(const float *a, const float *b, float *u, float *out, int64_t ncols, int64_t nrows,
                               const uint16_t *table, void *xws, int64_t Np, hipStream_t s) {
-    if (!op_x9_ok(ncols, nrows) || !out || !xws || Np < nrows || !al16(a) || !al16(b) || !al16(u) || !al16(out))
+    if (!op_x9_ok(ncols, nrows) || !out || !xws || Np < nrows || !x9_fits(ncols, Np) || !al16(a) || !al16(b) || !al16(u) || !al16(out))
         return hipErrorInvalidValue;
     uint8_t *ximg = (uint8_t *)xws;
     uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)(ncols / 32) * Np * 48);

@@ -162,27 +162,44 @@ __device__ __forceinline__ uint32_t e2m3_half(int n) {
 __device__ __forceinline__ uint32_t f6x4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
     return c0 | (c1 << 6) | (c2 << 12) | (c3 << 18);
 }
+// e2m3_half as byte tables for v_perm_b32 (e2m3_codes4): four codes per dword, n = n0 .. n0 + 3
+constexpr uint32_t e2m3_c(int n) {
+    const uint32_t a = (uint32_t)(n < 0 ? -n : n), e = (uint32_t)(a >= 4u) + (uint32_t)(a >= 8u);
+    return (n < 0 ? 0x20u : 0u) | ((a << (2u - e)) + 8u * e);
+}
+constexpr uint32_t e2m3_tab4(int n0) {
+    return e2m3_c(n0) | (e2m3_c(n0 + 1) << 8) | (e2m3_c(n0 + 2) << 16) | (e2m3_c(n0 + 3) << 24);
+}
+// the e2m3_half codes of four 4-bit indices, one per byte: index i < 8 is n = i (the shared table),
+// i >= 8 is looked up in (u0, u1) = the codes of the upper eight n (8..15 for q & 15, -8..-1 for q >> 4)
+__device__ __forceinline__ uint32_t e2m3_codes4(uint32_t idx, uint32_t u0, uint32_t u1) {
+    const uint32_t sel = idx & 0x07070707u;
+    const uint32_t r0 = __builtin_amdgcn_perm(e2m3_tab4(4), e2m3_tab4(0), sel);
+    const uint32_t r1 = __builtin_amdgcn_perm(u1, u0, sel);
+    const uint32_t m = ((idx >> 3) & 0x01010101u) * 0xFFu;
+    return (r1 & m) | (r0 & ~m);
+}
+// four 6-bit codes, one per byte -> the 24-bit field c0 | c1 << 6 | c2 << 12 | c3 << 18 (f6x4)
+__device__ __forceinline__ uint32_t f6x4_bytes(uint32_t c) {
+    return (c & 0x3Fu) | ((c >> 2) & 0xFC0u) | ((c >> 4) & 0x3F000u) | ((c >> 6) & 0xFC0000u);
+}
+
 // The k_gemm9 x image of one q8_0 block held by 8 consecutive lanes, 4 floats each (lane group
 // sub = lane & 7; the q8_0 quantization of q8_block_lane): each lane's four q give four (q >> 4) and
-// four (q & 15) codes (24 bits each), and lanes 0-5 of the group assemble the block's six dwords of
-// each half from their neighbours' fields.  Image layout (k_gemm9): codes [nb][3][Np][16 B] (part 0 =
-// the first 16 B of the (q >> 4) codes, part 1 = those of the (q & 15) codes, part 2 = the last 8 B
-// of both, swapped for tokens with bit 4 set) + fp16 d_x [nb][Np].  Every lane of the wave must call it
-// (DPP); live = false: this lane's group stores nothing.  Shared by k_prep9_x and the producers that
+// four (q & 15) codes (24 bits each; byte-table lookups, e2m3_codes4), and lanes 0-5 of the group
+// assemble the block's six dwords of each half from their neighbours' fields.  Image layout (k_gemm9):
+// codes [nb][3][Np][16 B] (part 0 = the first 16 B of the (q >> 4) codes, part 1 = those of the (q & 15)
+// codes, part 2 = the last 8 B of both, swapped for tokens with bit 4 set) + fp16 d_x [nb][Np].  Every
+// lane of the wave must call it (DPP); live = false: this lane's group stores nothing.  Offsets are
+// 32-bit: the callers check nb * Np * 48 < 2^32 (x9_fits).  Shared by k_prep9_x and the producers that
 // write the image beside their f32 output (ggml_ops.hip).
 __device__ __forceinline__ void x9_store_lane(float4 v, int sub, int64_t n, int64_t b, bool live, uint8_t *ximg,
                                               uint16_t *xd16, int64_t Np) {
     uint32_t d16;
     int qsum;
     const uint32_t packed = q8_block_lane(v, d16, qsum);
-    uint32_t hi[4], lo[4];
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-        const int q = (int)(int8_t)(packed >> (8 * e));
-        hi[e] = e2m3_half(q >> 4);
-        lo[e] = e2m3_half(q & 15);
-    }
-    const uint32_t Fh = f6x4(hi[0], hi[1], hi[2], hi[3]), Fl = f6x4(lo[0], lo[1], lo[2], lo[3]);
+    const uint32_t Fh = f6x4_bytes(e2m3_codes4(packed >> 4, e2m3_tab4(-8), e2m3_tab4(-4)));
+    const uint32_t Fl = f6x4_bytes(e2m3_codes4(packed, e2m3_tab4(8), e2m3_tab4(12)));
     // dword k of a half: fields s and s + 1 shifted by off (k = 0..5 -> (s, off) = (0,0) (1,8) (2,16)
     // (4,0) (5,8) (6,16)); the fields of lanes +1 and +2 by DPP row shifts (groups of 8 lanes sit
     // inside 16-lane rows; lanes 6 and 7, which read past their group, store nothing): k < 3 takes
@@ -198,10 +215,11 @@ __device__ __forceinline__ void x9_store_lane(float4 v, int sub, int64_t n, int6
     const uint32_t l0 = lo3 ? Fl : Fl1, l1 = lo3 ? Fl1 : Fl2;
     if (!live || sub >= 6) return;
     const uint32_t dh = (h0 >> off) | (h1 << (24 - off)), dl = (l0 >> off) | (l1 << (24 - off));
-    const int sw = (int)((n >> 4) & 1);
-    uint32_t *p0 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 0) * Np + n) * 16);
-    uint32_t *p1 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 1) * Np + n) * 16);
-    uint32_t *p2 = reinterpret_cast<uint32_t *>(ximg + ((b * 3 + 2) * Np + n) * 16);
+    const uint32_t np = (uint32_t)Np, nn = (uint32_t)n, bb = (uint32_t)b;
+    const int sw = (int)((nn >> 4) & 1u);
+    uint32_t *p0 = reinterpret_cast<uint32_t *>(ximg + (bb * 3u * np + nn) * 16u);
+    uint32_t *p1 = p0 + np * 4u;
+    uint32_t *p2 = p1 + np * 4u;
     if (k < 4) {
         p0[k] = dh;
         p1[k] = dl;
@@ -209,8 +227,10 @@ __device__ __forceinline__ void x9_store_lane(float4 v, int sub, int64_t n, int6
         p2[2 * sw + k - 4] = dh;
         p2[2 * (sw ^ 1) + k - 4] = dl;
     }
-    if (sub == 0) xd16[b * Np + n] = (uint16_t)d16;
+    if (sub == 0) xd16[bb * np + nn] = (uint16_t)d16;
 }
+// the image's offsets fit x9_store_lane's 32-bit arithmetic
+static inline bool x9_fits(int64_t K, int64_t Np) { return K > 0 && Np > 0 && (K / 32) * Np * 48 < ((int64_t)1 << 32); }
 
 // GGML_HIP_* tuning / test overrides read once (host)
 static inline int env_int(const char *name, int dflt) {

@@ -921,6 +921,7 @@ hipError_t gemm9_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStre
     if (N <= 0 || nb <= 0) return hipSuccess;
     if ((N + 7) / 8 > 65535) return hipErrorInvalidValue;
     const int64_t Np = gemm9_np(N);
+    if (!x9_fits(K, Np)) return hipErrorInvalidValue;
     uint8_t *ximg = (uint8_t *)xws;
     uint16_t *xd16 = (uint16_t *)((char *)xws + (size_t)nb * Np * 48);
     (void)hipGetLastError();

@@ -119,3 +119,43 @@ def test_g9_tile_order_is_a_permutation_and_xcd_local():
             assert split <= 7, (Mt, ny, split)
         if G % 8 == 0 and (G // 8) % ny == 0:
             assert split == 0, (Mt, ny)
+
+
+def e2m3_tab4(n0):
+    """csrc/q4_0_device.h e2m3_tab4: the codes of n0 .. n0 + 3, one per byte"""
+    return sum(e2m3_half(n0 + i) << (8 * i) for i in range(4))
+
+
+def v_perm_b32(s0, s1, sel):
+    """V_PERM_B32 for selector bytes 0..7: byte i of the result = byte sel_i of the 64-bit {s0 (high), s1 (low)}"""
+    src = (s0 << 32) | s1
+    return sum(((src >> (8 * ((sel >> (8 * i)) & 0xFF))) & 0xFF) << (8 * i) for i in range(4))
+
+
+def e2m3_codes4(idx, u0, u1):
+    """csrc/q4_0_device.h e2m3_codes4: four 4-bit indices (one per byte) -> four codes"""
+    sel = idx & 0x07070707
+    r0 = v_perm_b32(e2m3_tab4(4), e2m3_tab4(0), sel)
+    r1 = v_perm_b32(u1, u0, sel)
+    m = (((idx >> 3) & 0x01010101) * 0xFF) & 0xFFFFFFFF
+    return (r1 & m) | (r0 & ~m & 0xFFFFFFFF)
+
+
+def f6x4_bytes(c):
+    return (c & 0x3F) | ((c >> 2) & 0xFC0) | ((c >> 4) & 0x3F000) | ((c >> 6) & 0xFC0000)
+
+
+def test_byte_table_encoder_equals_per_element_encoder():
+    """x9_store_lane's lookups (packed >> 4 with the n = -8..-1 table for q >> 4, packed with 8..15 for
+    q & 15) give the per-element e2m3_half fields for every q8 value in every byte position"""
+    rng = np.random.default_rng(11)
+    qs = [list(range(-128, 128))[i:i + 4] for i in range(0, 256, 4)] + \
+         [[int(v) for v in rng.integers(-128, 128, 4)] for _ in range(2000)]
+    for q in qs:
+        packed = sum((v & 0xFF) << (8 * i) for i, v in enumerate(q))
+        fh = f6x4_bytes(e2m3_codes4(packed >> 4, e2m3_tab4(-8), e2m3_tab4(-4)))
+        fl = f6x4_bytes(e2m3_codes4(packed, e2m3_tab4(8), e2m3_tab4(12)))
+        hi = [e2m3_half(v >> 4) for v in q]
+        lo = [e2m3_half(v & 15) for v in q]
+        assert fh == hi[0] | hi[1] << 6 | hi[2] << 12 | hi[3] << 18, q
+        assert fl == lo[0] | lo[1] << 6 | lo[2] << 12 | lo[3] << 18, q

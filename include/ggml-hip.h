@@ -181,6 +181,9 @@ int64_t ggml_hip_weight_image_bytes(void);                  /* device bytes held
  * GEMM of the image when one exists; 10 is the default), 9 / 11 (k_gemm8 / k_gemm9 always, an
  * unregistered weight converted per call into the workspace); -1 = GGML_HIP_GEMM_V */
 int ggml_hip_debug_set_gemm_version(int v);
+// k_gemm9's tile: -1 = automatic (128 x 128 where it takes fewer CU rounds than 128 x 64; GGML_HIP_GEMM9_WIDE
+// overrides), 0 = always 128 x 64, 1 = always 128 x 128 (block order: y within the oracle bound of 128 x 64's).
+int ggml_hip_debug_set_gemm9_wide(int mode);
 
 /* ------------------------------------------------------------------------------------------
  * Decode chains: a sequence of dependent N = 1 q4_0 mul_mats, validated once and launched together.

@@ -152,6 +152,12 @@ int ggml_hip_debug_set_gemm_version(int v) {
     return GGML_HIP_OK;
 }
 
+int ggml_hip_debug_set_gemm9_wide(int mode) {
+    if (mode < -1 || mode > 1) return fail(GGML_HIP_ERR_INVALID, "mode must be -1, 0 or 1");
+    ghip::gemm9_set_wide(mode);
+    return GGML_HIP_OK;
+}
+
 int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M) {
     ensure_init();
     if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");

@@ -3,6 +3,8 @@
 // Shared device helpers and the HBM layouts: q4_0_device.h / q4_0_kernels.h.
 #include "q4_0_device.h"
 
+#include <atomic>
+
 namespace ghip {
 
 // ---------------------------------------------------------------------------------------------
@@ -720,6 +722,12 @@ struct G9Mats {
     int nfull;                  // tiles [0, nfull) run whole; each later tile runs as two 64-row halves
 };
 
+// Timing-only diagnostic builds (tools/build_variant.sh FILE=q4_0_gemm -DGEMM9_KO=n; results invalid):
+// 1 = no LDS DMAs at all (compute only), 2 = no x code DMAs, 3 = no weight code DMAs.
+#ifndef GEMM9_KO
+#define GEMM9_KO 0
+#endif
+
 // HALF: the workgroup computes rows [64 hsel, 64 hsel + 64) of its 128-row tile, one 32 x 32 tile per compute
 // wave (the same per-output arithmetic: bitwise the whole tile's values for those rows).  Tile order: see
 // G9Mats; the HALF instantiation runs the tiles from mats.nfull on, two workgroups per tile (gemm9_run_multi:
@@ -767,7 +775,7 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
     const int lw = wave - 8;
     const int lb = 2 * lw;
     auto issue = [&](int st) __attribute__((always_inline)) {
-        if (wave < 8) return;
+        if (wave < 8 || GEMM9_KO == 1) return;
         uint8_t *base = smem + (st % G9_NS) * G9_STAGE;
         const int kb0 = st * G9_KB;
         const bool v = kb0 + lb < nb;                                             // nb even: both or none
@@ -778,10 +786,12 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
             const int b = lb + j;
 #pragma unroll
             for (int r = 0; r < 3; r++)
+                if (GEMM9_KO != 3)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(wr_, (lds_void_t *)(base + b * G9_WB + r * 1024), 16,
                                                          (kb0 + b) * G9_WB + r * 1024 + lane * 16, 0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 3; r++)
+                if (GEMM9_KO != 2)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(xr_, (lds_void_t *)(base + G9_W + b * G9_XB + r * 1024), 16,
                                                          (int)((((int64_t)(kb0 + b) * 3 + r) * Np + n0) * 16) + lane * 16,
                                                          0, 0, 0);
@@ -911,6 +921,190 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
     }
 }
 
+// The larger tile (round 5, verdict r4 item 3): 128 rows x 128 tokens per workgroup, half the LDS-DMA bytes
+// of x per MFMA (a block stage moves 3 KB of weight codes + 6 KB of x codes for 16 tile MFMAs instead of
+// 3 + 3 KB for 8).  No K split between waves: compute wave w owns tokens 32 (w & 3) .. and rows
+// 64 (w >> 2) + {0, 32} over every block of a stage (k_gemm9's two-tile operand reuse); stage 76 KB, ring
+// of 2.  The same per-block integer sums and scale products as k_gemm9, summed in block order (k_gemm9 sums
+// blocks 0-3 and 4-7 of every stage apart and adds the two at the end; keeping both partial sums here needs
+// 32 more VGPRs than the 168 a wave has at 3 waves per SIMD: 279 spilled): y is within the oracle bound of
+// k_gemm9's, not bitwise, so gemm9_run_multi's choice is a function of the launch's tile counts and the
+// tests pin the mode wherever they compare two launches bitwise.  gemm9_run_multi picks it per launch by
+// rounds of CUs (wide_pays).  Knockouts as GEMM9_KO.
+static constexpr int W9_BN = 128, W9_NS = 2;
+static constexpr int W9_XB = W9_BN * 48;                          // 6 KB
+static constexpr int W9_X = G9_KB * W9_XB;                        // 48 KB
+static constexpr int W9_XD = G9_KB * W9_BN * 2;                   // 2 KB
+static constexpr int W9_STAGE = G9_W + W9_X + G9_WD + W9_XD;      // 76 KB
+static constexpr int W9_ZERO = 2048;                                // zero d_w: 8 blocks x 256 B
+static constexpr int W9_LDS = W9_NS * W9_STAGE + W9_ZERO;          // 154 KB
+
+__global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9w_q4_0(const G9Mats mats, int nb,
+                                                                const uint8_t *__restrict__ ximg,
+                                                                const uint16_t *__restrict__ xd16, int64_t Np, int N) {
+    const int Mt = mats.tb[mats.n];
+    int j = (int)blockIdx.x;
+    if (mats.xcd) {
+        const int C = (int)gridDim.x >> 3;
+        if (j < 8 * C) j = (j & 7) * C + (j >> 3);
+    }
+    const int rtg = mats.xcd ? j / mats.ny : j % Mt, ty = mats.xcd ? j - rtg * mats.ny : j / Mt;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *zero = smem + W9_NS * W9_STAGE;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 31, h = lane >> 5;
+    const int mi = (mats.n > 1 && rtg >= mats.tb[1]) + (mats.n > 2 && rtg >= mats.tb[2]) + (mats.n > 3 && rtg >= mats.tb[3]);
+    const uint8_t *wimg = mi == 0 ? mats.wimg[0] : mi == 1 ? mats.wimg[1] : mi == 2 ? mats.wimg[2] : mats.wimg[3];
+    const uint16_t *wd16 = mi == 0 ? mats.wd16[0] : mi == 1 ? mats.wd16[1] : mi == 2 ? mats.wd16[2] : mats.wd16[3];
+    float *y = mi == 0 ? mats.y[0] : mi == 1 ? mats.y[1] : mi == 2 ? mats.y[2] : mats.y[3];
+    const int64_t ldy = mi == 0 ? mats.ldy[0] : mi == 1 ? mats.ldy[1] : mi == 2 ? mats.ldy[2] : mats.ldy[3];
+    const int M = mi == 0 ? mats.M[0] : mi == 1 ? mats.M[1] : mi == 2 ? mats.M[2] : mats.M[3];
+    const int rt = rtg - (mi == 0 ? 0 : mi == 1 ? mats.tb[1] : mi == 2 ? mats.tb[2] : mats.tb[3]);
+    const int m0 = rt * G9_BM, n0 = ty * W9_BN;
+    if (tid < W9_ZERO / 4) reinterpret_cast<uint32_t *>(zero)[tid] = 0u;
+
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(wimg + (int64_t)rt * nb * G9_WB, (uint32_t)nb * G9_WB);
+    const __amdgpu_buffer_rsrc_t wdrs = make_rsrc(wd16 + (int64_t)rt * nb * G9_BM, (uint32_t)nb * G9_BM * 2u);
+    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(ximg, (uint32_t)((int64_t)nb * Np * 48));
+    const __amdgpu_buffer_rsrc_t xdrs = make_rsrc(xd16, (uint32_t)((int64_t)nb * Np * 2));
+    const __amdgpu_buffer_rsrc_t nul = make_rsrc(wimg, 0);
+
+    const int lb = 2 * (wave - 8);
+    auto issue = [&](int st) __attribute__((always_inline)) {
+        if (wave < 8 || GEMM9_KO == 1) return;
+        uint8_t *base = smem + (st % W9_NS) * W9_STAGE;
+        const int kb0 = st * G9_KB;
+        const bool v = kb0 + lb < nb;
+        const __amdgpu_buffer_rsrc_t wr_ = v ? wrs : nul, xr_ = v ? xrs : nul, dr_ = v ? xdrs : nul,
+                                     wdr_ = v ? wdrs : nul;
+#pragma unroll
+        for (int jj = 0; jj < 2; jj++) {
+            const int b = lb + jj;
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+                if (GEMM9_KO != 3)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wr_, (lds_void_t *)(base + b * G9_WB + r * 1024), 16,
+                                                         (kb0 + b) * G9_WB + r * 1024 + lane * 16, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++)
+                    if (GEMM9_KO != 2)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        xr_, (lds_void_t *)(base + G9_W + b * W9_XB + r * 2048 + hh * 1024), 16,
+                        (int)((((int64_t)(kb0 + b) * 3 + r) * Np + n0 + 64 * hh) * 16) + lane * 16, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wdr_, (lds_void_t *)(base + G9_W + W9_X + b * 256), 4,
+                                                     (kb0 + b) * 256 + lane * 4, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dr_, (lds_void_t *)(base + G9_W + W9_X + G9_WD + b * 256), 4,
+                                                     (int)(((int64_t)(kb0 + b) * Np + n0) * 2) + lane * 4, 0, 0, 0);
+        }
+    };
+    const int tq = wave & 3, rh = (wave >> 2) & 1;
+    const int tt = 32 * tq + c;
+    const int r0 = 64 * rh + c, r1 = r0 + 32;
+    const int xo16 = h * 2048 + tt * 16, xo8 = 4096 + tt * 16 + 8 * (h ^ ((tt >> 4) & 1));
+    const int sa = h ? G9_SCALE_1 : G9_SCALE_5;
+    const f32x16 fz = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    float acc0[16], acc1[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc0[i] = acc1[i] = 0.0f;
+    f32x16 S0 = fz, S1 = fz, P0 = fz, P1 = fz;
+    u32x4 as = {0u, 0u, 0u, 0u}, bs0 = {0u, 0u, 0u, 0u}, bs1 = {0u, 0u, 0u, 0u};
+    auto epi = [&](float *a, const f32x16 &S, const f32x16 &P) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) a[i] = fmaf(S[i], P[i], a[i]);
+    };
+    struct Ops {
+        i32x8 ax, bw0, bw1;
+        uint32_t sx, sw0, sw1;
+    };
+    auto rd24 = [&](const uint8_t *p16, const uint8_t *p8) __attribute__((always_inline)) {
+        const u32x4 u = *reinterpret_cast<const u32x4 *>(p16);
+        const u32x2 v = *reinterpret_cast<const u32x2 *>(p8);
+        const i32x8 r = {(int)u.x, (int)u.y, (int)u.z, (int)u.w, (int)v.x, (int)v.y, 0, 0};
+        return r;
+    };
+    auto block = [&](const Ops &o) __attribute__((always_inline)) {
+        as.x = o.sx;
+        bs0.x = o.sw0;
+        bs1.x = o.sw1;
+        epi(acc0, S0, P0);
+        epi(acc1, S1, P1);
+        __builtin_amdgcn_sched_barrier(0);
+        S0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw0, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+        S1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(o.ax, o.bw1, fz, 2, 2, 0, sa, 0, G9_SCALE_1);
+        P0 = scale_rank1(as, bs0);
+        P1 = scale_rank1(as, bs1);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto sync = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    const int nstages = (nb + G9_KB - 1) / G9_KB;
+    issue(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int s = 0; s < nstages; s++) {
+        issue(s + 1);
+        const int kb = s * G9_KB;
+        if (wave < 8) {
+            const uint32_t sb = (uint32_t)(s % W9_NS) * W9_STAGE;
+            uint32_t xa = sb + G9_W + xo16, xb8 = sb + G9_W + xo8;
+            uint32_t wa0 = sb + r0 * 16, wa1 = wa0 + 512;
+            uint32_t w80 = sb + 2048 + r0 * 8, w81 = w80 + 256;
+            uint32_t da = h ? (uint32_t)(W9_NS * W9_STAGE) : sb + G9_W + W9_X + r0 * 2;
+            uint32_t xd = sb + G9_W + W9_X + G9_WD + tt * 2;
+            asm volatile("" : "+v"(wa1), "+v"(w81));
+            auto rdj = [&](int jb) __attribute__((always_inline)) {
+                Ops o;
+                o.ax = rd24(smem + xa + jb * W9_XB, smem + xb8 + jb * W9_XB);
+                o.bw0 = rd24(smem + wa0 + jb * G9_WB, smem + w80 + jb * G9_WB);
+                o.bw1 = rd24(smem + wa1 + jb * G9_WB, smem + w81 + jb * G9_WB);
+                o.sw0 = *reinterpret_cast<const uint16_t *>(smem + da + jb * 256);
+                o.sw1 = *reinterpret_cast<const uint16_t *>(smem + da + jb * 256 + 64);
+                o.sx = *reinterpret_cast<const uint16_t *>(smem + xd + jb * 256);
+                return o;
+            };
+#pragma unroll
+            for (int jb = 0; jb < G9_KB; jb++) {
+                if (kb + jb >= nb) break;
+                block(rdj(jb));
+            }
+        }
+        sync();
+    }
+    epi(acc0, S0, P0);
+    epi(acc1, S1, P1);
+    if (wave < 8) {
+        const int row0 = m0 + r0, row1 = m0 + r1;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int tk = n0 + 32 * tq + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (tk < N) {
+                if (row0 < M) y[(int64_t)tk * ldy + row0] = acc0[i];
+                if (row1 < M) y[(int64_t)tk * ldy + row1] = acc1[i];
+            }
+        }
+    }
+}
+
+
+// wide tile choice: -1 auto (GGML_HIP_GEMM9_WIDE unset), 0 never, 1 always (tests / A/B)
+static std::atomic<int> g_wide_mode{env_int("GGML_HIP_GEMM9_WIDE", -1)};
+void gemm9_set_wide(int mode) { g_wide_mode.store(mode < 0 ? env_int("GGML_HIP_GEMM9_WIDE", -1) : mode, std::memory_order_relaxed); }
+
+// Rounds of one-workgroup-per-CU tiles: the 128 x 64 launch takes ceil(tiles / CUs) rounds (a last round of
+// at most half the CUs as 64-row halves: half a round); a 128 x 128 round costs W9_ROUND of them (measured
+// at one full round each, 4096 x 4096 x 1024: 40.4 vs 2 x 23.6 us; profiles/r05_gemm9_wide_tile.txt).
+static constexpr double W9_ROUND = 1.72;
+static bool wide_pays(int64_t tiles, bool halves, int64_t tiles_w, int cus) {
+    const double base = (double)(tiles / cus) + (tiles % cus == 0 ? 0.0 : halves ? 0.5 : 1.0);
+    const double wide = (double)((tiles_w + cus - 1) / cus) * W9_ROUND;
+    return wide < 0.97 * base;
+}
 
 int64_t gemm9_np(int64_t N) { return (N + 3) & ~(int64_t)3; }
 size_t gemm9_x_bytes(int64_t K, int64_t N) { return (size_t)(K / QK) * gemm9_np(N) * 50; }
@@ -988,6 +1182,20 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     const uint8_t *ximg = (const uint8_t *)xws;
     const uint16_t *xd16 = (const uint16_t *)((const char *)xws + (size_t)nb * Np * 48);
     if ((int64_t)nb * Np * 48 >= ((int64_t)1 << 31) || (int64_t)nb * G9_WB >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    const int64_t Nyw = (N + W9_BN - 1) / W9_BN, tiles_w = (int64_t)mats.tb[n] * Nyw;
+    const int wm = g_wide_mode.load(std::memory_order_relaxed);
+    if (wm == 1 || (wm == -1 && wide_pays(tiles, halves, tiles_w, cus))) {
+        static bool wattr = false;
+        if (!wattr) {
+            const hipError_t e = hipFuncSetAttribute((const void *)k_gemm9w_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize, W9_LDS);
+            if (e != hipSuccess) return e;
+            wattr = true;
+        }
+        mats.ny = (int)Nyw;
+        (void)hipGetLastError();
+        launch_k(k_gemm9w_q4_0, dim3((unsigned)tiles_w), dim3(G9_THREADS), W9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
+        return hipGetLastError();
+    }
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);

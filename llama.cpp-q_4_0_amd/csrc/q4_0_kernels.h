@@ -115,6 +115,8 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *M, int6
                            float *const *y, const int64_t *ldy, hipStream_t s);
 hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
                      hipStream_t s);
+// the 128 x 128 tile (k_gemm9w): -1 auto by rounds of CUs (GGML_HIP_GEMM9_WIDE overrides), 0 never, 1 always
+void gemm9_set_wide(int mode);
 
 // Small / medium N (split-K over the waves of a 32x32-tile workgroup, operands straight to registers).
 hipError_t gemm_sk_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, const float *xd, int64_t N,

@@ -628,13 +628,71 @@ def test_gemm9_fp6_bitwise_equals_gemm8_int8(K, M, N):
     whole int8 range, so the (q >> 4, q & 15) split sees every code)."""
     wq, x = make_case(K, M, N, seed=K * 5 + M + N)
     ys = {}
+    _gemm9_wide(0)                                       # the 128 x 64 tile: k_gemm8's block order
     try:
         for v in (9, 11):
             _gemm_version(v)
             ys[v], _ = gpu_mul_mat(wq, K, x, algo=2)
     finally:
         _gemm_version(-1)
+        _gemm9_wide(-1)
     assert np.array_equal(ys[9].view(np.uint32), ys[11].view(np.uint32))
+
+
+def _gemm9_wide(mode):
+    L = ggml_hip.load()
+    L.ggml_hip_debug_set_gemm9_wide.argtypes = [ctypes.c_int]
+    ggml_hip.check(L.ggml_hip_debug_set_gemm9_wide(mode), "gemm9 wide")
+
+
+@pytest.mark.parametrize("K,M,N", [s for s in EDGE_SHAPES if s[2] > 8] +
+                         [(4544, 4672, 130), (128, 1, 200), (4096, 4096, 1024), (11008, 4096, 300), (4096, 11008, 257)])
+def test_gemm9_wide_tile_vs_oracle(K, M, N):
+    """The 128 x 128 k_gemm9 tile (k_gemm9w_q4_0, forced): ragged M / N, K = 64 (one partial stage), K = 4544
+    (a partial last stage), full LLaMA shapes; within the oracle bound, and within it of the 128 x 64 tile."""
+    wq, x = make_case(K, M, N, seed=K * 7 + M + N)
+    ys = {}
+    try:
+        _gemm_version(11)
+        for mode in (0, 1):
+            _gemm9_wide(mode)
+            ys[mode], _ = gpu_mul_mat(wq, K, x, algo=2)
+    finally:
+        _gemm_version(-1)
+        _gemm9_wide(-1)
+    xq = O.quantize_q8_0(x, "avx2")
+    _, s_abs = block_terms(wq, xq, K)
+    ref = O.mul_mat(wq, K, x, nthreads=8, mode="avx2", pool=True)
+    check_y(ys[1], ref, s_abs, RTOL, ATOL_BLOCKS)
+    check_y(ys[1], ys[0], s_abs, RTOL, ATOL_BLOCKS)
+
+
+def test_gemm9_auto_tile_takes_wide_for_llama_w1w3():
+    """The automatic tile choice (wide_pays, rounds of CUs): the LLaMA-7B w1|w3 group at 512 tokens (1,376
+    128 x 64 tiles = 5 rounds + a half-round tail on 256 CUs; 688 128 x 128 tiles = 3 rounds) runs the wide
+    tile, bitwise its forced result; q|k|v at 512 tokens (768 vs 384 tiles) keeps the 128 x 64 tile."""
+    L = ggml_hip.load()
+    K, N = 4096, 512
+    x = make_case(K, 8, N, seed=77)[1]
+    xd = DB.from_array(x)
+    for Ms, wide in (([11008, 11008], True), ([4096, 4096, 4096], False)):
+        cases = [make_case(K, M, 1, seed=900 + 3 * i + M)[0] for i, M in enumerate(Ms)]
+        wds = [DB.from_array(c) for c in cases]
+        for wd, M in zip(wds, Ms):
+            ggml_hip.check(L.ggml_hip_weight_image_create(wd.ptr, K, M, None), "image")
+        try:
+            out = {}
+            for mode in (-1, 0, 1):
+                _gemm9_wide(mode)
+                ys = [DB(N * M * 4) for M in Ms]
+                ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
+                out[mode] = [y.download((N, M), np.float32).view(np.uint32) for y, M in zip(ys, Ms)]
+        finally:
+            _gemm9_wide(-1)
+            for wd in wds:
+                L.ggml_hip_weight_image_free(wd.ptr)
+        want = out[1] if wide else out[0]
+        assert all(np.array_equal(a, b) for a, b in zip(out[-1], want)), (Ms, wide)
 
 
 def test_gemm9_fp6_extreme_blocks_exact():
@@ -795,10 +853,12 @@ def test_gemm8_mixed_sibling_group_bitwise():
     (4544, [4672, 4544], 100),                # Falcon shapes, N just above IMG_MIN_N
     (4096, [129, 11008], 40),                 # tall sibling below IMG_MIN_N with a short one (both imaged)
 ])
-def test_gemm9_sibling_group_one_launch_bitwise(K, Ms, N):
+@pytest.mark.parametrize("wide", [0, 1], ids=["tile128x64", "tile128x128"])
+def test_gemm9_sibling_group_one_launch_bitwise(K, Ms, N, wide):
     """Siblings that all have fp6 images run as ONE k_gemm9 launch over their row tiles (the x image built
-    once): every y bitwise equal to a separate call per matrix, within the oracle bound."""
+    once): every y bitwise equal to a separate call per matrix with the same tile, within the oracle bound."""
     L = ggml_hip.load()
+    _gemm9_wide(wide)
     cases = [make_case(K, M, N, seed=700 + 7 * i + M) for i, M in enumerate(Ms)]
     x = cases[0][1]
     wds = [DB.from_array(c[0]) for c in cases]
@@ -818,6 +878,7 @@ def test_gemm9_sibling_group_one_launch_bitwise(K, Ms, N):
         check_y(outs[i], O.mul_mat(cases[i][0], K, x, nthreads=8, mode="avx2", pool=True),
                 s_abs_exact(cases[i][0], xq, K), RTOL, ATOL_BLOCKS)
     finally:
+        _gemm9_wide(-1)
         for wd in wds:
             L.ggml_hip_weight_image_free(wd.ptr)
 

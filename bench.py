@@ -799,7 +799,8 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0,
             "GBps": round(nbytes / t / 1e9, 1), "TOPs": round(ops / t / 1e12, 1),
             "mfma_frac": round(ops / t / 1e12 / INT8_PEAK_TOPS, 4), "peak_TOPs": INT8_PEAK_TOPS,
             "stack_7B_prefill_ms": round(t / layers * 32 * 1e3, 3),
-            "kernel": "k_gemm9_q4_0: exact block sums on the block-scaled fp6 MFMA, per-weight e2m3 images built "
+            "kernel": "k_gemm9_q4_0 / k_gemm9w_q4_0: exact block sums on the block-scaled fp6 MFMA, 128x64 or "
+                      "128x128 workgroup tiles chosen per launch by rounds of CUs, per-weight e2m3 images built "
                       f"once (26 B per 32 weights; image bytes {image_bytes} for {layers} layers)",
             "int8_images": alt("k_gemm8_q4_0: i8 MFMA on per-weight int8 images (34 B per 32 weights; image bytes "
                                f"{image_bytes8})", t8),

@@ -1096,14 +1096,15 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9w_q4_0(const G9Mats mats
 static std::atomic<int> g_wide_mode{env_int("GGML_HIP_GEMM9_WIDE", -1)};
 void gemm9_set_wide(int mode) { g_wide_mode.store(mode < 0 ? env_int("GGML_HIP_GEMM9_WIDE", -1) : mode, std::memory_order_relaxed); }
 
-// Rounds of one-workgroup-per-CU tiles: the 128 x 64 launch takes ceil(tiles / CUs) rounds (a last round of
-// at most half the CUs as 64-row halves: half a round); a 128 x 128 round costs W9_ROUND of them (measured
-// at one full round each, 4096 x 4096 x 1024: 40.4 vs 2 x 23.6 us; profiles/r05_gemm9_wide_tile.txt).
-static constexpr double W9_ROUND = 1.72;
-static bool wide_pays(int64_t tiles, bool halves, int64_t tiles_w, int cus) {
-    const double base = (double)(tiles / cus) + (tiles % cus == 0 ? 0.0 : halves ? 0.5 : 1.0);
-    const double wide = (double)((tiles_w + cus - 1) / cus) * W9_ROUND;
-    return wide < 0.97 * base;
+// Which tile, by rounds of one-workgroup-per-CU tiles (fit to tools/g9_tile_sweep.py over the LLaMA-7B / 13B and
+// Falcon-7B prefill launches at 128-2048 tokens, profiles/r05_gemm9_tile_sweep.txt): 128 x 64 when its tiles fit one
+// round; else 128 x 128 when its tiles fit one round, fill at least two, or leave a last round more than half full
+// (a last 128 x 128 round at most half full costs nearly a full one while 128 x 64 runs its tail as half tiles:
+// 1.03-1.18x at 1.1-1.5 rounds).
+static bool wide_pays(int64_t tiles, int64_t tiles_w, int cus) {
+    if (tiles <= cus) return false;
+    if (tiles_w <= cus || tiles_w >= 2 * (int64_t)cus) return true;
+    return 2 * (tiles_w - cus) > cus;
 }
 
 int64_t gemm9_np(int64_t N) { return (N + 3) & ~(int64_t)3; }
@@ -1184,7 +1185,7 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     if ((int64_t)nb * Np * 48 >= ((int64_t)1 << 31) || (int64_t)nb * G9_WB >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     const int64_t Nyw = (N + W9_BN - 1) / W9_BN, tiles_w = (int64_t)mats.tb[n] * Nyw;
     const int wm = g_wide_mode.load(std::memory_order_relaxed);
-    if (wm == 1 || (wm == -1 && wide_pays(tiles, halves, tiles_w, cus))) {
+    if (wm == 1 || (wm == -1 && wide_pays(tiles, tiles_w, cus))) {
         static bool wattr = false;
         if (!wattr) {
             const hipError_t e = hipFuncSetAttribute((const void *)k_gemm9w_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize, W9_LDS);

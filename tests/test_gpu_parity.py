@@ -668,14 +668,15 @@ def test_gemm9_wide_tile_vs_oracle(K, M, N):
 
 
 def test_gemm9_auto_tile_takes_wide_for_llama_w1w3():
-    """The automatic tile choice (wide_pays, rounds of CUs): the LLaMA-7B w1|w3 group at 512 tokens (1,376
-    128 x 64 tiles = 5 rounds + a half-round tail on 256 CUs; 688 128 x 128 tiles = 3 rounds) runs the wide
-    tile, bitwise its forced result; q|k|v at 512 tokens (768 vs 384 tiles) keeps the 128 x 64 tile."""
+    """The automatic tile choice (wide_pays, rounds of 256 CUs): the LLaMA-7B w1|w3 group at 512 tokens (1,376
+    128 x 64 tiles = 5 rounds + a half-round tail; 688 128 x 128 tiles = 2.7 rounds) and q|k|v at 256 tokens (384
+    vs 192 tiles: 128 x 128 fits one round) run the wide tile, bitwise its forced result; q|k|v at 512 tokens (768
+    vs 384 tiles: a last wide round half full) keeps 128 x 64."""
     L = ggml_hip.load()
-    K, N = 4096, 512
-    x = make_case(K, 8, N, seed=77)[1]
-    xd = DB.from_array(x)
-    for Ms, wide in (([11008, 11008], True), ([4096, 4096, 4096], False)):
+    K = 4096
+    x = make_case(K, 8, 512, seed=77)[1]
+    for Ms, N, wide in (([11008, 11008], 512, True), ([4096, 4096, 4096], 512, False), ([4096, 4096, 4096], 256, True)):
+        xd = DB.from_array(np.ascontiguousarray(x[:N]))
         cases = [make_case(K, M, 1, seed=900 + 3 * i + M)[0] for i, M in enumerate(Ms)]
         wds = [DB.from_array(c) for c in cases]
         for wd, M in zip(wds, Ms):
@@ -692,7 +693,7 @@ def test_gemm9_auto_tile_takes_wide_for_llama_w1w3():
             for wd in wds:
                 L.ggml_hip_weight_image_free(wd.ptr)
         want = out[1] if wide else out[0]
-        assert all(np.array_equal(a, b) for a, b in zip(out[-1], want)), (Ms, wide)
+        assert all(np.array_equal(a, b) for a, b in zip(out[-1], want)), (Ms, N, wide)
 
 
 def test_gemm9_fp6_extreme_blocks_exact():

@@ -720,6 +720,7 @@ struct G9Mats {
     int tb[5];
     int n, ny, xcd;
     int nfull;                  // tiles [0, nfull) run whole; each later tile runs as two 64-row halves
+    int toff;                   // 128 x 64 launch after a 128 x 128 one: its tiles start at this index (xcd order)
 };
 
 // Timing-only diagnostic builds (tools/build_variant.sh FILE=q4_0_gemm -DGEMM9_KO=n; results invalid):
@@ -746,6 +747,7 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
         const int C = (int)gridDim.x >> 3;
         if (j < 8 * C) j = (j & 7) * C + (j >> 3);
     }
+    j += mats.toff;
     const int rtg = mats.xcd ? j / mats.ny : j % Mt, ty = mats.xcd ? j - rtg * mats.ny : j / Mt;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *zero = smem + G9_NS * G9_STAGE;
@@ -1185,6 +1187,42 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     if ((int64_t)nb * Np * 48 >= ((int64_t)1 << 31) || (int64_t)nb * G9_WB >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     const int64_t Nyw = (N + W9_BN - 1) / W9_BN, tiles_w = (int64_t)mats.tb[n] * Nyw;
     const int wm = g_wide_mode.load(std::memory_order_relaxed);
+    // Mixed (GGML_HIP_GEMM9_MIXED=0 turns it off): a launch whose 128 x 128 tiles would leave a last round at most half
+    // full runs its whole rounds of them (row tiles [0, R)) and the remaining row tiles as 128 x 64, that launch's
+    // tail as half tiles: 5-10 % below the faster single tile (profiles/r05_gemm9_mixed.txt); rows [0, 128 R) are
+    // bitwise the 128 x 128 tile's, the rest the 128 x 64 tile's.
+    static const int mixed_on = env_int("GGML_HIP_GEMM9_MIXED", 1);
+    const int64_t rem_w = tiles_w % cus, R = Nyw > 0 ? (tiles_w / cus) * cus / Nyw : 0;
+    if (mixed_on && wm == -1 && mats.xcd && tiles > cus && tiles_w > cus && rem_w > 0 && 2 * rem_w <= cus && R > 0 &&
+        R < mats.tb[n]) {
+        static bool mattr = false;
+        if (!mattr) {
+            hipError_t e = hipFuncSetAttribute((const void *)k_gemm9w_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize, W9_LDS);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
+            if (e != hipSuccess) return e;
+            mattr = true;
+        }
+        (void)hipGetLastError();
+        G9Mats mw = mats;                               // row tiles [0, R): 128 x 128
+        mw.ny = (int)Nyw;
+        mw.toff = 0;
+        launch_k(k_gemm9w_q4_0, dim3((unsigned)(R * Nyw)), dim3(G9_THREADS), W9_LDS, s, mw, nb, ximg, xd16, Np, (int)N);
+        G9Mats mb = mats;                               // row tiles [R, Mt): 128 x 64, tail as half tiles
+        const int64_t tb2 = ((int64_t)mats.tb[n] - R) * Ny, rem2 = tb2 % cus;
+        const bool halves2 = half_on && rem2 > 0 && 2 * rem2 <= cus;
+        mb.toff = (int)(R * Ny);
+        mb.nfull = (int)(halves2 ? tb2 - rem2 : tb2);
+        const int64_t grid2 = halves2 ? tb2 + rem2 : tb2;
+        if (mb.nfull > 0)
+            launch_k(k_gemm9_q4_0<false>, dim3((unsigned)mb.nfull), dim3(G9_THREADS), G9_LDS, s, mb, nb, ximg, xd16, Np, (int)N);
+        if (grid2 > mb.nfull)
+            launch_k(k_gemm9_q4_0<true>, dim3((unsigned)(grid2 - mb.nfull)), dim3(G9_THREADS), G9_LDS, s, mb, nb, ximg, xd16,
+                     Np, (int)N);
+        return hipGetLastError();
+    }
     if (wm == 1 || (wm == -1 && wide_pays(tiles, tiles_w, cus))) {
         static bool wattr = false;
         if (!wattr) {

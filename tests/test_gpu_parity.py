@@ -667,15 +667,33 @@ def test_gemm9_wide_tile_vs_oracle(K, M, N):
     check_y(ys[1], ys[0], s_abs, RTOL, ATOL_BLOCKS)
 
 
+def g9_wide_rows(Ms, N, cus=256):
+    """csrc/q4_0_gemm.hip gemm9_run_multi's tile plan, restated: how many leading rows of the concatenated row tiles
+    run the 128 x 128 tile (the rest 128 x 64): none when the 128 x 64 tiles fit one round; one or more whole
+    128 x 128 rounds' row tiles when the 128 x 128 tiles would leave a last round at most half full (mixed); all
+    otherwise (wide_pays)."""
+    Mt = sum((M + 127) // 128 for M in Ms)
+    tiles, tiles_w = Mt * ((N + 63) // 64), Mt * ((N + 127) // 128)
+    total = sum(Ms)
+    if tiles <= cus:
+        return 0
+    rem_w = tiles_w % cus
+    if tiles_w > cus and rem_w > 0 and 2 * rem_w <= cus:
+        return min(total, 128 * ((tiles_w // cus) * cus // ((N + 127) // 128)))
+    if tiles_w <= cus or tiles_w >= 2 * cus or 2 * (tiles_w - cus) > cus:
+        return total
+    return 0
+
+
 def test_gemm9_auto_tile_takes_wide_for_llama_w1w3():
-    """The automatic tile choice (wide_pays, rounds of 256 CUs): the LLaMA-7B w1|w3 group at 512 tokens (1,376
-    128 x 64 tiles = 5 rounds + a half-round tail; 688 128 x 128 tiles = 2.7 rounds) and q|k|v at 256 tokens (384
-    vs 192 tiles: 128 x 128 fits one round) run the wide tile, bitwise its forced result; q|k|v at 512 tokens (768
-    vs 384 tiles: a last wide round half full) keeps 128 x 64."""
+    """The automatic tile plan (256 CUs): the LLaMA-7B w1|w3 group at 512 tokens (1,376 128 x 64 tiles; 688
+    128 x 128 = 2.7 rounds) and q|k|v at 256 tokens (192 128 x 128 tiles: one round) run the wide tile; q|k|v at
+    512 tokens (384 wide tiles: a last round half full) runs one round of it (wq, wk) and wv as 128 x 64; wo at 512
+    tokens (256 128 x 64 tiles: one round) keeps 128 x 64.  Every row bitwise the forced result of its tile."""
     L = ggml_hip.load()
     K = 4096
     x = make_case(K, 8, 512, seed=77)[1]
-    for Ms, N, wide in (([11008, 11008], 512, True), ([4096, 4096, 4096], 512, False), ([4096, 4096, 4096], 256, True)):
+    for Ms, N in (([11008, 11008], 512), ([4096, 4096, 4096], 512), ([4096, 4096, 4096], 256), ([4096], 512)):
         xd = DB.from_array(np.ascontiguousarray(x[:N]))
         cases = [make_case(K, M, 1, seed=900 + 3 * i + M)[0] for i, M in enumerate(Ms)]
         wds = [DB.from_array(c) for c in cases]
@@ -687,13 +705,16 @@ def test_gemm9_auto_tile_takes_wide_for_llama_w1w3():
                 _gemm9_wide(mode)
                 ys = [DB(N * M * 4) for M in Ms]
                 ggml_hip.mul_mat_multi(wds, Ms, K, xd, N, ys)
-                out[mode] = [y.download((N, M), np.float32).view(np.uint32) for y, M in zip(ys, Ms)]
+                out[mode] = np.concatenate([y.download((N, M), np.float32).view(np.uint32) for y, M in zip(ys, Ms)], 1)
         finally:
             _gemm9_wide(-1)
             for wd in wds:
                 L.ggml_hip_weight_image_free(wd.ptr)
-        want = out[1] if wide else out[0]
-        assert all(np.array_equal(a, b) for a, b in zip(out[-1], want)), (Ms, N, wide)
+        cut = g9_wide_rows(Ms, N)
+        assert np.array_equal(out[-1][:, :cut], out[1][:, :cut]), (Ms, N, cut)
+        assert np.array_equal(out[-1][:, cut:], out[0][:, cut:]), (Ms, N, cut)
+    assert [g9_wide_rows(*c) for c in (([11008, 11008], 512), ([4096] * 3, 512), ([4096] * 3, 256), ([4096], 512))] == \
+        [22016, 8192, 12288, 0]
 
 
 def test_gemm9_fp6_extreme_blocks_exact():

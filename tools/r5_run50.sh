@@ -1,0 +1,6 @@
+# the mixed launch generalised to any number of whole 128 x 128 rounds: correctness split + timings (mixed on / off)
+set -o pipefail
+O=gpurun_out/r05; mkdir -p $O
+for r in 1 2; do for m in 0 1; do
+  GGML_HIP_GEMM9_MIXED=$m timeout -k 10 400 python tools/g9_mixed_check.py > $O/mixedg_${m}_$r.jsonl 2> $O/mixedg_${m}_$r.err || exit 1
+done; done

@@ -1169,8 +1169,10 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     static const int xcd = env_int("GGML_HIP_GEMM9_XCD", 1);
     mats.xcd = xcd ? 1 : 0;
     // a last partial round of at most half the CUs runs as twice as many 64-row half tiles, each about half
-    // a tile's time (one workgroup per CU: 154 KB of LDS); GGML_HIP_GEMM9_HALF=0 runs it whole
-    static const int half_on = env_int("GGML_HIP_GEMM9_HALF", 1);
+    // a tile's time (one workgroup per CU: 154 KB of LDS), and so does a whole launch of at most half the CUs
+    // (10-27 % faster at 96-192 tokens on the wo / w2 shapes, profiles/r05_gemm9_small_halves.txt);
+    // GGML_HIP_GEMM9_HALF=1 keeps only the tail, 0 runs every tile whole
+    static const int half_on = env_int("GGML_HIP_GEMM9_HALF", 2);
     static int cus = 0;
     if (cus == 0) {
         int dev = 0, v = 0;
@@ -1179,7 +1181,7 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
         if (cus <= 0) cus = 256;
     }
     const int64_t rem = tiles % cus;
-    const bool halves = half_on && tiles > cus && rem > 0 && 2 * rem <= cus;
+    const bool halves = (half_on && tiles > cus && rem > 0 && 2 * rem <= cus) || (half_on == 2 && 2 * tiles <= cus);
     mats.nfull = (int)(halves ? tiles - rem : tiles);
     const int64_t grid = halves ? tiles + rem : tiles;
     const uint8_t *ximg = (const uint8_t *)xws;

@@ -19,13 +19,22 @@ NS = [int(v) for v in os.environ.get("NS", "128 256 384 512 768 1024 2048").spli
 NMAX = max(NS)
 out = []
 s = L.ggml_hip_default_stream()
+# COLD=1: the calls cycle over distinct copies of the weight (> 600 MB of images in all), so every call streams its
+# image from HBM as a model's layers do (the default reuses one copy: Infinity-Cache hits)
+COLD = os.environ.get("COLD", "0") == "1"
 for K, M in SHAPES:
     tmp = gh.DeviceBuffer(K * M * 4)
-    w = gh.DeviceBuffer(18 * K // 32 * M)
     gh.check(L.ggml_hip_fill_gaussian(tmp.ptr, K * M, 11, 0.0, 0.02, None))
-    gh.check(L.ggml_hip_quantize_q4_0(tmp.ptr, K, M, w.ptr, None))
+    img = ((M + 127) // 128) * 128 * K // 32 * 26
+    ncopy = max(2, -(-600 * 2 ** 20 // img)) if COLD else 1
+    ws = []
+    for _ in range(ncopy):
+        wc = gh.DeviceBuffer(18 * K // 32 * M)
+        gh.check(L.ggml_hip_quantize_q4_0(tmp.ptr, K, M, wc.ptr, None))
+        gh.check(L.ggml_hip_weight_image_create(wc.ptr, K, M, None))
+        ws.append(wc)
     tmp.free()
-    gh.check(L.ggml_hip_weight_image_create(w.ptr, K, M, None))
+    w = ws[0]
     x = gh.DeviceBuffer(K * NMAX * 4)
     gh.check(L.ggml_hip_fill_gaussian(x.ptr, K * NMAX, 9, 0.0, 1.0, None))
     y = gh.DeviceBuffer(M * NMAX * 4)
@@ -38,8 +47,8 @@ for K, M in SHAPES:
                 gh.check(L.ggml_hip_mul_mat_q4_0_ex(w.ptr, K, M, x.ptr, N, y.ptr, M, 2, s))
             a, b = gh.Event(), gh.Event()
             a.record(s)
-            for _ in range(10):
-                gh.check(L.ggml_hip_mul_mat_q4_0_ex(w.ptr, K, M, x.ptr, N, y.ptr, M, 2, s))
+            for i in range(10):
+                gh.check(L.ggml_hip_mul_mat_q4_0_ex(ws[i % len(ws)].ptr, K, M, x.ptr, N, y.ptr, M, 2, s))
             b.record(s)
             gh.check(L.ggml_hip_stream_synchronize(s))
             row[name] = round(a.elapsed_ms(b) * 100, 2)          # us per call
@@ -49,6 +58,8 @@ for K, M in SHAPES:
         print(json.dumps(row), flush=True)
         out.append(row)
     gh.check(L.ggml_hip_debug_set_gemm9_wide(-1))
-    L.ggml_hip_weight_image_free(w.ptr)
-    for b_ in (w, x, y):
+    for wc in ws:
+        L.ggml_hip_weight_image_free(wc.ptr)
+        wc.free()
+    for b_ in (x, y):
         b_.free()

@@ -147,7 +147,9 @@ int ggml_hip_mul_mat_q4_0_ex(const void *dev_w, int64_t K, int64_t M, const floa
 /* Sibling mul_mats that share the activation x (ggml graphs issue wq/wk/wv and w1/w3 on the same
  * src1): n <= 4 weight matrices of the same K, y_i = W_i x with y_i f32 [N][M_i].  One launch for
  * N <= 8 (rows concatenated); for N > 8 x is quantized once and each W_i runs the GEMM.  Results
- * are identical to n separate ggml_hip_mul_mat_q4_0 calls. */
+ * are identical to n separate ggml_hip_mul_mat_q4_0 calls, except where siblings with fp6 weight images
+ * run as one prefill launch whose tile plan (128 x 64 / 128 x 128, by the launch's tile count) differs from
+ * the single calls' (within the oracle bound; bitwise with ggml_hip_debug_set_gemm9_wide pinning the tile). */
 int ggml_hip_mul_mat_q4_0_multi(int n, const void *const *dev_w, const int64_t *M, int64_t K, const float *dev_x,
                                 int64_t N, float *const *dev_y, void *stream);
 /* Exact (reproducible) mode, process-wide: every auto-selected mul_mat, including the ggml hook

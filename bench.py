@@ -65,12 +65,22 @@ def log(*a):
 
 
 # ---------------------------------------------------------------------------------------------
-def launch_ranks(n_gpus):
+def error_line(n_gpus, msg):
+    """the one JSON line of a run that could not measure (a rank stalled, failed or ran out of time)"""
+    return json.dumps({"metric": METRIC, "value": None, "unit": "tok/s", "n_gpus": n_gpus, "higher_is_better": True,
+                       "error": msg})
+
+
+def launch_ranks(n_gpus, deadline_s):
     """`bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment): start N fresh child
     processes of this script, one per rank, before this process loads any GPU library (no exec, no
     relaunch of a process that touched the GPU).  Rank 0's stdout (the one JSON line) is this process's
     stdout, the other ranks' go to stderr.  The ranks rendezvous through a fresh directory (RCCL unique
-    id file, or the file comm when ranks share a device).  Returns the exit code (the worst rank's)."""
+    id file, or the file comm when ranks share a device).  Returns the exit code (the worst rank's).
+    Overall deadline (verdict r5 item 4): when the ranks have not all exited `deadline_s` after the start
+    (a rank stuck before or in RCCL init, or in a collective), every remaining rank is terminated (killed
+    10 s later) and this process prints ONE JSON line with "error" and returns 124; a failed rank gives
+    the others 60 s (or what is left of the deadline)."""
     import shutil
     import socket
     import subprocess
@@ -91,7 +101,22 @@ def launch_ranks(n_gpus):
                                           stdout=None if r == 0 else sys.stderr))
         rcs = [None] * n_gpus
         t_fail = None
+        t_start = time.time()
         while any(rc is None for rc in rcs):
+            if time.time() - t_start > deadline_s:
+                stuck = [r for r in range(n_gpus) if rcs[r] is None]
+                log(f"[launcher] deadline {deadline_s:.0f} s passed: terminating ranks {stuck}")
+                for r in stuck:
+                    procs[r].terminate()
+                t_kill = time.time()
+                while any(procs[r].poll() is None for r in stuck) and time.time() - t_kill < 10:
+                    time.sleep(0.05)
+                for r in stuck:
+                    if procs[r].poll() is None:
+                        procs[r].kill()
+                print(error_line(n_gpus, f"launcher deadline {deadline_s:.0f} s passed with ranks {stuck} still running "
+                                         f"(exit codes so far: {rcs})"), flush=True)
+                return 124
             for r, p in enumerate(procs):
                 if rcs[r] is None:
                     rcs[r] = p.poll()
@@ -111,6 +136,33 @@ def launch_ranks(n_gpus):
             if p.poll() is None:
                 p.kill()
         shutil.rmtree(work, ignore_errors=True)
+
+
+def rank_watchdog(L, rank, world, deadline_s, get_comm):
+    """N > 1 ranks (torchrun's or the self-launcher's): if this rank has not finished `deadline_s` after it
+    started, a timer thread aborts its communicator (ncclCommAbort releases a collective stuck on the device;
+    the P2P notice tells the peers), rank 0 prints the one JSON line with "error", and the process exits 3
+    (torchrun then stops the other ranks).  RCCL init and every RCCL call are bounded inside the library too
+    (GGML_HIP_COMM_TIMEOUT_MS, default 120 s)."""
+    import threading
+
+    def fire():
+        log(f"[rank {rank}] deadline {deadline_s:.0f} s passed: aborting the communicator and exiting")
+        c = get_comm()
+        if c is not None and c.value:            # bounded: the exit below happens even if the abort blocks
+            ab = threading.Thread(target=L.ggml_hip_comm_abort, args=(c,), daemon=True)
+            ab.start()
+            ab.join(15.0)
+        if rank == 0:
+            print(error_line(world, f"rank deadline {deadline_s:.0f} s passed (stuck in init or a collective)"),
+                  flush=True)
+        sys.stderr.flush()
+        os._exit(3)
+
+    t = threading.Timer(deadline_s, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def setup_dist():
@@ -216,23 +268,38 @@ def main():
                     help="N > 1: skip the direct-store (P2P) all-gather line next to RCCL's")
     ap.add_argument("--no-batch-siblings", action="store_true",
                     help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
+    ap.add_argument("--deadline", type=float, default=300.0,
+                    help="N > 1: seconds after which a rank that has not finished aborts its communicator and exits "
+                         "(rank 0 prints an error line); the self-launcher terminates its ranks 30 s later")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus))
+        sys.exit(launch_ranks(args.gpus, args.deadline + 30.0))
+    stall = os.environ.get("GGML_HIP_BENCH_STALL_RANKS")     # test hook: these ranks hang before any GPU work
+    if stall and os.environ.get("RANK", "0") in stall.split(","):
+        log(f"[rank {os.environ.get('RANK')}] GGML_HIP_BENCH_STALL_RANKS: stalling before GPU init")
+        while True:
+            time.sleep(1)
 
     import ggml_hip as gh
     L = gh.load()                            # /opt/rocm HIP + RCCL (no torch in this process)
     rank, world, local = setup_dist()
     if world > 1 and args.gpus != world:
         log(f"[rank {rank}] --gpus {args.gpus} but WORLD_SIZE {world}: using {world} ranks")
+    comm = None
+    watchdog = rank_watchdog(L, rank, world, args.deadline, lambda: comm) if world > 1 else None
+    armed = os.environ.get("GGML_HIP_BENCH_STALL_ARMED_RANKS")   # test hook: hang with the watchdog armed
+    if armed and str(rank) in armed.split(","):
+        log(f"[rank {rank}] GGML_HIP_BENCH_STALL_ARMED_RANKS: stalling with the watchdog armed")
+        while True:
+            time.sleep(1)
     ndev = L.ggml_hip_device_count()
     if ndev < 1:
         raise SystemExit("no HIP device")
     gh.check(L.ggml_hip_set_device(local % ndev), "set_device")
     stream = L.ggml_hip_default_stream()
 
-    comm, comm_kind = None, None
+    comm_kind = None
     if world > 1 or args.force_split:
         comm_kind = args.comm if args.comm != "auto" else ("file" if world > ndev else "rccl")
         comm = ctypes.c_void_p()
@@ -271,6 +338,8 @@ def main():
 
     if comm is not None:
         result = sharded_main(gh, L, comm, comm_kind, rank, world, args, stream, allreduce, barrier)
+        if watchdog is not None:
+            watchdog.cancel()
         if rank == 0:
             print(json.dumps(result), flush=True)
         L.ggml_hip_comm_destroy(comm)

@@ -294,8 +294,10 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
 }
 
 // Sibling matrices (one x) that all take k_gemm9 on a registered fp6 image: ONE launch over their
-// row tiles (the x image built once, as before).  Each output is computed exactly as by the
-// per-matrix launch (same block order, same workgroup-half split), so y is bitwise the same.
+// row tiles (the x image built once, as before).  The launch plans its tiles (128 x 128 / 128 x 64 /
+// mixed, half tiles) from its own total tile count, which can differ from the per-matrix launches'
+// plans: y is within the oracle bound of the separate calls, and bitwise equal to them only with the
+// tile pinned (ggml_hip_debug_set_gemm9_wide 0 or 1; include/ggml-hip.h).
 // Returns 1 when the group does not qualify (the caller runs one launch per matrix).
 int mul_mat_group_g9(int n, const void *const *w, const int64_t *M, int64_t K, const float *x, int64_t N,
                      float *const *y, hipStream_t s) {

@@ -507,7 +507,9 @@ bool try_fuse(tensor *t) {
 // behind it ("after" nodes, replayed in arrival order once the group has run), and a later q4_0
 // mul_mat with the same src1 joins the group when running it ahead of the held nodes is safe: it
 // reads none of their outputs and its output overlaps none of their operands.  The group is one
-// multi-matrix GEMV launch (ggml_hip_mul_mat_q4_0_multi), bit-identical to separate launches.
+// multi-matrix GEMV launch (ggml_hip_mul_mat_q4_0_multi), bit-identical to separate launches at decode; a
+// prefill group on fp6 images is one k_gemm9 launch whose tile plan follows its total tile count (within the
+// oracle bound of separate launches; bitwise only with the tile pinned, include/ggml-hip.h).
 struct Group {
     int n = 0, na = 0;
     tensor *mm[4] = {};

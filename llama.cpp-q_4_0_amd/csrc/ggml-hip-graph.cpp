@@ -86,12 +86,16 @@ Launcher &launcher() {
     return *l;
 }
 // the launcher's CPU: GGML_HIP_LAUNCHER_CPU=n pins it to CPU n, -1 leaves it to the scheduler; by default
-// the first allowed CPU that is neither the starting thread's nor its SMT sibling (tools/launch_thread_cost.hip:
-// 2.75 vs 2.87 us per hipLaunchKernel pinned vs free)
+// (tools/launch_thread_cost.hip: 2.75 vs 2.87 us per hipLaunchKernel pinned vs free) one of the process's own
+// allowed CPUs that is neither the starting thread's nor its SMT sibling, the LOCAL_RANK-th such CPU so that
+// rank processes sharing a node (and an unrestricted affinity mask) do not all spin on the same core
+// (ADVICE r5); with several ranks and fewer candidate CPUs than ranks the thread stays unpinned
 void launcher_pin(int main_cpu) {
     const char *e = getenv("GGML_HIP_LAUNCHER_CPU");
     const int want = e ? atoi(e) : -2;
     if (want == -1) return;
+    const char *lr = getenv("LOCAL_RANK");
+    const int local_rank = lr ? atoi(lr) : 0;
     cpu_set_t allowed, one;
     if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
     int sib[2] = {-1, -1};
@@ -101,9 +105,10 @@ void launcher_pin(int main_cpu) {
         if (fscanf(f, "%d%*[,-]%d", &sib[0], &sib[1]) < 1) sib[0] = -1;
         fclose(f);
     }
+    int skip = want >= 0 ? 0 : (local_rank > 0 ? local_rank : 0);
     for (int c = 0; c < CPU_SETSIZE; c++) {
         const bool ok = want >= 0 ? c == want : (CPU_ISSET(c, &allowed) && c != main_cpu && c != sib[0] && c != sib[1]);
-        if (!ok) continue;
+        if (!ok || skip-- > 0) continue;
         CPU_ZERO(&one);
         CPU_SET(c, &one);
         (void)sched_setaffinity(0, sizeof one, &one);
@@ -142,9 +147,10 @@ void launcher_main(Launcher *L, int main_cpu) {
             (void)hipSetDevice(cur_dev);
         }
         for (int a = 0; a < sl.nargs; a++) argv[a] = sl.blob + sl.off[a];
-        const long long t0 = g_launch_prof ? launch_prof_now() : 0;
+        const bool prof = g_launch_prof.load(std::memory_order_relaxed);
+        const long long t0 = prof ? launch_prof_now() : 0;
         const hipError_t e = hipLaunchKernel(sl.fn, sl.grid, sl.block, argv, sl.lds, L->stream);
-        if (g_launch_prof) launch_prof_add(launch_prof_now() - t0);     // the worker's hipLaunchKernel cost
+        if (prof) launch_prof_add(launch_prof_now() - t0);     // the worker's hipLaunchKernel cost
         if (e != hipSuccess) L->err.store((int)e, std::memory_order_relaxed);
         L->tail.store(t + 1, std::memory_order_release);
     }
@@ -477,7 +483,7 @@ void rec_stats(long long *runs, long long *kernels, long long *updated, long lon
     *built = r.built;
 }
 
-bool g_launch_prof = false;
+std::atomic<bool> g_launch_prof{false};
 static std::atomic<long long> g_lp_count{0}, g_lp_ns{0};
 long long launch_prof_now() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();

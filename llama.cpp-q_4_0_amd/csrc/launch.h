@@ -9,6 +9,7 @@
 // nodes whose grid or arguments changed (hipGraphExecKernelNodeSetParams, ~0.6 us per changed node)
 // and one hipGraphLaunch (~0.03 us per kernel of host time).
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -43,7 +44,7 @@ void rec_stats(long long *runs, long long *kernels, long long *updated, long lon
 // submits what is pending and destroys every cached graph
 void rec_clear_cache();
 // host-cost profile of eager launches (ggml_hip_debug_launch_stats): count and ns inside hipLaunchKernel
-extern bool g_launch_prof;
+extern std::atomic<bool> g_launch_prof;   // read by the launcher thread, written by the API
 void launch_prof_add(long long ns);
 long long launch_prof_now();
 void launch_prof_read(long long *count, long long *ns, bool reset);
@@ -53,7 +54,7 @@ inline void launch_k(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStre
     static_assert(sizeof...(P) == sizeof...(A), "launch_k: argument count");
     if (!rec_active(s)) {
         if (rec_pending()) rec_flush_at("eager launch");   // never overtakes recorded launches
-        if (__builtin_expect(g_launch_prof, 0)) {
+        if (__builtin_expect(g_launch_prof.load(std::memory_order_relaxed), 0)) {
             const long long t0 = launch_prof_now();
             hipLaunchKernelGGL(k, grid, block, lds, s, std::forward<A>(a)...);
             launch_prof_add(launch_prof_now() - t0);

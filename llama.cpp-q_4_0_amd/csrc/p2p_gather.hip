@@ -24,7 +24,8 @@ namespace ghip {
 // its own ctl[3] beside the flag, so a peer fails within one poll of the first failure instead of
 // after its own timeout (round 4: each rank paid its own 10 s on the next epoch, so an 8-rank job
 // took >= 10 s per rank to error out).  ggml_hip_comm_abort sends the same notice from the host side
-// (p2p_abort below).  A comm with any bit in ctl[2] or ctl[3] is failed for good: every later launch
+// (p2p_abort below; it also releases this rank's OWN gather in flight: the host sets a request word in
+// host-mapped memory that the waits poll).  A comm with any bit in ctl[2] or ctl[3] is failed for good: every later launch
 // only copies this rank's own slice and fills the peers' segments with NaN (no stores to peers, no
 // waits, the epoch stays), and the host returns an error before launching the next all-gather
 // (ggml-hip-comm.cpp comm_allgather).  Before round 4 a timed-out wait copied the stale slot and
@@ -41,7 +42,8 @@ __global__ __launch_bounds__(256) void k_p2p_allgather(const P2PArgs a, const fl
     const uint64_t e = a.ctl[0] + 1;                 // written only by the previous launch's last workgroup
     const int slot = (int)(e & 1);
     const bool failed = __hip_atomic_load(a.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-                        __hip_atomic_load(a.ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+                        __hip_atomic_load(a.ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+                        (a.herr && __hip_atomic_load(a.herr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0);
     const float qnan = __builtin_nanf("");
     if (blockIdx.x == 0 && recv + (int64_t)me * count != send)   // own slice (not in place)
         for (int64_t i = tid; i < count; i += blockDim.x) recv[(int64_t)me * count + i] = send[i];
@@ -65,13 +67,21 @@ __global__ __launch_bounds__(256) void k_p2p_allgather(const P2PArgs a, const fl
             // arrives fails the comm instead of hanging the device); a peer's failure notice ends it too
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             int ok = 1;
+            unsigned spins = 0;
             while (__hip_atomic_load(a.flag[me] + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-                const bool notice = __hip_atomic_load(a.ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+                // a peer's notice (ctl[3]), another workgroup of this launch failing (ctl[2]), or this
+                // rank's own abort: the host's request word (checked every 16th poll: a host-memory
+                // round trip) and ctl[2] as set by k_p2p_abort on another stream
+                const bool notice = __hip_atomic_load(a.ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+                                    __hip_atomic_load(a.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                const bool aborted = a.herr && (++spins & 15u) == 0 &&
+                                     __hip_atomic_load(a.herr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
                 const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout;
-                if (notice || late) {
+                if (notice || late || aborted) {
                     __hip_atomic_fetch_or(a.ctl + 2, 1ull << q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (a.herr) __hip_atomic_store(a.herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (late) p2p_notify_peers(a);    // this rank saw the failure first: tell the others
+                    // this rank saw the failure first (its timeout) or is the one aborting: tell the others
+                    if (late || aborted) p2p_notify_peers(a);
                     ok = 0;
                     break;
                 }
@@ -100,7 +110,10 @@ __global__ __launch_bounds__(256) void k_p2p_allgather(const P2PArgs a, const fl
     }
 }
 
-// ggml_hip_comm_abort: this rank fails (every peer bit in its own ctl[2]) and notifies every peer
+// ggml_hip_comm_abort: this rank fails (every peer bit in its own ctl[2]) and notifies every peer.  The host
+// has already set herr[1], so a gather of this rank that was blocked ahead of this launch on the same stream
+// has ended (and notified the peers itself) by the time this runs; on another stream, the blocked gather
+// sees ctl[2] at its next poll.
 __global__ void k_p2p_abort(const P2PArgs a) {
     if (threadIdx.x != 0) return;
     const uint64_t peers = (a.R >= 64 ? ~0ull : ((1ull << a.R) - 1)) & ~(1ull << a.me);

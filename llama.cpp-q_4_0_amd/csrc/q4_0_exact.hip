@@ -2,6 +2,8 @@
 // Shared device helpers and the HBM layouts: q4_0_device.h / q4_0_kernels.h.
 #include "q4_0_device.h"
 
+#include <atomic>
+
 namespace ghip {
 
 // ---------------------------------------------------------------------------------------------
@@ -254,12 +256,14 @@ static hipError_t launch_exact(const ExMats &m, int n, int64_t K, const int8_t *
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     const int lds = ExLayout<NC, EXC, SLOTS>::S * ExLayout<NC, EXC, SLOTS>::SLOT;
-    static bool attr = false;
-    if (!attr) {
+    static std::atomic<uint32_t> attr{0};            // one bit per device (16 max), thread-safe
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev > 15) dev = 0;
+    if (!(attr.load(std::memory_order_acquire) & (1u << dev))) {
         hipError_t e = hipFuncSetAttribute((const void *)k_mm_exact_q4_0<NC, EXC, SLOTS>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
-        attr = true;
+        attr.fetch_or(1u << dev, std::memory_order_acq_rel);
     }
     dim3 grid((unsigned)m.wg_begin[n], (unsigned)((N + NC - 1) / NC));
     (void)hipGetLastError();  // report only this launch's error

@@ -5,6 +5,22 @@
 
 #include <atomic>
 
+namespace {
+constexpr int G9_MAX_DEV = 16;
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device), thread-safe: a bit per kernel key
+// in a per-device atomic mask (the flags were plain function-static bools, set from whichever
+// device was current on the first call)
+hipError_t lds_attr_once(int key, const void *fn, int bytes) {
+    static std::atomic<uint32_t> done[G9_MAX_DEV];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= G9_MAX_DEV) dev = 0;
+    if (done[dev].load(std::memory_order_acquire) & (1u << key)) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done[dev].fetch_or(1u << key, std::memory_order_acq_rel);
+    return e;
+}
+}  // namespace
+
 namespace ghip {
 
 // ---------------------------------------------------------------------------------------------
@@ -573,12 +589,7 @@ hipError_t gemm8_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     const int8_t *ximg = (const int8_t *)xws;
     const uint16_t *xd16 = (const uint16_t *)((const char *)xws + (size_t)nb * Np * 32);
     if ((int64_t)nb * Np * 32 >= ((int64_t)1 << 31) || (int64_t)nb * 2048 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_gemm8_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize, G8_LDS);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    if (const hipError_t e = lds_attr_once(0, (const void *)k_gemm8_q4_0, G8_LDS); e != hipSuccess) return e;
     (void)hipGetLastError();
     launch_k(k_gemm8_q4_0, dim3((unsigned)Mt, (unsigned)((N + G8_BN - 1) / G8_BN)), dim3(G8_THREADS), G8_LDS, s, wimg, wd16,
              nb, (int)M, ximg, xd16, Np, (int)N, y, ldy);
@@ -1173,12 +1184,15 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     // (10-27 % faster at 96-192 tokens on the wo / w2 shapes, profiles/r05_gemm9_small_halves.txt);
     // GGML_HIP_GEMM9_HALF=1 keeps only the tail, 0 runs every tile whole
     static const int half_on = env_int("GGML_HIP_GEMM9_HALF", 2);
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-            cus = v;
-        if (cus <= 0) cus = 256;
+    // the CU count of the device this launch runs on (devices of one process may differ, e.g. partitions)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= G9_MAX_DEV) dev = 0;
+    static std::atomic<int> cus_of[G9_MAX_DEV];
+    int cus = cus_of[dev].load(std::memory_order_relaxed);
+    if (cus <= 0) {
+        int v = 0;
+        cus = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+        cus_of[dev].store(cus, std::memory_order_relaxed);
     }
     const int64_t rem = tiles % cus;
     const bool halves = (half_on && tiles > cus && rem > 0 && 2 * rem <= cus) || (half_on == 2 && 2 * tiles <= cus);
@@ -1197,16 +1211,10 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     const int64_t rem_w = tiles_w % cus, R = Nyw > 0 ? (tiles_w / cus) * cus / Nyw : 0;
     if (mixed_on && wm == -1 && mats.xcd && tiles > cus && tiles_w > cus && rem_w > 0 && 2 * rem_w <= cus && R > 0 &&
         R < mats.tb[n]) {
-        static bool mattr = false;
-        if (!mattr) {
-            hipError_t e = hipFuncSetAttribute((const void *)k_gemm9w_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize, W9_LDS);
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
-            if (e != hipSuccess) return e;
-            mattr = true;
-        }
+        hipError_t e = lds_attr_once(1, (const void *)k_gemm9w_q4_0, W9_LDS);
+        if (e == hipSuccess) e = lds_attr_once(2, (const void *)k_gemm9_q4_0<false>, G9_LDS);
+        if (e == hipSuccess) e = lds_attr_once(3, (const void *)k_gemm9_q4_0<true>, G9_LDS);
+        if (e != hipSuccess) return e;
         (void)hipGetLastError();
         G9Mats mw = mats;                               // row tiles [0, R): 128 x 128
         mw.ny = (int)Nyw;
@@ -1226,24 +1234,16 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
         return hipGetLastError();
     }
     if (wm == 1 || (wm == -1 && wide_pays(tiles, tiles_w, cus))) {
-        static bool wattr = false;
-        if (!wattr) {
-            const hipError_t e = hipFuncSetAttribute((const void *)k_gemm9w_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize, W9_LDS);
-            if (e != hipSuccess) return e;
-            wattr = true;
-        }
+        if (const hipError_t e = lds_attr_once(1, (const void *)k_gemm9w_q4_0, W9_LDS); e != hipSuccess) return e;
         mats.ny = (int)Nyw;
         (void)hipGetLastError();
         launch_k(k_gemm9w_q4_0, dim3((unsigned)tiles_w), dim3(G9_THREADS), W9_LDS, s, mats, nb, ximg, xd16, Np, (int)N);
         return hipGetLastError();
     }
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void *)k_gemm9_q4_0<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G9_LDS);
+    {
+        hipError_t e = lds_attr_once(2, (const void *)k_gemm9_q4_0<false>, G9_LDS);
+        if (e == hipSuccess) e = lds_attr_once(3, (const void *)k_gemm9_q4_0<true>, G9_LDS);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     (void)hipGetLastError();
     if (mats.nfull > 0)
@@ -1384,12 +1384,7 @@ hipError_t gemm_q4_0(const void *W, int64_t K, int64_t M, const int8_t *xqs, con
     const int nb = (int)(K / QK);
     const int64_t rowbytes = (int64_t)nb * Q4B;
     dim3 grid((unsigned)((M + GM_BM - 1) / GM_BM), (unsigned)((N + GM_BN - 1) / GM_BN));
-    static bool attr7 = false;
-    if (!attr7) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_gemm7_q4_0, hipFuncAttributeMaxDynamicSharedMemorySize, G7_LDS);
-        if (e != hipSuccess) return e;
-        attr7 = true;
-    }
+    if (const hipError_t e = lds_attr_once(4, (const void *)k_gemm7_q4_0, G7_LDS); e != hipSuccess) return e;
     (void)hipGetLastError();  // report only this launch's error
     if (!xd16) return hipErrorInvalidValue;
     launch_k(k_gemm7_q4_0, grid, dim3(GM_THREADS), G7_LDS, s, (const uint8_t *)W, rowbytes, nb, (int)M, xqs, xd16,

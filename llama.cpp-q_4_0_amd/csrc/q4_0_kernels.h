@@ -149,13 +149,16 @@ struct P2PArgs {
     uint64_t *ctl;                   // [0] epoch, [1] arrivals, [2] error bits (peer q timed out: bit q),
                                      // [3] failure notices from peers (peer p failed: bit p, stored by p)
     uint64_t *pctl[P2P_MAX_RANKS];   // every rank's control block (ctl of rank r, mapped here)
-    uint32_t *herr;                  // host-mapped error word (nonzero: the comm failed), or nullptr
+    uint32_t *herr;                  // host-mapped words, or nullptr: [0] error (nonzero: the comm failed),
+                                     // [1] abort request (set by the host in ggml_hip_comm_abort; polled by
+                                     // this rank's own waits, so an in-flight gather ends at its next poll)
     uint64_t timeout;                // peer-wait bound in s_memrealtime ticks (100 MHz)
     int me, R;
     int64_t cap;
 };
 hipError_t p2p_allgather(const P2PArgs &a, const float *send, int64_t count, float *recv, hipStream_t s);
-// fail this rank's comm and notify every peer (bit me in each peer's ctl[3]); stream-ordered on s
+// fail this rank's comm and notify every peer (bit me in each peer's ctl[3]); stream-ordered on s (the host
+// sets herr[1] first, so a gather of this rank blocked ahead of it on s ends and sends the notice itself)
 hipError_t p2p_abort(const P2PArgs &a, hipStream_t s);
 
 // Synthetic inputs for the bench (splitmix64 + Box-Muller on device).

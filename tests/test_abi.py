@@ -159,3 +159,47 @@ def test_op_enum_mirror_matches_reference_header():
     for name, v in ref.items():
         key = name.replace("GGML_", "")
         assert mine[key] == v, (name, mine.get(key), v)
+
+
+def test_library_identity_soname_and_exports():
+    """libggml_hip.so carries SONAME libggml_hip.so and exports the C ABI only (ggml_*): no internal
+    C++ symbol (ghip:: / ghh:: globals) can be interposed by, or interpose onto, another copy."""
+    dyn = subprocess.check_output(["readelf", "-d", LIB_PATH], text=True)
+    assert "Library soname: [libggml_hip.so]" in dyn
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB_PATH], text=True)
+    exported = [line.split()[-1] for line in out.splitlines() if line.strip()]
+    assert exported and all(s.startswith("ggml_") for s in exported), [s for s in exported if not s.startswith("ggml_")][:5]
+
+
+_MAPS_PROBE = r"""
+import ctypes, os, sys
+sys.path.insert(0, sys.argv[1])
+import ggml_hip
+ggml_hip.load()
+for p in sys.argv[2:]:
+    ctypes.CDLL(p)            # the caller side: NEEDED libggml_hip_cuda.so -> NEEDED libggml_hip.so
+maps = {l.split()[-1] for l in open("/proc/self/maps") if "/" in l}
+copies = sorted(m for m in maps if os.path.basename(m).startswith("libggml_hip") and "_cuda" not in m)
+print("\n".join(copies))
+"""
+
+
+def test_variant_library_is_the_only_mapped_copy(tmp_path):
+    """GGML_HIP_LIB pointing at a variant build (another file name) and the reference's hooked llama.cpp
+    (or the ggml-cuda.h shim) loaded after it: exactly ONE libggml_hip is mapped.  Without a SONAME the
+    shim's NEEDED libggml_hip.so resolved through its RUNPATH to the in-tree file, a second copy whose
+    default-visibility globals interposed onto the first and whose static destructors ran on the same
+    objects at exit (round 5's `double free or corruption` after the e2e line)."""
+    import shutil
+    variant = tmp_path / "libggml_hip_variant.so"
+    shutil.copy(LIB_PATH, variant)
+    callers = [os.path.join(os.path.dirname(LIB_PATH), "libggml_hip_cuda.so")]
+    ref = os.path.join(os.path.dirname(PKG), "oracle", "_ref", "libllama_ref_hip.so")
+    if os.path.exists(ref):
+        callers.append(ref)
+    env = dict(os.environ, GGML_HIP_LIB=str(variant))
+    r = subprocess.run([os.sys.executable, "-c", _MAPS_PROBE, os.path.join(PKG, "python")] + callers, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    copies = r.stdout.split()
+    assert copies == [str(variant)], copies

@@ -133,3 +133,48 @@ def test_file_comm_session_nonce_and_reuse():
         ggml_hip.check(L.ggml_hip_comm_allreduce_host(c, v, 1, 0))
         assert v[0] == 3.0
         ggml_hip.check(L.ggml_hip_comm_destroy(c))
+
+
+def _bench_json(stdout):
+    lines = [l for l in stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_launcher_deadline_with_a_stalled_rank():
+    """Verdict r5 item 4: `bench.py --gpus 2` self-launched with both ranks forced to stall before any GPU
+    work (GGML_HIP_BENCH_STALL_RANKS) returns within its deadline (--deadline + 30 s for the launcher), prints
+    ONE JSON line with "error" and exits non-zero, instead of waiting for the driver's kill."""
+    import time
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, GGML_HIP_BENCH_STALL_RANKS="0,1")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--deadline", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    took = time.time() - t0
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    line = _bench_json(r.stdout)
+    assert "deadline" in line["error"] and line["value"] is None and line["n_gpus"] == 2
+    assert took < 2 + 30 + 10 + 20, took
+
+
+def test_bench_rank_watchdog_under_external_launcher():
+    """The driver launches N > 1 through torchrun (WORLD_SIZE set), so the launcher deadline does not apply:
+    each rank's own watchdog does.  A rank started as torchrun would start it, forced to hang with its watchdog
+    armed (GGML_HIP_BENCH_STALL_ARMED_RANKS: as if stuck in RCCL init or a collective), ends after --deadline:
+    rank 0 prints the one JSON line with "error" and the process exits 3."""
+    import time
+    root = os.path.dirname(HERE)
+    work = tempfile.mkdtemp(prefix="bench_wd_")
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), GGML_HIP_UID_FILE=os.path.join(work, "uid"),
+               GGML_HIP_COMM_DIR=os.path.join(work, "comm"), GGML_HIP_BENCH_STALL_ARMED_RANKS="0")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--deadline", "3"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    took = time.time() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    line = _bench_json(r.stdout)
+    assert "deadline" in line["error"] and line["value"] is None
+    assert took < 3 + 30, took

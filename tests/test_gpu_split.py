@@ -462,6 +462,55 @@ def test_p2p_abort_notifies_a_waiting_peer():
         L.ggml_hip_comm_destroy(c1)
 
 
+def test_p2p_abort_releases_own_gather_on_default_stream():
+    """abort while THIS rank's own gather is blocked on a peer, on the very stream the abort's notice
+    queues on (the backend's default stream, stream = NULL).  Rank 1 runs a split mul_mat whose all-gather
+    waits for rank 0, which never gathers; ggml_hip_comm_abort(rank 1) sets its host-mapped request word, the
+    blocked wait sees it at its next poll, notifies rank 0 and ends, so the abort returns in well under the
+    10 s timeout: rank 1's own rows bitwise, rank 0's segment NaN, both ranks' status failed (rank 0 through
+    the notice), and the next split call on either rank returns GGML_HIP_ERR_COMM."""
+    import time
+    K, M, N = 4096, 1024, 1
+    wq, x = make_case(K, M, N, seed=79)
+    rb = split_rows(M, 2)
+    L = ggml_hip.load()
+    xd = DB.from_array(x)
+    wds = [DB.from_array(wq[rb[r]:rb[r + 1]]) for r in range(2)]
+    y = DB(N * M * 4)
+    own = gpu_y(wq[rb[1]:rb[2]], K, x)
+    comms = (ctypes.c_void_p * 2)()
+    ggml_hip.check(L.ggml_hip_comm_init_local(comms, 2, None))
+    c0, c1 = ctypes.c_void_p(comms[0]), ctypes.c_void_p(comms[1])
+    try:
+        th = threading.Thread(target=lambda: ggml_hip.check(L.ggml_hip_comm_enable_p2p(c1, N * M)))
+        th.start()
+        ggml_hip.check(L.ggml_hip_comm_enable_p2p(c0, N * M))
+        th.join(timeout=60)
+        L.ggml_hip_memset(y.ptr, 0, y.nbytes, None)
+        ggml_hip.synchronize()
+        rc = L.ggml_hip_mul_mat_q4_0_split(c1, wds[1].ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p), xd.ptr, N,
+                                           y.ptr, None)
+        assert rc == 0
+        time.sleep(0.3)                                   # rank 1's gather is spinning on rank 0's flag now
+        t0 = time.time()
+        ggml_hip.check(L.ggml_hip_comm_abort(c1), "abort rank 1")
+        took = time.time() - t0
+        assert took < 1.0, f"abort took {took:.3f} s behind its own blocked gather (timeout 10 s)"
+        got = y.download((N, M), np.float32)
+        assert np.array_equal(got[:, rb[1]:rb[2]].view(np.uint32), own.view(np.uint32))
+        assert np.all(np.isnan(got[:, rb[0]:rb[1]])), "the never-arrived peer's segment must read NaN"
+        assert L.ggml_hip_comm_p2p_status(c1) != 0
+        assert L.ggml_hip_comm_p2p_status(c0) & 2, "rank 0 must hold rank 1's failure notice"
+        for c, r in ((c1, 1), (c0, 0)):
+            rc = L.ggml_hip_mul_mat_q4_0_split(c, wds[r].ptr, K, M, rb.ctypes.data_as(ctypes.c_void_p), xd.ptr, N,
+                                               y.ptr, None)
+            assert rc == ggml_hip.ERR_COMM, (r, rc)
+        print(f"abort returned {took * 1e3:.1f} ms after the call, own gather released")
+    finally:
+        L.ggml_hip_comm_destroy(c0)
+        L.ggml_hip_comm_destroy(c1)
+
+
 def test_p2p_abort_across_processes_one_gpu():
     """The same active failure across the process boundary (IPC mappings, tests/split_worker.py mode abort):
     after one good split on both ranks, rank 1 starts the next one while rank 0 aborts 0.3 s later; rank 1

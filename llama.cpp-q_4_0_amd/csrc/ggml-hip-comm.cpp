@@ -702,7 +702,11 @@ int ggml_hip_comm_p2p_status(ggml_hip_comm *c) {
     HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
     uint64_t err[2] = {0, 0};
     HIP_RET(GHIP_SYNC(hipMemcpy)(err, c->p2p.ctl + 2, 16, hipMemcpyDeviceToHost));
-    return (int)(err[0] | err[1]);             // sticky: a failed comm stays failed
+    // sticky: a failed comm stays failed.  A notice that arrived while this rank was idle (no gather of its
+    // own saw it yet) is latched into the host error word here, so the next split call already returns
+    // GGML_HIP_ERR_COMM instead of enqueueing one more NaN gather
+    if ((err[0] | err[1]) && c->p2p_herr) __atomic_store_n(c->p2p_herr, 1u, __ATOMIC_RELEASE);
+    return (int)(err[0] | err[1]);
 }
 
 int ggml_hip_comm_rank(const ggml_hip_comm *c, int *rank, int *nranks) {

@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--modes", default="fast,exact")
     ap.add_argument("--out", default="")
     ap.add_argument("--shape", choices=("7b", "host"), default="7b")
+    ap.add_argument("--maps", action="store_true",
+                    help="record the libggml_hip files mapped into this process (one copy expected; GGML_HIP_LIB)")
     ap.add_argument("--hostprof", default="", help="sample the host walk of each mode (tools/hostprof.c) into PATH.<mode>")
     args = ap.parse_args()
     hp = HP7B if args.shape == "7b" else HPHOST
@@ -195,6 +197,11 @@ def main():
     finally:
         os.remove(model)
         os.rmdir(d)
+    if args.maps:      # after the evals: every library the reference llama.cpp pulled in is mapped by now
+        mapped = {l.split()[-1] for l in open("/proc/self/maps") if "/" in l}
+        res["libggml_hip_mapped"] = sorted(m for m in mapped if os.path.basename(m).startswith("libggml_hip")
+                                           and "_cuda" not in m)
+        res["ggml_hip_lib_env"] = os.environ.get("GGML_HIP_LIB")
     if "cpu" in res:
         res["cpu_cpu_name"] = open("/proc/cpuinfo").read().split("model name")[1].split(":")[1].split("\n")[0].strip()
     line = json.dumps(res)

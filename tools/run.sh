@@ -1,0 +1,64 @@
+#!/bin/bash
+# The one GPU job runner (replaces the round-4/5 one-off scripts; their history is in git).
+#   PARTS="tests smoke bench prof pmc gpmc e2e e2e_variant" O=gpurun_out/r06 bash tools/run.sh
+# Every GPU step runs under its own time limit; a fault, abort or timeout (rc 124/134/137/139 or any
+# rc >= 2 of a step that must pass) ends the script there: no further GPU step in the same call.
+# Extra arguments per part: BENCH_ARGS (bench, prof), E2E_ARGS (e2e), VARIANT (e2e_variant: a
+# tools/build_variant.sh name under variants/, default base).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=${O:-gpurun_out/r06}
+mkdir -p "$O"
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+step() {   # step <name> <seconds> <cmd...>; counter passes get SIGKILL at the limit (rocprofv3 --pmc hangs on SIGTERM)
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  case $name in pmc_*|gpmc_*) timeout -s KILL "$t" "$@" > "$O/$name.log" 2>&1;;
+                *) timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1;; esac
+  local rc=$?
+  echo "=== $name rc=$rc"
+  case $rc in 0) return 0;; 1) tail -5 "$O/$name.log"; return 0;; *) tail -20 "$O/$name.log"; exit $rc;; esac
+}
+has() { [[ " ${PARTS:-tests smoke bench prof} " == *" $1 "* ]]; }
+
+if has tests; then
+  step gputest 1100 python -u -m pytest tests -m gpu -v -rs --timeout 300 --timeout-method thread ${TEST_ARGS:-}
+  grep -E "passed|failed" "$O/gputest.log" | tail -1
+fi
+has smoke && step smoke 180 python -c "import __graft_entry__ as g; g.smoke()"
+if has bench; then
+  step bench 480 python bench.py ${BENCH_ARGS:-}
+  tail -1 "$O/bench.log" | cut -c1-400
+fi
+if has prof; then    # the bench's own timed replays under the kernel tracer
+  step prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extra ${BENCH_ARGS:-}
+  tail -1 "$O/prof.log" | cut -c1-300
+fi
+if has pmc; then     # decode GEMV HBM bytes: one counter per pass (gfx950: FETCH_SIZE is half the streamed bytes)
+  for c in FETCH_SIZE WRITE_SIZE; do
+    step pmc_$c 300 rocprofv3 --pmc $c -d "$O/pmc/$c" -o run --output-format csv -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu --no-prefill --no-extra --no-exact ${BENCH_ARGS:-}
+  done
+  python3 tools/pmc_summary.py "$O/pmc" > "$O/gemv_pmc_traffic.json" && cat "$O/gemv_pmc_traffic.json" | cut -c1-400
+fi
+if has gpmc; then    # prefill GEMM counters, k_gemm9 at 4096 x 4096 x 512 (tools/gemm_one.py)
+  i=0
+  IFS='|' read -ra sets <<< "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES|SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA|SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU|FETCH_SIZE|WRITE_SIZE|GRBM_GUI_ACTIVE SQ_INSTS_SALU"
+  for c in "${sets[@]}"; do
+    i=$((i+1))
+    step gpmc_$i 60 rocprofv3 --pmc $c -d "$O/gpmc/p$i" -o run --output-format csv -- python3 tools/gemm_one.py
+  done
+fi
+if has e2e; then     # the hook path end to end: the reference llama.cpp at full offload, LLaMA-7B shape
+  step e2e 700 python tools/e2e_llama.py --decode 128 --modes fast,exact --out "$O/e2e_7b.json" ${E2E_ARGS:-}
+fi
+if has e2e_variant; then
+  # a variant library through GGML_HIP_LIB, then the reference llama.cpp through the shim (the round-5 abort at
+  # teardown): the process must exit 0 after llama_free / llama_free_model, with ONE libggml_hip mapped
+  v=${VARIANT:-base}
+  [ -f "variants/libggml_hip_$v.so" ] || { echo "variants/libggml_hip_$v.so missing: build it with tools/build_variant.sh"; exit 2; }
+  GGML_HIP_LIB=$PWD/variants/libggml_hip_$v.so step e2e_variant 700 python tools/e2e_llama.py --decode 128 --no-cpu \
+      --modes fast --maps --out "$O/e2e_variant_$v.json"
+  python3 -c "import json; r=json.load(open('$O/e2e_variant_$v.json')); print('maps', r.get('libggml_hip_mapped'), 'tok/s', r['offload_fast']['decode_tok_s'])"
+fi
+exit 0

@@ -268,6 +268,10 @@ def main():
                     help="N > 1: skip the direct-store (P2P) all-gather line next to RCCL's")
     ap.add_argument("--no-batch-siblings", action="store_true",
                     help="one launch per mul_mat (7 per layer) instead of batching wq/wk/wv and w1/w3")
+    ap.add_argument("--decode", choices=("auto", "engine", "launches"), default="auto",
+                    help="headline decode path: the persistent LDS-DMA engine (one launch per token, "
+                         "ggml_hip_chain_set_engine), the per-launch graph (4 sibling GEMVs per layer), or auto = "
+                         "the engine when it plans the chain and its outputs are bitwise the launches'")
     ap.add_argument("--deadline", type=float, default=300.0,
                     help="N > 1: seconds after which a rank that has not finished aborts its communicator and exits "
                          "(rank 0 prints an error line); the self-launcher terminates its ranks 30 s later")
@@ -410,20 +414,31 @@ def main():
         else:
             decode_step()
 
-    for _ in range(args.warmup):
-        run_step()
-    barrier()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        run_step()
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    ms_per_step = elapsed / args.steps * 1e3
-    tok_s = args.steps / elapsed * 32 / args.layers if args.layers else 0.0   # per full 32-layer token
+    def timed(step_fn):
+        for _ in range(args.warmup):
+            step_fn()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_fn()
+        barrier()
+        return time.perf_counter() - t0
+
+    elapsed_launches = timed(run_step)
     last = yb[6].download((LAYER[6][2],), np.float32, stream=stream)          # the step's last output
     finite = bool(np.all(np.isfinite(last)))
     if not finite:
         log("WARNING: the decode chain's last output is not finite")
+    outs_launches = [yb[i].download((LAYER[i][2],), np.float32, stream=stream) for i in range(len(LAYER))]
+    engine = None
+    if args.decode != "launches" and graph is not None and batch:
+        engine = engine_decode(gh, L, launch_args, yb, outs_launches, stream, timed)
+        if args.decode == "engine" and not engine.get("on"):
+            raise SystemExit(f"--decode engine: the engine declined the chain: {engine.get('declined')}")
+    use_engine = engine is not None and engine.get("on") and engine["bitwise_vs_launches"] and engine["status"] == 0
+    elapsed = engine["elapsed_s"] if use_engine else elapsed_launches
+    ms_per_step = elapsed / args.steps * 1e3
+    tok_s = args.steps / elapsed * 32 / args.layers if args.layers else 0.0   # per full 32-layer token
 
     result = {
         "metric": METRIC, "value": round(tok_s, 2), "unit": "tok/s", "n_gpus": 1, "steps": args.steps,
@@ -435,11 +450,20 @@ def main():
         "config": {"workload": "LLaMA-7B q4_0 decode, 32 layers x 7 mul_mats (wq,wk,wv,wo 4096x4096; w1,w3 "
                                "4096->11008; w2 11008->4096), N=1, q8_0 quantize of x included, lm_head excluded",
                    "layers": args.layers, "weights_bytes_per_rank": stack.total_bytes,
-                   "graph": graph is not None, "launches_per_layer": len(groups),
+                   "graph": graph is not None,
+                   "decode_path": ("persistent LDS-DMA engine: ONE launch per token (ggml_hip_chain_set_engine), "
+                                   "outputs bitwise the per-launch GEMVs'" if use_engine else
+                                   "per-launch GEMVs, one HIP graph per token"),
+                   "launches_per_layer": 0.0 if use_engine else len(groups),
                    "sibling_batching": "wq|wk|wv and w1|w3 share src1 -> one launch each" if batch else "off",
                    "collectives_per_layer": 0, "parallelism": "single GPU", "activations_finite": finite},
     }
     result["config"]["runtime_libs"] = gh.mapped_runtime_libs()
+    result["launches_graph"] = {"tok_s": round(args.steps / elapsed_launches * 32 / args.layers, 2),
+                                "ms_per_step": round(elapsed_launches / args.steps * 1e3, 4),
+                                "launches_per_layer": len(groups)}
+    if engine is not None:
+        result["engine"] = {k: v for k, v in engine.items() if k != "elapsed_s"}
     result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
     if not args.no_prefill and args.prefill_tokens > 0:
         result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens,
@@ -723,6 +747,49 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
             "avg_launch_us": round(tot_t / nlaunch * 1e6, 3), "per_shape": shapes,
             "timing": "HIP events around graph replays of each launch position's 32 back-to-back launches",
             "bytes_per_launch_def": "sum over the launch's matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y)"}
+
+
+def engine_decode(gh, L, launch_args, yb, outs_launches, stream, timed):
+    """The same decode chain (the bench's 128 launches per token with their real data dependencies) on the
+    persistent LDS-DMA engine: one launch per token (q4_0_engine.hip).  Timed like the per-launch graph
+    (barrier + synchronize around `steps` replays of a graph holding the one launch); self-check: every
+    output of the last layer bitwise equal to the per-launch graph's (same weights, same input)."""
+    tasks = []
+    for kind, a in launch_args:
+        if kind == "multi":
+            n, wp, mp, K, yp, xp = a
+            tasks.append(([wp[i] for i in range(n)], [mp[i] for i in range(n)], K, xp, [yp[i] for i in range(n)]))
+        else:
+            name, K, M, m_loc, buf, rb, ylocal, _, xp = a
+            tasks.append(([buf.ptr], [m_loc], K, xp, [ylocal.ptr]))
+    ch = gh.Chain(tasks)
+    on = ch.set_engine(1)
+    out = {"on": bool(on)}
+    if not on:
+        out["declined"] = L.ggml_hip_last_error().decode(errors="replace")
+        return out
+    for i in range(len(outs_launches)):          # the engine must write every output itself
+        gh.check(L.ggml_hip_memset(yb[i].ptr, 0xFF, outs_launches[i].size * 4, stream))
+    ch.launch(stream)
+    gh.check(L.ggml_hip_stream_synchronize(stream))
+    g = gh.Graph(stream)
+    with g:
+        ch.launch(stream)
+    el = timed(g.launch)
+    st = ch.status()
+    same = all(np.array_equal(yb[i].download((o.size,), np.float32, stream=stream).view(np.uint32), o.view(np.uint32))
+               for i, o in enumerate(outs_launches))
+    info = ch.engine_info()
+    out.update({"elapsed_s": el, "status": st, "bitwise_vs_launches": bool(same), "units": info["units"],
+                "cus": info["cus"], "max_cu_stream_bytes": info["max_stream_bytes"],
+                "weight_bytes": info["weight_bytes"],
+                "structure": "per CU: 1 loader wave (global_load_lds_dwordx4, 40 x 1 KiB in flight, 128 KiB LDS ring) + "
+                             "4 consumer waves (the decode GEMV's per-row arithmetic); edges = q8_0 granules "
+                             "quantized once by the producing CU, swept by one consumer wave per CU"})
+    if st != 0:
+        out["error"] = L.ggml_hip_last_error().decode(errors="replace")
+    del g
+    return out
 
 
 def exact_decode(gh, L, decode_step, stream, args):

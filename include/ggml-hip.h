@@ -211,9 +211,21 @@ typedef struct ggml_hip_chain ggml_hip_chain;
 int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **chain);
 /* Stream-ordered (graph-capturable): one GEMV launch per task. */
 int ggml_hip_chain_launch(ggml_hip_chain *chain, void *stream);
-/* Synchronizes the device; 0 (kept for source compatibility with the in-launch designs). */
+/* Synchronizes the device; 0, or (engine) the nonzero error bits of a bounded wait that expired. */
 int ggml_hip_chain_status(ggml_hip_chain *chain);
 int ggml_hip_chain_destroy(ggml_hip_chain *chain);
+/* The persistent decode engine: the whole chain as ONE launch, one workgroup per CU, a loader
+ * wave streaming each CU's weight rows by LDS-DMA ahead across the dependency edges, the edges carried by q8_0
+ * blocks quantized once by their producer.  Results are bitwise those of the per-launch chain.  It takes chains
+ * in which every task t >= 1 reads x = y[i] of task t - 1 (the same pointer, its first K values), task 0 reads an
+ * x that no task writes, K <= 12288, and any output region written again later is ordered by the edges; other
+ * chains, and every launch in exact mode, keep the per-launch path.  It needs the device to itself while it
+ * runs (all workgroups co-resident); every wait is bounded (GGML_HIP_ENGINE_TIMEOUT_MS, default 2000) and
+ * chain_status reports an expired one.  mode 1 on (builds the plan; returns 1 when the engine runs the chain, 0
+ * when it declined: ggml_hip_last_error says why), 0 off, -1 query.  GGML_HIP_CHAIN_ENGINE=1 turns it on at
+ * create.  info: [0] engine on, [1] work units, [2] largest per-CU stream (bytes), [3] weight bytes, [4] CUs. */
+int ggml_hip_chain_set_engine(ggml_hip_chain *chain, int mode);
+int ggml_hip_chain_engine_info(ggml_hip_chain *chain, int64_t *info, int n);
 
 /* ------------------------------------------------------------------------------------------
  * Multi-GPU, one process per GPU (torch.distributed-style ranks), RCCL over xGMI.

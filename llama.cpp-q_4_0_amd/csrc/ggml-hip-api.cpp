@@ -166,18 +166,43 @@ int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M) {
 }
 
 // ------------------------------------------------------------------------------------------
-// decode chains: tasks validated once, launched as stream-ordered sibling GEMVs (one launch per task).
-// Round 2 ran a chain as one persistent launch and round 4 as overlapped launches on two streams with
-// per-workgroup flag hand-offs; both were bitwise equal and measured slower than one
-// kernel per task (the in-launch hand-off costs more than a kernel boundary plus the GEMV's prologue),
-// so a chain is the per-launch path.
+// decode chains: tasks validated once, launched as stream-ordered sibling GEMVs (one launch per task), or
+// (ggml_hip_chain_set_engine / GGML_HIP_CHAIN_ENGINE) as ONE launch of the persistent LDS-DMA decode engine
+// (q4_0_engine.hip), bitwise the same y.  Round 2 ran a chain as one persistent launch and round 4 as
+// overlapped launches on two streams with per-workgroup flag hand-offs; both were bitwise
+// equal and slower than one kernel per task.  The engine differs in what those lacked: one loader wave per
+// CU streams the weights by LDS-DMA ahead across the edges, and an edge moves q8_0 granules quantized once.
 
 }  // extern "C"
 
 struct ggml_hip_chain {
     int device = 0;
     std::vector<ggml_hip_chain_task> tasks;
+    ghip::EnginePlan *eng = nullptr;  // the engine's plan when the chain runs on it
+    int eng_mode = 0;                 // 0 per-launch, 1 engine requested
+    std::string eng_why;              // why the engine declined the chain (empty when it runs)
 };
+
+namespace {
+int engine_env() {
+    const char *e = getenv("GGML_HIP_CHAIN_ENGINE");
+    return e ? atoi(e) : 0;
+}
+uint32_t engine_timeout_ticks() {       // s_memrealtime ticks (100 MHz); GGML_HIP_ENGINE_TIMEOUT_MS, default 2 s
+    const char *e = getenv("GGML_HIP_ENGINE_TIMEOUT_MS");
+    double ms = e ? atof(e) : 2000.0;
+    if (!(ms > 0.0)) ms = 2000.0;
+    if (ms > 40000.0) ms = 40000.0;     // fits 32 bits of ticks
+    return (uint32_t)(ms * 1e5);
+}
+int chain_engine_on(ggml_hip_chain *c) {
+    if (c->eng) return 1;
+    c->eng_why.clear();
+    const int ncu = g_dev[c->device].info.num_cus;
+    c->eng = ghip::engine_plan_create((int)c->tasks.size(), c->tasks.data(), ncu, engine_timeout_ticks(), c->eng_why);
+    return c->eng ? 1 : 0;
+}
+}  // namespace
 
 extern "C" {
 
@@ -204,7 +229,39 @@ int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip
     auto *c = new ggml_hip_chain();
     c->device = current_device();
     c->tasks.assign(tasks, tasks + ntasks);
+    if (engine_env() == 1) {
+        c->eng_mode = 1;
+        (void)chain_engine_on(c);           // a declined chain keeps the per-launch path
+    }
     *out = c;
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_chain_set_engine(ggml_hip_chain *c, int mode) {
+    ensure_init();
+    if (!c || mode < -1 || mode > 1) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    if (mode == -1) return c->eng ? 1 : 0;
+    if (current_device() != c->device) return fail(GGML_HIP_ERR_INVALID, "chain belongs to another device");
+    c->eng_mode = mode;
+    if (mode == 0) {
+        if (c->eng) {
+            HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());   // no launch of the plan in flight
+            ghip::engine_plan_destroy(c->eng);
+            c->eng = nullptr;
+        }
+        return 0;
+    }
+    if (chain_engine_on(c)) return 1;
+    g_last_error = c->eng_why;
+    return 0;
+}
+
+int ggml_hip_chain_engine_info(ggml_hip_chain *c, int64_t *info, int n) {
+    if (!c || !info || n < 1) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    int64_t v[5] = {c->eng ? 1 : 0, 0, 0, 0, 0};
+    if (c->eng) ghip::engine_plan_info(c->eng, v + 1);
+    for (int i = 0; i < n && i < 5; i++) info[i] = v[i];
+    if (!c->eng && !c->eng_why.empty()) g_last_error = c->eng_why;
     return GGML_HIP_OK;
 }
 
@@ -213,6 +270,10 @@ int ggml_hip_chain_launch(ggml_hip_chain *c, void *stream) {
     if (!c) return fail(GGML_HIP_ERR_INVALID, "null chain");
     if (current_device() != c->device) return fail(GGML_HIP_ERR_INVALID, "chain belongs to another device");
     hipStream_t s = resolve_stream(stream);
+    if (c->eng && !exact_mode()) {          // exact mode: the per-launch exact kernels
+        HIP_RET(ghip::engine_launch(c->eng, s));
+        return GGML_HIP_OK;
+    }
     for (const auto &k : c->tasks) {
         const int rc = ggml_hip_mul_mat_q4_0_multi(k.nmat, k.W, k.M, k.K, k.x, 1, (float *const *)k.y, s);
         if (rc != GGML_HIP_OK) return rc;
@@ -223,10 +284,24 @@ int ggml_hip_chain_launch(ggml_hip_chain *c, void *stream) {
 int ggml_hip_chain_status(ggml_hip_chain *c) {
     if (!c) return fail(GGML_HIP_ERR_INVALID, "null chain");
     HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
+    if (c->eng) {                           // sticky error bits of the engine's bounded waits
+        uint64_t detail = 0;
+        const int bits = ghip::engine_status(c->eng, &detail);
+        if (bits < 0) return fail(GGML_HIP_ERR_DEVICE, "engine status read failed");
+        if (bits) {
+            g_last_error = "decode engine: a bounded wait expired (bits " + std::to_string(bits) + ", first at CU " +
+                           std::to_string(detail >> 8) + " code " + std::to_string(detail & 0xFF) + ")";
+            return bits;
+        }
+    }
     return 0;
 }
 
 int ggml_hip_chain_destroy(ggml_hip_chain *c) {
+    if (c && c->eng) {
+        (void)GHIP_SYNC(hipDeviceSynchronize)();
+        ghip::engine_plan_destroy(c->eng);
+    }
     delete c;
     return GGML_HIP_OK;
 }

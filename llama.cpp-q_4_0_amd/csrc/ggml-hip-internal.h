@@ -62,6 +62,17 @@
         }                                                                                            \
     } while (0)
 
+// ---- the persistent decode engine (q4_0_engine.hip): a chain of dependent N = 1 mul_mats as one launch
+namespace ghip {
+struct EnginePlan;
+EnginePlan *engine_plan_create(int ntasks, const ggml_hip_chain_task *tasks, int ncu, uint32_t timeout_ticks,
+                               std::string &why);
+hipError_t engine_launch(EnginePlan *p, hipStream_t s);
+int engine_status(EnginePlan *p, uint64_t *detail);
+void engine_plan_destroy(EnginePlan *p);
+void engine_plan_info(const EnginePlan *p, int64_t *info);   // units, max CU stream bytes, weight bytes, CUs
+}  // namespace ghip
+
 namespace ghh {
 
 using gabi::tensor;

@@ -112,6 +112,8 @@ def _bind(L):
         "ggml_hip_chain_launch": ([vp, vp], i32),
         "ggml_hip_chain_status": ([vp], i32),
         "ggml_hip_chain_destroy": ([vp], i32),
+        "ggml_hip_chain_set_engine": ([vp, i32], i32),
+        "ggml_hip_chain_engine_info": ([vp, vp, i32], i32),
         "ggml_hip_last_error": ([], cp),
         "ggml_hip_version": ([], cp),
     }
@@ -256,7 +258,7 @@ class Chain:
     """A decode chain (ggml_hip_chain_*): tasks = [(ws, Ms, K, x, ys), ...] run in stream order, one
     sibling GEMV per task; task t reads x after every earlier task wrote its y."""
 
-    def __init__(self, tasks):
+    def __init__(self, tasks, engine=None):
         L = load()
         arr = (ChainTask * len(tasks))()
         for t, (ws, Ms, K, x, ys) in enumerate(tasks):
@@ -269,6 +271,22 @@ class Chain:
                 arr[t].y[i] = _ptr(ys[i])
         self.h = ctypes.c_void_p()
         check(L.ggml_hip_chain_create(len(tasks), arr, ctypes.byref(self.h)), "chain_create")
+        if engine is not None:
+            self.set_engine(engine)
+
+    def set_engine(self, on):
+        """1 on (returns True when the persistent engine runs the chain), 0 off; the reason of a decline is
+        in ggml_hip_last_error()"""
+        rc = load().ggml_hip_chain_set_engine(self.h, 1 if on else 0)
+        if rc < 0:
+            check(rc, "chain_set_engine")
+        return rc == 1
+
+    def engine_info(self):
+        """{on, units, max_stream_bytes, weight_bytes, cus} of the engine's plan (on = 0: per-launch path)"""
+        v = (ctypes.c_int64 * 5)()
+        check(load().ggml_hip_chain_engine_info(self.h, v, 5), "chain_engine_info")
+        return dict(zip(("on", "units", "max_stream_bytes", "weight_bytes", "cus"), list(v)))
 
     def launch(self, stream=None):
         check(load().ggml_hip_chain_launch(self.h, stream), "chain_launch")

@@ -224,3 +224,144 @@ def test_chain_invalid_arguments():
     assert L.ggml_hip_chain_launch(h, None) == ggml_hip.OK
     assert L.ggml_hip_chain_status(h) == 0
     assert L.ggml_hip_chain_destroy(h) == ggml_hip.OK
+
+
+# ---- the persistent decode engine (ggml_hip_chain_set_engine; q4_0_engine.hip) -----------------------------
+def _engine_chain(spec, seed):
+    c = ChainCase(spec, seed=seed)
+    ch = ggml_hip.Chain(c.tasks(0))
+    on = ch.set_engine(1)
+    return c, ch, on
+
+
+def test_engine_llama7b_two_layers_bitwise():
+    """Full LLaMA-7B layer shapes (wq|wk|wv -> wo -> w1|w3 -> w2, x of each task = an output of the previous
+    one, as llama.cpp:1334-1500 chains them): the engine's ONE launch reproduces the per-launch GEMVs bit for
+    bit over three launches with fresh inputs (stale granules or stale x would show)."""
+    c, ch, on = _engine_chain(llama_layers(2), 5)
+    assert on, ggml_hip.load().ggml_hip_last_error()
+    info = ch.engine_info()
+    assert info["on"] == 1 and info["units"] > 0
+    for rep in range(3):
+        c.randomize(50 + rep)
+        ch.launch()
+        c.run_separate()
+        assert ch.status() == 0, ggml_hip.load().ggml_hip_last_error()
+        assert_bitwise(c.outputs(0), c.outputs(1))
+
+
+def test_engine_ragged_linear_chain_bitwise():
+    """Ragged shapes on a linear chain: M not a multiple of 32 (partial units), prefix x (K < M of the
+    producer), one-row and 33-row siblings, K = 64 (one pair per row), K = 4544 (2 pairs per lane), K = 11008 and
+    12288 (3 per lane), rows that wrap the LDS ring."""
+    spec = [(4096, [4100, 1, 33], None),      # consumed: the 4100-row output (prefix 4096 read next)
+            (4096, [777, 64], 0),            # x = task 0's first output, prefix
+            (640, [4544], 1),                # K 640 < 777: prefix of task 1's output 0
+            (4544, [12288, 5], 2),           # Falcon K
+            (12288, [256], 3),               # K = 12288: 3 pairs per lane, 6912-byte rows
+            (256, [11008], 4),
+            (11008, [96, 3], 5),
+            (64, [64], 6)]                   # K = 64: one pair, lanes 1..63 idle
+    c, ch, on = _engine_chain(spec, 6)
+    assert on, ggml_hip.load().ggml_hip_last_error()
+    for rep in range(2):
+        c.randomize(60 + rep)
+        ch.launch()
+        c.run_separate()
+        assert ch.status() == 0, ggml_hip.load().ggml_hip_last_error()
+        assert_bitwise(c.outputs(0), c.outputs(1))
+
+
+def test_engine_many_tasks_and_replays():
+    """600 dependent tasks (the epoch tags of 600 x 4 units' granules), eager and as a replayed HIP graph."""
+    spec = [(128, [128], None)] + [(128, [128], t) for t in range(599)]
+    c, ch, on = _engine_chain(spec, 7)
+    assert on
+    c.randomize(70)
+    ch.launch()
+    c.run_separate()
+    assert ch.status() == 0
+    assert_bitwise(c.outputs(0), c.outputs(1))
+    g = ggml_hip.Graph(None)
+    with g:
+        ch.launch(ggml_hip.load().ggml_hip_default_stream())
+    for rep in range(3):
+        c.randomize(71 + rep)
+        g.launch()
+        c.run_separate()
+        assert ch.status() == 0
+        assert_bitwise(c.outputs(0), c.outputs(1))
+
+
+def test_engine_graph_replay_llama_layer():
+    c, ch, on = _engine_chain(llama_layers(1, K=1024, F=2816), 8)
+    assert on
+    g = ggml_hip.Graph(None)
+    with g:
+        ch.launch(ggml_hip.load().ggml_hip_default_stream())
+    for rep in range(4):
+        c.randomize(80 + rep)
+        g.launch()
+        c.run_separate()
+        assert ch.status() == 0
+        assert_bitwise(c.outputs(0), c.outputs(1))
+
+
+def test_engine_declines_nonlinear_chains_and_stays_correct():
+    """A task whose x is not an output of the task before it (or a first x the chain writes): the engine
+    declines (ggml_hip_last_error says why) and the chain runs per launch, bitwise as before."""
+    spec = [(4096, [4100], None), (4096, [1, 33, 777], 0), (4096, [64], 0)]
+    c, ch, on = _engine_chain(spec, 9)
+    assert not on
+    assert b"not an output of task" in ggml_hip.load().ggml_hip_last_error()
+    assert ch.engine_info()["on"] == 0
+    c.randomize(90)
+    ch.launch()
+    c.run_separate()
+    assert ch.status() == 0
+    assert_bitwise(c.outputs(0), c.outputs(1))
+
+
+def test_engine_exact_mode_runs_per_launch():
+    L = ggml_hip.load()
+    c, ch, on = _engine_chain(llama_layers(1, K=512, F=1408), 10)
+    assert on
+    c.randomize(100)
+    L.ggml_hip_set_exact(1)
+    try:
+        ch.launch()
+        c.run_separate()
+    finally:
+        L.ggml_hip_set_exact(0)
+    assert ch.status() == 0
+    assert_bitwise(c.outputs(0), c.outputs(1))
+
+
+def test_engine_against_oracle():
+    """Every task's y of a small linear chain against the oracle on its actual input (the previous y)."""
+    spec = [(256, [224], None), (192, [320, 64], 0), (320, [256], 1), (256, [96], 2)]
+    wq, ws = [], []
+    for t, (K, Ms, _) in enumerate(spec):
+        row, wrow = [], []
+        for i, M in enumerate(Ms):
+            q, _ = O.quantize_q4_0(O.gaussian(M * K, 0xA100 + 8 * t + i, 0.0, 0.05).reshape(M, K))
+            row.append(q)
+            wrow.append(DB.from_array(q))
+        wq.append(row)
+        ws.append(wrow)
+    ys = [[DB(M * 4) for M in Ms] for (_, Ms, _) in spec]
+    x0 = O.gaussian(256, 0xB100, 0.0, 1.0).astype(np.float32)
+    xd0 = DB.from_array(x0)
+    xs = [xd0 if src is None else ys[src][0] for (_, _, src) in spec]
+    ch = ggml_hip.Chain([(ws[t], Ms, K, xs[t], ys[t]) for t, (K, Ms, _) in enumerate(spec)], engine=1)
+    assert ch.engine_info()["on"] == 1
+    ch.launch()
+    assert ch.status() == 0
+    for t, (K, Ms, src) in enumerate(spec):
+        xin = x0 if src is None else ys[src][0].download((spec[src][1][0],), np.float32)[:K]
+        xq = O.quantize_q8_0(xin.reshape(1, K), "avx2")
+        for i, M in enumerate(Ms):
+            y = ys[t][i].download((1, M), np.float32)
+            y_ref = O.mul_mat(wq[t][i], K, xin.reshape(1, K), nthreads=1)
+            _, s_abs = block_terms(wq[t][i], xq, K)
+            check_y(y, y_ref, s_abs, rtol=1e-3, atol_blocks=1e-6)

@@ -256,6 +256,13 @@ int ggml_hip_chain_set_engine(ggml_hip_chain *c, int mode) {
     return 0;
 }
 
+// diagnostics (not in the header): per-CU stamps of the engine's last launch (tools/engine_stamps.py)
+int ggml_hip_debug_engine_stamps(ggml_hip_chain *c, uint64_t *out, int64_t n) {
+    if (!c || !c->eng) return -1;
+    (void)GHIP_SYNC(hipDeviceSynchronize)();
+    return ghip::engine_stamps(c->eng, out, n);
+}
+
 int ggml_hip_chain_engine_info(ggml_hip_chain *c, int64_t *info, int n) {
     if (!c || !info || n < 1) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
     int64_t v[5] = {c->eng ? 1 : 0, 0, 0, 0, 0};

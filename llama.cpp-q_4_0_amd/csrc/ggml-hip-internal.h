@@ -71,6 +71,7 @@ hipError_t engine_launch(EnginePlan *p, hipStream_t s);
 int engine_status(EnginePlan *p, uint64_t *detail);
 void engine_plan_destroy(EnginePlan *p);
 void engine_plan_info(const EnginePlan *p, int64_t *info);   // units, max CU stream bytes, weight bytes, CUs
+int engine_stamps(EnginePlan *p, uint64_t *out, int64_t n);
 }  // namespace ghip
 
 namespace ghh {

@@ -86,7 +86,12 @@ struct EngArgs {
     const EngCU *cus;
     uint64_t *ctl;              // [0] epoch, [1] arrivals, [2] error bits, [3] first error site
     uint32_t timeout;           // ticks of s_memrealtime
+    uint32_t diag;              // diagnostics only (GGML_HIP_ENGINE_DIAG): 1 the gather takes granules unchecked,
+                                // 2 the consumers skip the row arithmetic (results wrong in both)
+    uint64_t *stamps;           // diagnostics only (GGML_HIP_ENGINE_STAMPS=1): per CU ENG_ST_HDR header words +
+                                // ENG_ST_TASKS x 4 per-task stamps of consumer wave 0, or nullptr
 };
+constexpr int ENG_ST_HDR = 8, ENG_ST_TASKS = 160, ENG_ST_CU = ENG_ST_HDR + 4 * ENG_ST_TASKS;
 
 typedef __attribute__((address_space(1))) uint64_t g_u64;
 // the tables are read through the constant address space: wave-uniform scalar loads (SMEM) that neither wait
@@ -286,10 +291,12 @@ __device__ __forceinline__ void eng_task_rows(const EngArgs &a, uint32_t *ctl, c
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 while (cld(ctl + C_LANDED) < end)
                     if (!eng_spin(a, ctl, t0, ENG_E_LANDED)) { abort = true; return; }
+                if (a.stamps && w == 0 && lane == 0)           // wave 0's ticks waiting for landed lines
+                    a.stamps[(uint64_t)blockIdx.x * ENG_ST_CU + 3] += __builtin_amdgcn_s_memrealtime() - t0;
             }
             asm volatile("" ::: "memory");
             const uint32_t rb = start & (ENG_RING - 1);
-            const float out = eng_row<PPL>(ring, rb, rb + tk.rowbytes > ENG_RING, x, npairs, lane);
+            const float out = (a.diag & 2) ? 0.0f : eng_row<PPL>(ring, rb, rb + tk.rowbytes > ENG_RING, x, npairs, lane);
             if (consumed) {
                 if (lane == 0) par[slot * 32 + r] = out;
                 uint32_t old = 0;
@@ -341,8 +348,11 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
     __syncthreads();
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t *)elds);   // ring's LDS address
 
+    uint64_t *st = a.stamps ? a.stamps + (uint64_t)blockIdx.x * ENG_ST_CU : nullptr;
     if (w == ENG_NC) {
         // ---------------- loader: the CU's stream, line by line, into the ring
+        const uint64_t tl0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t ring_wait = 0;
         const uint32_t nlines = (cu.stream_bytes + ENG_LINE - 1) / ENG_LINE;
         uint32_t ui = cu.unit0;
         uint32_t uend_b = 0, usoff = 0, ubytes = 0;
@@ -380,6 +390,7 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
+                ring_wait += __builtin_amdgcn_s_memrealtime() - t0;
                 if (!ok) break;
             }
             const uint32_t off = s0 - usoff + 16u * (uint32_t)lane;       // byte of the unit
@@ -397,6 +408,11 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may outlive the workgroup
         if (lane == 0) eng_st_asm(lds0 + L_CTL + C_LANDED * 4, ok ? 0xFFFFFFFFu : 0u);
+        if (st && lane == 0) {                  // loader start, end, ticks waiting for ring space
+            st[0] = tl0;
+            st[1] = __builtin_amdgcn_s_memrealtime();
+            st[2] = ring_wait;
+        }
     } else {
         // ---------------- consumers
         uint32_t ui = cu.unit0;
@@ -410,6 +426,11 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
             const uint32_t task = ld_unit(a.units, ui).tmn & 0xFFFFu;
             const EngTask tk = ld_task(a.tasks, task);
             ntask++;
+            uint64_t *sk = st && ntask <= (uint32_t)ENG_ST_TASKS ? st + ENG_ST_HDR + 4 * (ntask - 1) : nullptr;
+            if (w == 0 && sk && lane == 0) {
+                sk[0] = __builtin_amdgcn_s_memrealtime();
+                sk[3] = task;
+            }
             if (w == 0) {
                 // ---- gather x of this task into LDS (after every wave loaded the previous task's x)
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -447,7 +468,7 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
                                 g[k] = idx < ng ? __hip_atomic_load((const g_u64 *)(tk.xgran + idx), __ATOMIC_RELAXED,
                                                                     __HIP_MEMORY_SCOPE_AGENT)
                                                 : (uint64_t)tag << 48;
-                                okl &= (uint32_t)(g[k] >> 48) == tag;
+                                okl &= (uint32_t)(g[k] >> 48) == tag || (a.diag & 1);
                             }
                             if (__builtin_amdgcn_ballot_w64(!okl) == 0) break;   // no lane still waiting
                             if (!eng_spin(a, ctl, t1, ENG_E_GATHER)) { abort = true; break; }
@@ -476,6 +497,7 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
                 if (abort) break;
             }
             asm volatile("" ::: "memory");
+            if (w == 0 && sk && lane == 0) sk[1] = __builtin_amdgcn_s_memrealtime();
             const int ppl = ((int)tk.npairs + 63) >> 6;
             if (ppl == 1)
                 eng_task_rows<1>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort);
@@ -483,6 +505,7 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
                 eng_task_rows<2>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort);
             else
                 eng_task_rows<3>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort);
+            if (w == 0 && sk && lane == 0) sk[2] = __builtin_amdgcn_s_memrealtime();
         }
         if (lane == 0) cst(ctl + C_PROG + w, 0xFFFFFFFFu);   // never holds the loader back again
     }
@@ -506,7 +529,8 @@ struct EnginePlan {
     EngCU *d_cus = nullptr;
     uint64_t *d_ctl = nullptr;
     uint64_t *d_gran = nullptr;
-    uint32_t timeout = 0;
+    uint32_t timeout = 0, diag = 0;
+    uint64_t *d_stamps = nullptr;
     size_t units = 0;
     uint64_t max_stream = 0, total_bytes = 0;
 };
@@ -518,6 +542,7 @@ static void plan_free(EnginePlan *p) {
     if (p->d_cus) (void)hipFree(p->d_cus);
     if (p->d_ctl) (void)hipFree(p->d_ctl);
     if (p->d_gran) (void)hipFree(p->d_gran);
+    if (p->d_stamps) (void)hipFree(p->d_stamps);
     delete p;
 }
 
@@ -700,8 +725,23 @@ EnginePlan *engine_plan_create(int T, const ggml_hip_chain_task *tk, int ncu, ui
         plan_free(p);
         return decline(std::string("engine: ") + hipGetErrorString(e));
     }
+    if (const char *d = getenv("GGML_HIP_ENGINE_DIAG")) p->diag = (uint32_t)atoi(d);
+    if (getenv("GGML_HIP_ENGINE_STAMPS") && atoi(getenv("GGML_HIP_ENGINE_STAMPS")) == 1) {
+        const size_t n = (size_t)ncu * ENG_ST_CU * 8;
+        if (hipMalloc(&p->d_stamps, n) != hipSuccess || hipMemset(p->d_stamps, 0, n) != hipSuccess) p->d_stamps = nullptr;
+    }
     (void)hipGetDevice(&p->device);
     return p;
+}
+
+// diagnostics: the stamps of the last launch (GGML_HIP_ENGINE_STAMPS=1 at plan creation), zeroed after the copy
+int engine_stamps(EnginePlan *p, uint64_t *out, int64_t n) {
+    if (!p->d_stamps) return -1;
+    const int64_t need = (int64_t)p->ncu * ENG_ST_CU;
+    if (n < need) return (int)need;
+    if (hipMemcpy(out, p->d_stamps, need * 8, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+    if (hipMemset(p->d_stamps, 0, need * 8) != hipSuccess) return -2;
+    return (int)need;
 }
 
 hipError_t engine_launch(EnginePlan *p, hipStream_t s) {
@@ -719,6 +759,8 @@ hipError_t engine_launch(EnginePlan *p, hipStream_t s) {
     a.cus = p->d_cus;
     a.ctl = p->d_ctl;
     a.timeout = p->timeout;
+    a.diag = p->diag;
+    a.stamps = p->d_stamps;
     (void)hipGetLastError();
     launch_k(k_engine_q4_0, dim3((unsigned)p->ncu), dim3(ENG_THREADS), ENG_LDS, s, a);
     return hipGetLastError();

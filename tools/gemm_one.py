@@ -1,4 +1,4 @@
-"""One prefill GEMM shape timed on the device (the PMC passes of tools/r4_final.sh profile it):
+"""One prefill GEMM shape timed on the device (the PMC passes of tools/run.sh PARTS=gpmc profile it):
 K x M weights (fp6 image built per call under GGML_HIP_GEMM_V=11, or registered once with IMAGE=1), N tokens.
 Usage: [K=4096 M=4096 N=512 IMAGE=1] python tools/gemm_one.py"""
 import os

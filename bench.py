@@ -271,7 +271,7 @@ def main():
     ap.add_argument("--decode", choices=("auto", "engine", "launches"), default="auto",
                     help="headline decode path: the persistent LDS-DMA engine (one launch per token, "
                          "ggml_hip_chain_set_engine), the per-launch graph (4 sibling GEMVs per layer), or auto = "
-                         "the engine when it plans the chain and its outputs are bitwise the launches'")
+                         "the engine when its outputs are bitwise the launches' and it ran faster (both are timed)")
     ap.add_argument("--deadline", type=float, default=300.0,
                     help="N > 1: seconds after which a rank that has not finished aborts its communicator and exits "
                          "(rank 0 prints an error line); the self-launcher terminates its ranks 30 s later")
@@ -435,7 +435,14 @@ def main():
         engine = engine_decode(gh, L, launch_args, yb, outs_launches, stream, timed)
         if args.decode == "engine" and not engine.get("on"):
             raise SystemExit(f"--decode engine: the engine declined the chain: {engine.get('declined')}")
-    use_engine = engine is not None and engine.get("on") and engine["bitwise_vs_launches"] and engine["status"] == 0
+    # the engine is the headline only when asked for, or (auto) when it checked bitwise AND ran faster than the
+    # per-launch graph; round 6 measured it slower (profiles/r06_engine_variants.txt), so auto keeps
+    # the launches and the line carries both
+    engine_ok = engine is not None and engine.get("on") and engine["bitwise_vs_launches"] and engine["status"] == 0
+    use_engine = engine_ok and (args.decode == "engine" or engine["elapsed_s"] < elapsed_launches)
+    if engine is not None and engine.get("on"):
+        engine["tok_s"] = round(args.steps / engine["elapsed_s"] * 32 / args.layers, 2)
+        engine["ms_per_step"] = round(engine["elapsed_s"] / args.steps * 1e3, 4)
     elapsed = engine["elapsed_s"] if use_engine else elapsed_launches
     ms_per_step = elapsed / args.steps * 1e3
     tok_s = args.steps / elapsed * 32 / args.layers if args.layers else 0.0   # per full 32-layer token

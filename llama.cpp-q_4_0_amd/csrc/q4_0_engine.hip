@@ -40,11 +40,30 @@
 
 namespace ghip {
 
-constexpr int ENG_NC = 4;                       // consumer waves (wave ENG_NC is the loader)
+#ifndef ENG_NC_DEF
+#define ENG_NC_DEF 8
+#endif
+#ifndef ENG_PRIO
+#define ENG_PRIO 0          // the loader wave's s_setprio (variants)
+#endif
+#ifndef ENG_G_DEF
+#define ENG_G_DEF 16
+#endif
+#ifndef ENG_THIN
+#define ENG_THIN 0          // lines the loader keeps in flight while its CU sweeps granules (0: not thinned)
+#endif
+#ifndef ENG_SLEEP
+#define ENG_SLEEP 1         // s_sleep argument of the consumers' spin steps
+#endif
+// consumer waves (wave ENG_NC is the loader): a consumer row is a serial chain of LDS reads, VALU, a DPP tree and
+// the output store (~500+ cycles), so rows in flight need waves: 4 consumers (one per SIMD) retired ~18 GB/s per
+// CU, below the loader's stream
+constexpr int ENG_NC = ENG_NC_DEF;
 constexpr int ENG_THREADS = (ENG_NC + 1) * 64;
 constexpr uint32_t ENG_RING = 128u * 1024u;     // LDS ring (power of two)
 constexpr uint32_t ENG_LINE = 1024u;            // one LDS-DMA instruction: 64 lanes x 16 B
 constexpr int ENG_D = 40;                       // lines in flight per loader (vmcnt <= 63)
+constexpr int ENG_G = ENG_G_DEF;                // lines per loader step (control work once per step)
 constexpr int ENG_MAXNB = 384;                  // K <= 12288 (3 block pairs per lane)
 constexpr int ENG_SLOTS = 16;                   // park slots of consumed units (32 floats each)
 // LDS layout (bytes)
@@ -53,10 +72,12 @@ constexpr uint32_t L_XD = L_XQ + ENG_MAXNB * 32;              // float [nb]: h2f
 constexpr uint32_t L_XS = L_XD + ENG_MAXNB * 4;               // int [nb]: 8 * sum(q)
 constexpr uint32_t L_PAR = L_XS + ENG_MAXNB * 4;              // float [SLOTS][32]
 constexpr uint32_t L_CTL = L_PAR + ENG_SLOTS * 32 * 4;        // uint32 control words
-enum { C_LANDED = 0, C_PROG = 4, C_XGEN = 8, C_XLOADED = 9, C_ABORT = 10, C_CNT = 16, C_QDONE = 32, C_WORDS = 48 };
+enum { C_LANDED = 0, C_XGEN = 1, C_XLOADED = 2, C_ABORT = 3, C_PROG = 4, C_CNT = 20, C_QDONE = 36, C_GATHER = 52,
+       C_WORDS = 56 };
 constexpr uint32_t ENG_LDS = L_CTL + C_WORDS * 4;
 static_assert(ENG_LDS <= 160 * 1024, "engine LDS");
-static_assert(C_PROG + ENG_NC <= C_XGEN && C_CNT + ENG_SLOTS <= C_QDONE && C_QDONE + ENG_SLOTS <= C_WORDS, "ctl words");
+static_assert(ENG_NC >= 1 && ENG_NC <= 12 && C_PROG + 16 <= C_CNT && C_CNT + ENG_SLOTS <= C_QDONE &&
+              C_QDONE + ENG_SLOTS <= C_WORDS, "ctl words");
 
 // error bits (ctl[2]); ctl[3] = the first timeout's site (CU << 8 | code)
 enum { ENG_E_LOADER = 1, ENG_E_LANDED = 2, ENG_E_XGEN = 4, ENG_E_GATHER = 8, ENG_E_SLOT = 16, ENG_E_XLOADED = 32 };
@@ -87,11 +108,14 @@ struct EngArgs {
     uint64_t *ctl;              // [0] epoch, [1] arrivals, [2] error bits, [3] first error site
     uint32_t timeout;           // ticks of s_memrealtime
     uint32_t diag;              // diagnostics only (GGML_HIP_ENGINE_DIAG): 1 the gather takes granules unchecked,
-                                // 2 the consumers skip the row arithmetic (results wrong in both)
+                                // 2 the consumers skip the row arithmetic, 4 no y stores of unconsumed rows
+                                // (results wrong in all three)
     uint64_t *stamps;           // diagnostics only (GGML_HIP_ENGINE_STAMPS=1): per CU ENG_ST_HDR header words +
-                                // ENG_ST_TASKS x 4 per-task stamps of consumer wave 0, or nullptr
+                                // ENG_ST_TASKS x ENG_ST_W per-task stamps, or nullptr: [0] wave 0 starts the task
+                                // (gather), [1] x in LDS, [2] wave 0's last row, [3] task id, [4] the CU's last
+                                // granule publish of the task (max), [5] wave 0's first row consumed
 };
-constexpr int ENG_ST_HDR = 8, ENG_ST_TASKS = 160, ENG_ST_CU = ENG_ST_HDR + 4 * ENG_ST_TASKS;
+constexpr int ENG_ST_HDR = 8, ENG_ST_TASKS = 160, ENG_ST_W = 6, ENG_ST_CU = ENG_ST_HDR + ENG_ST_W * ENG_ST_TASKS;
 
 typedef __attribute__((address_space(1))) uint64_t g_u64;
 // the tables are read through the constant address space: wave-uniform scalar loads (SMEM) that neither wait
@@ -152,6 +176,17 @@ __device__ __forceinline__ u32x4 eng_ld4_asm(uint32_t addr) {
     asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
     return v;
 }
+// the consumers' minimum progress (loader): the NC words by ds_read_b128
+__device__ __forceinline__ uint32_t eng_min_prog(uint32_t addr) {
+    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+    for (int q = 0; q < (ENG_NC + 3) / 4; q++) {     // the words past NC hold ~0 (kernel start)
+        const u32x4 pg = eng_ld4_asm(addr + 16 * q);
+        m = min(m, min(min(pg.x, pg.y), min(pg.z, pg.w)));
+    }
+    return __builtin_amdgcn_readfirstlane(m);
+}
+
 __device__ __forceinline__ uint32_t eng_ld_asm(uint32_t addr) {
     uint32_t v;
     asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
@@ -178,7 +213,7 @@ __device__ __forceinline__ bool eng_spin(const EngArgs &a, uint32_t *ctl, uint64
         eng_fail(a, ctl, code);
         return false;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(ENG_SLEEP);
     return true;
 }
 
@@ -250,7 +285,8 @@ __device__ __forceinline__ float eng_row(const uint32_t *ring, uint32_t rb, bool
 template <int PPL>
 __device__ __forceinline__ void eng_task_rows(const EngArgs &a, uint32_t *ctl, const uint32_t *ring, float *par,
                                               const EngTask &tk, uint32_t &ui, uint32_t uend, uint32_t task, int w,
-                                              int lane, uint32_t tag, bool &abort) {
+                                              int lane, uint32_t tag, bool &abort, uint64_t *sk) {
+    bool first_row = true;
     const uint32_t *xq = ring + L_XQ / 4;
     const float *xd = reinterpret_cast<const float *>(ring + L_XD / 4);
     const int *xs = reinterpret_cast<const int *>(ring + L_XS / 4);
@@ -271,8 +307,13 @@ __device__ __forceinline__ void eng_task_rows(const EngArgs &a, uint32_t *ctl, c
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_fetch_add(ctl + C_XLOADED, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     typedef __attribute__((address_space(1))) float gfloat;
+    // the next unit's descriptor is loaded while this one's rows run (a scalar-cache miss per unit otherwise
+    // stalls the wave ahead of its first row); landed is re-read only when a row lies past the value last seen
+    EngUnit Un = ld_unit(a.units, ui);
+    uint32_t lnd = 0;
     for (; ui < uend; ui++) {
-        const EngUnit U = ld_unit(a.units, ui);
+        const EngUnit U = Un;
+        if (ui + 1 < uend) Un = ld_unit(a.units, ui + 1);
         const uint32_t tmn = U.tmn;
         if ((tmn & 0xFFFFu) != task) break;
         const uint32_t mat = (tmn >> 16) & 0xFFu, nrows = tmn >> 24;
@@ -287,9 +328,10 @@ __device__ __forceinline__ void eng_task_rows(const EngArgs &a, uint32_t *ctl, c
         }
         for (; r < nrows; r += ENG_NC) {
             const uint32_t start = U.soff + r * tk.rowbytes, end = start + tk.rowbytes;
-            if (cld(ctl + C_LANDED) < end) {
+            if (lnd < end) lnd = cld(ctl + C_LANDED);
+            if (lnd < end) {
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while (cld(ctl + C_LANDED) < end)
+                while ((lnd = cld(ctl + C_LANDED)) < end)
                     if (!eng_spin(a, ctl, t0, ENG_E_LANDED)) { abort = true; return; }
                 if (a.stamps && w == 0 && lane == 0)           // wave 0's ticks waiting for landed lines
                     a.stamps[(uint64_t)blockIdx.x * ENG_ST_CU + 3] += __builtin_amdgcn_s_memrealtime() - t0;
@@ -297,6 +339,8 @@ __device__ __forceinline__ void eng_task_rows(const EngArgs &a, uint32_t *ctl, c
             asm volatile("" ::: "memory");
             const uint32_t rb = start & (ENG_RING - 1);
             const float out = (a.diag & 2) ? 0.0f : eng_row<PPL>(ring, rb, rb + tk.rowbytes > ENG_RING, x, npairs, lane);
+            if (sk && first_row && w == 0 && lane == 0) sk[5] = __builtin_amdgcn_s_memrealtime();
+            first_row = false;
             if (consumed) {
                 if (lane == 0) par[slot * 32 + r] = out;
                 uint32_t old = 0;
@@ -320,12 +364,15 @@ __device__ __forceinline__ void eng_task_rows(const EngArgs &a, uint32_t *ctl, c
                         yo[2] = v.z;
                         yo[3] = v.w;
                     }
+                    if (sk && lane == 0)
+                        __hip_atomic_fetch_max(sk + 4, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
                     if (lane == 0) {
                         cst(ctl + C_CNT + slot, 0u);
                         __hip_atomic_fetch_add(ctl + C_QDONE + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
-            } else if (lane == 0) {
+            } else if (lane == 0 && !(a.diag & 4)) {
                 ((gfloat *)sel4(tk.y, mat))[U.row0 + r] = out;
             }
             if (lane == 0) cst(ctl + C_PROG + w, end);
@@ -344,60 +391,85 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
     // tag of this launch: the epoch (advanced by the last workgroup of the previous launch), 1..65535
     const uint32_t epoch = (uint32_t)__hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t tag = epoch % 65535u + 1u;
-    if (tid < C_WORDS) ctl[tid] = 0u;
+    if (tid < C_WORDS) ctl[tid] = (tid >= C_PROG + ENG_NC && tid < C_PROG + 16) ? 0xFFFFFFFFu : 0u;
     __syncthreads();
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t *)elds);   // ring's LDS address
 
     uint64_t *st = a.stamps ? a.stamps + (uint64_t)blockIdx.x * ENG_ST_CU : nullptr;
     if (w == ENG_NC) {
         // ---------------- loader: the CU's stream, line by line, into the ring
+        if (ENG_PRIO) __builtin_amdgcn_s_setprio(ENG_PRIO);
         const uint64_t tl0 = __builtin_amdgcn_s_memrealtime();
         uint64_t ring_wait = 0;
         const uint32_t nlines = (cu.stream_bytes + ENG_LINE - 1) / ENG_LINE;
         uint32_t ui = cu.unit0;
-        uint32_t uend_b = 0, usoff = 0, ubytes = 0;
-        uint64_t usrc = 0;
+        const uint32_t uend_i = cu.unit0 + cu.nunits;
+        uint32_t uend_b = 0, usoff = 0;
+        __amdgpu_buffer_rsrc_t urs = make_rsrc(nullptr, 0);
+        EngUnit Un{};                              // the next unit's descriptor, loaded one unit ahead
+        if (cu.nunits) Un = ld_unit(a.units, ui);
         uint32_t issued = 0, pub = 0;              // lines issued; landed bytes published (monotonic)
+        uint32_t freed = 0;                        // the consumers' progress as last read (rows before it are done)
         bool ok = true;
-        for (uint32_t i = 0; i < nlines; i++) {
-            const uint32_t s0 = i * ENG_LINE;
-            while (s0 >= uend_b) {                 // next unit (units start at line boundaries)
-                const EngUnit U = ld_unit(a.units, ui++);
-                usoff = U.soff;
-                ubytes = U.bytes;
-                usrc = (uint64_t)U.src_lo | (uint64_t)U.src_hi << 32;
-                uend_b = usoff + ((ubytes + ENG_LINE - 1) & ~(ENG_LINE - 1));
-            }
-            if (s0 + ENG_LINE > ENG_RING) {        // ring space: every consumer past s0 + LINE - RING
-                const uint32_t need = s0 + ENG_LINE - ENG_RING;
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                bool drained = false;
-                for (;;) {
-                    const u32x4 pg = eng_ld4_asm(lds0 + L_CTL + C_PROG * 4);
-                    const uint32_t mn = min(min(pg.x, pg.y), min(pg.z, pg.w));
-                    if (mn >= need) break;
-                    if (!drained) {                // the consumers may be waiting for lines already issued:
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // land all of them first
-                        pub = issued * ENG_LINE;
-                        if (lane == 0) eng_st_asm(lds0 + L_CTL + C_LANDED * 4, pub);
-                        drained = true;
+        // The loop's per-line cost IS the stream rate (a 1 KiB line every ~50 ns per CU at 20 GB/s): every control
+        // step (ring-space check, landed publication) runs once per group of ENG_G lines, the lines themselves
+        // are a compare + the DMA (tools/ldsdma_mb.hip: one LDS read + lgkmcnt wait per line halved the rate)
+        for (uint32_t g0 = 0; g0 < nlines && ok; g0 += ENG_G) {
+            const uint32_t gn = min((uint32_t)ENG_G, nlines - g0);
+            const uint32_t gend = (g0 + gn) * ENG_LINE;
+            // ring space for the whole group: every consumer past gend - RING
+            if (gend > ENG_RING && gend - ENG_RING > freed) {
+                const uint32_t need = gend - ENG_RING;
+                // (every value read by the asm is made wave-uniform: a VGPR result in a loop condition makes the
+                // compiler treat the unit descriptors as divergent, load them with vector loads and drain the DMAs)
+                freed = eng_min_prog(lds0 + L_CTL + C_PROG * 4);
+                if (freed < need) {
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    bool drained = false;
+                    for (;;) {
+                        if (!drained) {            // the consumers may be waiting for lines already issued:
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // land all of them first
+                            pub = issued * ENG_LINE;
+                            if (lane == 0) eng_st_asm(lds0 + L_CTL + C_LANDED * 4, pub);
+                            drained = true;
+                        }
+                        if (__builtin_amdgcn_readfirstlane(eng_ld_asm(lds0 + L_CTL + C_ABORT * 4)) != 0u) { ok = false; break; }
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+                            eng_fail(a, ctl, ENG_E_LOADER);
+                            ok = false;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        freed = eng_min_prog(lds0 + L_CTL + C_PROG * 4);
+                        if (freed >= need) break;
                     }
-                    if (eng_ld_asm(lds0 + L_CTL + C_ABORT * 4) != 0u) { ok = false; break; }
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
-                        eng_fail(a, ctl, ENG_E_LOADER);
-                        ok = false;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
+                    ring_wait += __builtin_amdgcn_s_memrealtime() - t0;
+                    if (!ok) break;
                 }
-                ring_wait += __builtin_amdgcn_s_memrealtime() - t0;
-                if (!ok) break;
             }
-            const uint32_t off = s0 - usoff + 16u * (uint32_t)lane;       // byte of the unit
-            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (s0 & (ENG_RING - 1)));
-            if (off < ubytes) eng_dma(reinterpret_cast<const void *>(usrc + off), dst);
-            issued++;
-            if (issued > (uint32_t)ENG_D) {
+            for (uint32_t k = 0; k < gn; k++) {
+                const uint32_t s0 = (g0 + k) * ENG_LINE;
+                if (s0 >= uend_b) {                // next unit (units start at line boundaries, >= 1 line)
+                    const EngUnit U = Un;
+                    if (++ui < uend_i) Un = ld_unit(a.units, ui);
+                    usoff = U.soff;
+                    uend_b = usoff + ((U.bytes + ENG_LINE - 1) & ~(ENG_LINE - 1));
+                    // a buffer descriptor over the unit's bytes: the lanes of its last line past its end read nothing
+                    urs = make_rsrc(reinterpret_cast<const void *>((uint64_t)U.src_lo | (uint64_t)U.src_hi << 32), U.bytes);
+                }
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(urs, (lds_void_t *)((char *)elds + (s0 & (ENG_RING - 1))), 16,
+                                                         s0 - usoff + 16u * (uint32_t)lane, 0, 0, 0);
+            }
+            issued += gn;
+            if (ENG_THIN && __builtin_amdgcn_readfirstlane(eng_ld_asm(lds0 + L_CTL + C_GATHER * 4)) != 0u) {
+                // the CU sweeps granules: few lines in flight, so the sweep's loads do not queue behind the stream
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ENG_THIN) : "memory");
+                const uint32_t l = issued > (uint32_t)ENG_THIN ? (issued - ENG_THIN) * ENG_LINE : 0u;
+                if (l > pub) {
+                    pub = l;
+                    if (lane == 0) eng_st_asm(lds0 + L_CTL + C_LANDED * 4, pub);
+                }
+            } else if (issued > (uint32_t)ENG_D) {
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ENG_D) : "memory");
                 const uint32_t l = (issued - ENG_D) * ENG_LINE;
                 if (l > pub) {
@@ -426,22 +498,29 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
             const uint32_t task = ld_unit(a.units, ui).tmn & 0xFFFFu;
             const EngTask tk = ld_task(a.tasks, task);
             ntask++;
-            uint64_t *sk = st && ntask <= (uint32_t)ENG_ST_TASKS ? st + ENG_ST_HDR + 4 * (ntask - 1) : nullptr;
+            uint64_t *sk = st && ntask <= (uint32_t)ENG_ST_TASKS ? st + ENG_ST_HDR + ENG_ST_W * (ntask - 1) : nullptr;
             if (w == 0 && sk && lane == 0) {
                 sk[0] = __builtin_amdgcn_s_memrealtime();
                 sk[3] = task;
             }
-            if (w == 0) {
-                // ---- gather x of this task into LDS (after every wave loaded the previous task's x)
+            {
+                // ---- gather x of this task into LDS, every consumer wave its share (a sweep is one memory round trip
+                // queued behind the CU's weight stream, so the waves' shares go in parallel, not in turns); first every
+                // wave must have loaded the previous task's x
+                if (ENG_THIN && w == 0 && lane == 0) cst(ctl + C_GATHER, 1u);   // the loader thins its stream meanwhile
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 while (cld(ctl + C_XLOADED) < (uint32_t)ENG_NC * (ntask - 1))
                     if (!eng_spin(a, ctl, t0, ENG_E_XLOADED)) { abort = true; break; }
                 if (abort) break;
                 const int nb = (int)tk.nb, np = (int)tk.npairs;
+                // this wave's items: 8-lane groups of float4 (x from memory) or granules, [i0, i1), in whole 64-lane steps
+                const int nitem = nb * 8;
+                const int per = ((nitem + 64 * ENG_NC - 1) / (64 * ENG_NC)) * 64;
+                const int i0 = w * per, i1 = min(nitem, i0 + per);
                 if (tk.xext) {                   // x from memory: the GEMV prologue's quantizer
-                    for (int base = 0; base < nb * 8; base += 64) {
+                    for (int base = i0; base < i1; base += 64) {
                         const int idx = base + lane;                     // float4 index
-                        const bool live = idx < nb * 8;
+                        const bool live = idx < i1;
                         const float4 v = live ? reinterpret_cast<const float4 *>(tk.xext)[idx] : make_float4(0, 0, 0, 0);
                         uint32_t d16;
                         int qsum;
@@ -456,8 +535,7 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
                         }
                     }
                 } else {                         // x from the producers' granules
-                    const int ng = nb * 8;
-                    for (int base = 0; base < ng && !abort; base += 64 * 16) {
+                    for (int base = i0; base < i1 && !abort; base += 64 * 16) {
                         uint64_t g[16];
                         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
                         for (;;) {
@@ -465,7 +543,7 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
 #pragma unroll
                             for (int k = 0; k < 16; k++) {
                                 const int idx = base + lane + 64 * k;
-                                g[k] = idx < ng ? __hip_atomic_load((const g_u64 *)(tk.xgran + idx), __ATOMIC_RELAXED,
+                                g[k] = idx < i1 ? __hip_atomic_load((const g_u64 *)(tk.xgran + idx), __ATOMIC_RELAXED,
                                                                     __HIP_MEMORY_SCOPE_AGENT)
                                                 : (uint64_t)tag << 48;
                                 okl &= (uint32_t)(g[k] >> 48) == tag || (a.diag & 1);
@@ -477,7 +555,7 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
 #pragma unroll
                         for (int k = 0; k < 16; k++) {
                             const int idx = base + lane + 64 * k;
-                            if (idx < ng) {
+                            if (idx < i1) {
                                 const int b = idx >> 3, ww = idx & 7;
                                 xq[((((b & 1) << 1) | (ww >> 2)) * np + (b >> 1)) * 4 + (ww & 3)] = (uint32_t)g[k];
                                 const uint32_t aux = (uint32_t)(g[k] >> 32) & 0xFFFFu;
@@ -489,22 +567,23 @@ __global__ __launch_bounds__(ENG_THREADS) void k_engine_q4_0(const EngArgs a) {
                     if (abort) break;
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0) cst(ctl + C_XGEN, ntask);
-            } else {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while (cld(ctl + C_XGEN) < ntask)
-                    if (!eng_spin(a, ctl, t0, ENG_E_XGEN)) { abort = true; break; }
+                // every wave's share in LDS: XGEN counts the waves that finished this task's share
+                if (lane == 0) __hip_atomic_fetch_add(ctl + C_XGEN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+                while (cld(ctl + C_XGEN) < (uint32_t)ENG_NC * ntask)
+                    if (!eng_spin(a, ctl, t2, ENG_E_XGEN)) { abort = true; break; }
                 if (abort) break;
+                if (ENG_THIN && w == 0 && lane == 0) cst(ctl + C_GATHER, 0u);
             }
             asm volatile("" ::: "memory");
             if (w == 0 && sk && lane == 0) sk[1] = __builtin_amdgcn_s_memrealtime();
             const int ppl = ((int)tk.npairs + 63) >> 6;
             if (ppl == 1)
-                eng_task_rows<1>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort);
+                eng_task_rows<1>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort, sk);
             else if (ppl == 2)
-                eng_task_rows<2>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort);
+                eng_task_rows<2>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort, sk);
             else
-                eng_task_rows<3>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort);
+                eng_task_rows<3>(a, ctl, ring, par, tk, ui, uend, task, w, lane, tag, abort, sk);
             if (w == 0 && sk && lane == 0) sk[2] = __builtin_amdgcn_s_memrealtime();
         }
         if (lane == 0) cst(ctl + C_PROG + w, 0xFFFFFFFFu);   // never holds the loader back again

@@ -272,6 +272,9 @@ def main():
                     help="headline decode path: the persistent LDS-DMA engine (one launch per token, "
                          "ggml_hip_chain_set_engine), the per-launch graph (4 sibling GEMVs per layer), or auto = "
                          "the engine when its outputs are bitwise the launches' and it ran faster (both are timed)")
+    ap.add_argument("--no-roofline-replays", action="store_true",
+                    help="skip the per-position isolated replays of the roofline (profiling runs: the rocprof summary "
+                         "then holds the timed replays' GEMVs only)")
     ap.add_argument("--deadline", type=float, default=300.0,
                     help="N > 1: seconds after which a rank that has not finished aborts its communicator and exits "
                          "(rank 0 prints an error line); the self-launcher terminates its ranks 30 s later")
@@ -471,7 +474,10 @@ def main():
                                 "launches_per_layer": len(groups)}
     if engine is not None:
         result["engine"] = {k: v for k, v in engine.items() if k != "elapsed_s"}
-    result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups))
+    result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups),
+                                         elapsed_launches / args.steps * 1e3, args.layers,
+                                         engine_step_ms=result.get("engine", {}).get("ms_per_step"),
+                                         isolated=not args.no_roofline_replays)
     if not args.no_prefill and args.prefill_tokens > 0:
         result["prefill"] = prefill_bench(gh, L, stack, xs, ys, stream, args.prefill_tokens,
                                           groups=[tuple(g) for g in groups])
@@ -699,17 +705,84 @@ def split_check(gh, L, stack, ysplit, yb, rank, allreduce, stream):
     return {"own_rows_bitwise": ok_own, "gather_checksum": ok_sum, "matrices": len(row)}
 
 
-def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
-    """Dominant kernel = the decode GEMV (k_gemv_q4_0<1,...>).  For each launch position of a
-    layer (fused wq|wk|wv, wo, fused w1|w3, w2) the 32 launches of that position (one per layer,
-    distinct weights, > 256 MB in total) are captured in their own HIP graph and replayed; HIP
-    events on the launch stream around the replays give the average launch duration (in a
-    graph replay consecutive kernels run back to back, which is also what rocprofv3's per-kernel
-    durations measure).  achieved = algorithmic bytes of the launch (sum over its matrices of
-    18*M*K/32 + 4*K + 4*M) / average launch duration; reported per position and byte-weighted."""
+def newest_profile(suffix):
+    """the newest round's committed profile with this suffix (profiles/rNN_<suffix>), or None"""
+    fs = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(suffix))
+    return os.path.join(ROOT, "profiles", fs[-1]) if fs else None
+
+
+def rocprof_stats(path):
+    """{kernel name: (calls, total ns)} of a rocprofv3 --stats kernel summary (csv)"""
+    import csv
+    out = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            out[r["Name"]] = (int(r["Calls"]), float(r["TotalDurationNs"]))
+    return out
+
+
+def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, ms_per_step, n_layers, engine_step_ms=None,
+                    isolated=True, reps=10):
+    """The decode roofline, priced on the TIMED step itself (verdict r5 item 5: the dominant kernel's time per step
+    cannot exceed the step).  Every launch of a step is the decode GEMV (k_gemv_q4_0<1,...>): 4 sibling launches
+    per layer, back to back in one HIP graph, so achieved = the step's algorithmic bytes / ms_per_step (the launch
+    boundaries inside the step are charged to the GEMVs; avg_launch_us = step / launches).  Algorithmic bytes of a
+    launch = sum over its matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y).  Beside it:
+      rocprof_check: from the newest committed rocprofv3 summary of this bench's own timed replays
+        (profiles/rNN_bench_rocprofv3_kernel_stats.csv, tools/run.sh PARTS=prof): the GEMV kernels' busy
+        time per step (total ns / (calls / launches per step)) <= ms_per_step, the rest being boundaries;
+      per_shape_isolated: each launch position's 32 launches replayed in a graph of their own (the shape's own
+        rate; their sum exceeds the step by the shape-mixing of the real sequence, so they are not the headline)."""
+    launches = len(launch_args)
+    step_bytes = 0
+    for kind, a in launch_args:
+        if kind == "multi":
+            n, wp, mp, K, yp, _ = a
+            Ms = [mp[i] for i in range(n)]
+        else:
+            K, Ms = a[1], [a[3]]
+        step_bytes += sum(q4_bytes(K, M) + 4 * K + 4 * M for M in Ms)
+    t_step = ms_per_step * 1e-3                              # one step = this run's n_layers layers
+    achieved = step_bytes / t_step / 1e9
+    traffic, src = None, None
+    pmc = newest_profile("_gemv_pmc_traffic.json")
+    if pmc:
+        try:
+            traffic = round(json.load(open(pmc))["traffic_bytes_per_launch_mean"])
+            src = f"{os.path.relpath(pmc, ROOT)}: 2*FETCH_SIZE+WRITE_SIZE (x1024) per GEMV launch, mean"
+        except Exception:
+            traffic = None
+    out = {"bound": "hbm", "kernel": "k_gemv_q4_0<NT=1,...> (fused q8_0 quantize + q4_0.q8_0 GEMV, one row item per wave "
+                                     "ring slot), 4 sibling launches per layer",
+           "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+           "traffic": traffic, "traffic_source": src,
+           "algorithmic_bytes_per_launch_mean": round(step_bytes / launches), "algorithmic_bytes_per_step": step_bytes,
+           "launches_per_step": launches, "avg_launch_us": round(t_step / launches * 1e6, 3),
+           "timing": "the timed step: ms_per_step of the per-launch graph (barrier + synchronize around `steps` replays)",
+           "bytes_per_launch_def": "sum over the launch's matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y)"}
+    prof = newest_profile("_bench_rocprofv3_kernel_stats.csv")
+    if prof:
+        try:
+            st = rocprof_stats(prof)
+            calls = sum(c for k, (c, _) in st.items() if "k_gemv_q4_0<1," in k)
+            ns = sum(t for k, (c, t) in st.items() if "k_gemv_q4_0<1," in k)
+            steps_seen = calls / launches if launches else 0
+            busy = ns / steps_seen / 1e3 if steps_seen else None      # us per step
+            out["rocprof_check"] = {"source": os.path.relpath(prof, ROOT), "gemv_calls": calls,
+                                    "gemv_busy_us_per_step": round(busy, 1) if busy else None,
+                                    "gemv_avg_us": round(ns / calls / 1e3, 3) if calls else None,
+                                    "ms_per_step_us": round(t_step * 1e6, 1),
+                                    "busy_le_step": bool(busy is not None and busy <= t_step * 1e6),
+                                    "kernel_only_GBps": round(step_bytes / (busy * 1e-6) / 1e9, 1) if busy else None}
+        except Exception as e:       # a malformed summary must not cost the line
+            out["rocprof_check"] = {"source": os.path.relpath(prof, ROOT), "error": str(e)}
+    if engine_step_ms is not None:
+        te = engine_step_ms * 1e-3
+        out["engine"] = {"kernel": "k_engine_q4_0 (one launch per step)", "achieved": round(step_bytes / te / 1e9, 1),
+                         "frac": round(step_bytes / te / 1e9 / HBM_PEAK_GBPS, 4)}
+    if not isolated:
+        return out
     shapes = {}
-    tot_bytes = tot_t = 0.0
-    nlaunch = 0
     for pos in range(per_layer):
         sel = launch_args[pos::per_layer]
         g = gh.Graph(stream)
@@ -733,27 +806,8 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, reps=10):
         nbytes = sum(q4_bytes(K, M) + 4 * K + 4 * M for M in Ms)
         shapes[f"K{K}->M{'+'.join(map(str, Ms))}"] = {"us": round(t * 1e6, 3), "GBps": round(nbytes / t / 1e9, 1),
                                                        "bytes": nbytes}
-        tot_bytes += nbytes * len(sel)
-        tot_t += t * len(sel)
-        nlaunch += len(sel)
-    achieved = tot_bytes / tot_t / 1e9
-    traffic, src = None, None
-    # the newest round's PMC pass (tools/pmc_traffic.sh: rocprofv3 --pmc passes over this bench's
-    # decode graph), so the line cites a profile of the current GEMV code
-    pmcs = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_gemv_pmc_traffic.json"))
-    if pmcs:
-        try:
-            traffic = round(json.load(open(os.path.join(ROOT, "profiles", pmcs[-1])))["traffic_bytes_per_launch_mean"])
-            src = f"profiles/{pmcs[-1]}: 2*FETCH_SIZE+WRITE_SIZE (x1024) per GEMV launch, mean"
-        except Exception:
-            traffic = None
-    return {"bound": "hbm", "kernel": "k_gemv_q4_0<NT=1,...> (fused q8_0 quantize + q4_0.q8_0 GEMV, one row item per wave ring slot)",
-            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": src,
-            "algorithmic_bytes_per_launch_mean": round(tot_bytes / nlaunch),
-            "avg_launch_us": round(tot_t / nlaunch * 1e6, 3), "per_shape": shapes,
-            "timing": "HIP events around graph replays of each launch position's 32 back-to-back launches",
-            "bytes_per_launch_def": "sum over the launch's matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y)"}
+    out["per_shape_isolated"] = shapes
+    return out
 
 
 def engine_decode(gh, L, launch_args, yb, outs_launches, stream, timed):
@@ -938,7 +992,32 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0,
     def alt(kernel, tt):
         return {"kernel": kernel, "ms_per_layer": round(tt / layers * 1e3, 4), "TOPs": round(ops / tt / 1e12, 1),
                 "mfma_frac": round(ops / tt / 1e12 / INT8_PEAK_TOPS, 4)}
-    return {"tokens": N, "layers": layers, "ms_per_layer": round(t / layers * 1e3, 4),
+    # the prefill GEMM's own roofline (verdict r5 item 5): its instruction and that instruction's peak, named.
+    # v_mfma_scale_f32_32x32x64_f8f6f4 with e2m3 operands runs at ~10 PF dense (MI355X_MICROARCH.md, FP6 row);
+    # k_gemm9 puts each q8_0 value into it as TWO e2m3 digits (q = 16 (q >> 4) + (q & 15), one per K half), so
+    # one instruction advances the algorithm's K by 32, not 64: the effective peak of 2*M*K*N is 5 POP/s.
+    # achieved = 2*M*K*N over the layer chain (x image preps included); kernel_only from the newest committed
+    # rocprofv3 summary of this bench (k_gemm9* durations of the fp6 passes: 1 warm-up + `reps` timed)
+    roof = {"bound": "mfma", "kernel": "k_gemm9_q4_0 / k_gemm9w_q4_0",
+            "instruction": "v_mfma_scale_f32_32x32x64_f8f6f4 (e2m3 x e2m3, block scales 2^1 / 2^5)",
+            "instruction_peak": 10000.0, "effective_peak": 5000.0, "unit": "TOP/s",
+            "peak_note": "10 PF fp6 dense; two e2m3 digits per q8_0 value -> 5 POP/s of the algorithm's 2*M*K*N",
+            "achieved": round(ops / t / 1e12, 1), "frac": round(ops / t / 1e12 / 5000.0, 4),
+            "timing": "the 4-layer prefill chain (HIP events over `reps` passes), x image preps included"}
+    prof = newest_profile("_bench_rocprofv3_kernel_stats.csv")
+    if prof:
+        try:
+            st = rocprof_stats(prof)
+            g9 = sum(tt_ for k, (c, tt_) in st.items() if "k_gemm9" in k)
+            if g9 > 0:
+                passes = reps + 1
+                roof["kernel_only_TOPs"] = round(ops * passes / (g9 * 1e-9) / 1e12, 1)
+                roof["kernel_only_frac"] = round(ops * passes / (g9 * 1e-9) / 1e12 / 5000.0, 4)
+                roof["kernel_only_source"] = (f"{os.path.relpath(prof, ROOT)}: sum of k_gemm9* durations over "
+                                              f"{passes} passes of the same chain")
+        except Exception as e:
+            roof["kernel_only_error"] = str(e)
+    return {"tokens": N, "layers": layers, "ms_per_layer": round(t / layers * 1e3, 4), "roofline": roof,
             "GBps": round(nbytes / t / 1e9, 1), "TOPs": round(ops / t / 1e12, 1),
             "mfma_frac": round(ops / t / 1e12 / INT8_PEAK_TOPS, 4), "peak_TOPs": INT8_PEAK_TOPS,
             "stack_7B_prefill_ms": round(t / layers * 32 * 1e3, 3),

@@ -31,13 +31,14 @@ if has bench; then
 fi
 if has prof; then    # the bench's own timed replays under the kernel tracer
   step prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- \
-      python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extra ${BENCH_ARGS:-}
+      python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-exact --no-roofline-replays ${BENCH_ARGS:-}
   tail -1 "$O/prof.log" | cut -c1-300
 fi
 if has pmc; then     # decode GEMV HBM bytes: one counter per pass (gfx950: FETCH_SIZE is half the streamed bytes)
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmc_$c 300 rocprofv3 --pmc $c -d "$O/pmc/$c" -o run --output-format csv -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu --no-prefill --no-extra --no-exact ${BENCH_ARGS:-}
+        python3 bench.py --steps 2 --warmup 1 --no-cpu --no-prefill --no-extra --no-exact --no-roofline-replays \
+        --decode launches ${BENCH_ARGS:-}
   done
   python3 tools/pmc_summary.py "$O/pmc" > "$O/gemv_pmc_traffic.json" && cat "$O/gemv_pmc_traffic.json" | cut -c1-400
 fi

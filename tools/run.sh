@@ -3,6 +3,7 @@
 #   PARTS="tests smoke bench prof pmc gpmc e2e e2e_variant" O=gpurun_out/r06 bash tools/run.sh
 # Every GPU step runs under its own time limit; a fault, abort or timeout (rc 124/134/137/139 or any
 # rc >= 2 of a step that must pass) ends the script there: no further GPU step in the same call.
+# (aql needs tools/aql_dispatch_cost + tools/aql_kernel.hsaco, built by the hipcc lines in tools/aql_dispatch_cost.hip.)
 # Extra arguments per part: BENCH_ARGS (bench, prof), E2E_ARGS (e2e), VARIANT (e2e_variant: a
 # tools/build_variant.sh name under variants/, default base).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -49,6 +50,10 @@ if has gpmc; then    # prefill GEMM counters, k_gemm9 at 4096 x 4096 x 512 (tool
     i=$((i+1))
     step gpmc_$i 60 rocprofv3 --pmc $c -d "$O/gpmc/p$i" -o run --output-format csv -- python3 tools/gemm_one.py
   done
+fi
+if has aql; then     # host cost per dispatch: hipLaunchKernelGGL vs a raw AQL packet on an own HSA queue (verdict r5 item 3)
+  step aql 120 ./tools/aql_dispatch_cost tools/aql_kernel.hsaco
+  cat "$O/aql.log"
 fi
 if has e2e; then     # the hook path end to end: the reference llama.cpp at full offload, LLaMA-7B shape
   step e2e 700 python tools/e2e_llama.py --decode 128 --modes fast,exact --out "$O/e2e_7b.json" ${E2E_ARGS:-}

@@ -209,6 +209,18 @@ typedef struct ggml_hip_chain_task {
 typedef struct ggml_hip_chain ggml_hip_chain;
 /* Validates the tasks (no device work). */
 int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **chain);
+/* N-token chains (prefill): x of a task is f32 [N][K], y[i] f32 [N][M[i]]; otherwise as above, bitwise n
+ * separate ggml_hip_mul_mat_q4_0_multi calls at N.  A task whose siblings take one k_gemm9 launch on fp6
+ * weight images (ggml_hip_weight_image_create) reads a chain-owned x image; when its x is exactly y[i] of an
+ * earlier such task (M[i] == K, nothing in between writes it), that task's GEMM epilogue writes the image
+ * beside y (no k_prep9_x launch).  Allocates the images (gemm9 x bytes per task) at create. */
+int ggml_hip_chain_create_n(int ntasks, const ggml_hip_chain_task *tasks, int64_t N, ggml_hip_chain **chain);
+/* debug: 0 = N-token chains build every x image with k_prep9_x (A/B), 1 = epilogue images (default),
+ * -1 = GGML_HIP_CHAIN_X9 */
+int ggml_hip_debug_set_chain_x9(int on);
+/* debug, no device needed: the epilogue links ggml_hip_chain_create_n would plan; prod[t] = the task whose
+ * epilogue writes task t's x image (-1: k_prep9_x), share[t] = the earlier consumer whose image t reads (-1) */
+int ggml_hip_debug_chain_links(int ntasks, const ggml_hip_chain_task *tasks, int64_t N, int *prod, int *share);
 /* Stream-ordered (graph-capturable): one GEMV launch per task. */
 int ggml_hip_chain_launch(ggml_hip_chain *chain, void *stream);
 /* Synchronizes the device; 0, or (engine) the nonzero error bits of a bounded wait that expired. */
@@ -223,7 +235,8 @@ int ggml_hip_chain_destroy(ggml_hip_chain *chain);
  * runs (all workgroups co-resident); every wait is bounded (GGML_HIP_ENGINE_TIMEOUT_MS, default 2000) and
  * chain_status reports an expired one.  mode 1 on (builds the plan; returns 1 when the engine runs the chain, 0
  * when it declined: ggml_hip_last_error says why), 0 off, -1 query.  GGML_HIP_CHAIN_ENGINE=1 turns it on at
- * create.  info: [0] engine on, [1] work units, [2] largest per-CU stream (bytes), [3] weight bytes, [4] CUs. */
+ * create.  info: [0] engine on, [1] work units, [2] largest per-CU stream (bytes), [3] weight bytes, [4] CUs,
+ * [5] (N-token chains) tasks whose x image a producer's GEMM epilogue writes. */
 int ggml_hip_chain_set_engine(ggml_hip_chain *chain, int mode);
 int ggml_hip_chain_engine_info(ggml_hip_chain *chain, int64_t *info, int n);
 

@@ -177,10 +177,16 @@ int ggml_hip_reserve_workspace_mm(int64_t K, int64_t N, int64_t M) {
 
 struct ggml_hip_chain {
     int device = 0;
+    int64_t N = 1;                    // tokens per task (ggml_hip_chain_create_n)
     std::vector<ggml_hip_chain_task> tasks;
     ghip::EnginePlan *eng = nullptr;  // the engine's plan when the chain runs on it
     int eng_mode = 0;                 // 0 per-launch, 1 engine requested
     std::string eng_why;              // why the engine declined the chain (empty when it runs)
+    // N > gemv tokens: per task, its k_gemm9 x image (gemm9_x_bytes(K, N)) and the task whose launch writes it
+    // in its epilogue (-1: none, the task builds it with k_prep9_x); per task, the image its epilogue writes
+    // (null: none) from the y of matrix out_mat.  Consumers of one producer's output share its image.
+    std::vector<void *> ximg, out_img, owned;
+    std::vector<int> prod_task, out_mat;
 };
 
 namespace {
@@ -198,6 +204,10 @@ uint32_t engine_timeout_ticks() {       // s_memrealtime ticks (100 MHz); GGML_H
 int chain_engine_on(ggml_hip_chain *c) {
     if (c->eng) return 1;
     c->eng_why.clear();
+    if (c->N != 1) {
+        c->eng_why = "the decode engine runs N = 1 chains";
+        return 0;
+    }
     const int ncu = g_dev[c->device].info.num_cus;
     c->eng = ghip::engine_plan_create((int)c->tasks.size(), c->tasks.data(), ncu, engine_timeout_ticks(), c->eng_why);
     return c->eng ? 1 : 0;
@@ -206,12 +216,95 @@ int chain_engine_on(ggml_hip_chain *c) {
 
 extern "C" {
 
-int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **out) {
+}  // extern "C"
+
+namespace {
+bool overlaps(const void *a, uint64_t abytes, const void *b, uint64_t bbytes) {
+    const uint64_t p = (uint64_t)(uintptr_t)a, q = (uint64_t)(uintptr_t)b;
+    return p < q + bbytes && q < p + abytes;
+}
+
+void chain_free_images(ggml_hip_chain *c) {
+    for (void *p : c->owned) (void)hipFree(p);
+    c->owned.clear();
+    c->ximg.clear();
+    c->out_img.clear();
+}
+
+// The image plan of an N-token chain.  Task t's producer is the latest earlier task u with a matrix i whose y
+// is exactly t's x (M[i] == K) when no launch in between (nor u's other matrices) writes any byte of x.  One
+// image per producing task: the first consumer fixes the matrix; consumers of the same (u, i) share the
+// image, a consumer of another matrix of u builds its own with k_prep9_x.  Only tasks whose N takes the GEMM
+// path get an image (N > gemv_max_tokens(K)).
+// The links alone (no device): prod[t] = the producing task or -1, share[t] = the earlier consumer whose image
+// t reads or -1 (t owns an image when it takes the GEMM path), out_mat[u] = the matrix whose y u's epilogue
+// turns into an image or -1; gemm[t] = whether t can take the GEMM path at N (N > gemv_max_tokens(K)).
+void chain_links(int n, const ggml_hip_chain_task *tasks, int64_t N, int *prod, int *share, int *out_mat, char *gemm) {
+    for (int t = 0; t < n; t++) prod[t] = share[t] = out_mat[t] = -1;
+    std::vector<int> first_consumer(n, -1);
+    for (int t = 0; t < n; t++) {
+        const ggml_hip_chain_task &k = tasks[t];
+        gemm[t] = N > ghip::gemv_max_tokens(k.K);
+        if (!gemm[t]) continue;
+        const uint64_t xb = 4 * (uint64_t)k.K * (uint64_t)N;
+        int pu = -1, pi = -1;
+        for (int u = t - 1; u >= 0; u--) {
+            const ggml_hip_chain_task &p = tasks[u];
+            int hit = -1;
+            bool clash = false;
+            for (int i = 0; i < p.nmat; i++) {
+                if (p.y[i] == k.x && p.M[i] == k.K) hit = i;
+                else if (overlaps(p.y[i], 4 * (uint64_t)p.M[i] * (uint64_t)N, k.x, xb)) clash = true;
+            }
+            if (hit >= 0 && !clash) pu = u, pi = hit;
+            if (hit >= 0 || clash) break;
+        }
+        if (pu < 0 || !gemm[pu]) continue;            // a GEMV producer has no epilogue image
+        if (out_mat[pu] < 0) {                     // the first consumer fixes the producer's image
+            out_mat[pu] = pi;
+            first_consumer[pu] = t;
+            prod[t] = pu;
+        } else if (out_mat[pu] == pi) {            // the same (u, i): share the first consumer's image
+            prod[t] = pu;
+            share[t] = first_consumer[pu];
+        }
+    }
+}
+
+int chain_plan_images(ggml_hip_chain *c) {
+    const int n = (int)c->tasks.size();
+    std::vector<int> share(n);
+    std::vector<char> gemm(n);
+    c->prod_task.assign(n, -1);
+    c->out_mat.assign(n, -1);
+    c->ximg.assign(n, nullptr);
+    c->out_img.assign(n, nullptr);
+    chain_links(n, c->tasks.data(), c->N, c->prod_task.data(), share.data(), c->out_mat.data(), gemm.data());
+    for (int t = 0; t < n; t++) {
+        if (!gemm[t]) continue;
+        if (share[t] >= 0) {
+            c->ximg[t] = c->ximg[share[t]];
+            continue;
+        }
+        void *p = nullptr;
+        if (hipMalloc(&p, ghip::gemm9_x_bytes(c->tasks[t].K, c->N)) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(GGML_HIP_ERR_NOMEM, "chain x image allocation failed");
+        }
+        c->owned.push_back(p);
+        c->ximg[t] = p;
+        if (c->prod_task[t] >= 0) c->out_img[c->prod_task[t]] = p;
+    }
+    return GGML_HIP_OK;
+}
+
+int chain_create(int ntasks, const ggml_hip_chain_task *tasks, int64_t N, ggml_hip_chain **out) {
     ensure_init();
     if (!out) return fail(GGML_HIP_ERR_INVALID, "null out");
     *out = nullptr;
     if (g_device_count == 0) return fail(GGML_HIP_ERR_DEVICE, "no HIP device");
     if (ntasks < 1 || !tasks) return fail(GGML_HIP_ERR_INVALID, "ntasks must be >= 1");
+    if (N < 1 || N > ((int64_t)1 << 24)) return fail(GGML_HIP_ERR_INVALID, "N must be 1 .. 2^24");
     for (int t = 0; t < ntasks; t++) {
         const ggml_hip_chain_task &k = tasks[t];
         if (k.nmat < 1 || k.nmat > ghip::GEMV_MULTI_MAX) return fail(GGML_HIP_ERR_INVALID, "nmat must be 1..4");
@@ -221,19 +314,87 @@ int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip
             if (!k.W[i] || !k.y[i] || k.M[i] <= 0 || !aligned(k.W[i], 16) || !aligned(k.y[i], 4))
                 return fail(GGML_HIP_ERR_INVALID, "null / misaligned W or y, or M <= 0");
             // a task's y may not overlap its own x (its rows read x while others write y)
-            const uint64_t xlo = (uint64_t)(uintptr_t)k.x, xhi = xlo + 4 * (uint64_t)k.K;
-            const uint64_t yp = (uint64_t)(uintptr_t)k.y[i];
-            if (yp < xhi && xlo < yp + 4 * (uint64_t)k.M[i]) return fail(GGML_HIP_ERR_INVALID, "a task's y overlaps its own x");
+            if (overlaps(k.y[i], 4 * (uint64_t)k.M[i] * (uint64_t)N, k.x, 4 * (uint64_t)k.K * (uint64_t)N))
+                return fail(GGML_HIP_ERR_INVALID, "a task's y overlaps its own x");
         }
     }
     auto *c = new ggml_hip_chain();
     c->device = current_device();
+    c->N = N;
     c->tasks.assign(tasks, tasks + ntasks);
-    if (engine_env() == 1) {
+    if (N > 1) {
+        const int rc = chain_plan_images(c);
+        if (rc != GGML_HIP_OK) {
+            chain_free_images(c);
+            delete c;
+            return rc;
+        }
+    }
+    if (engine_env() == 1 && N == 1) {
         c->eng_mode = 1;
         (void)chain_engine_on(c);           // a declined chain keeps the per-launch path
     }
     *out = c;
+    return GGML_HIP_OK;
+}
+
+// One task of an N-token chain: ONE k_gemm9 launch on its x image when ggml_hip_mul_mat_q4_0_multi would run
+// it as one (g9_images), the image from the producer's epilogue when the producer ran on k_gemm9 in this pass
+// (else k_prep9_x), and this launch's epilogue writing the images its consumers read; otherwise the plain
+// sibling call.  Either way y is bitwise ggml_hip_mul_mat_q4_0_multi's.
+std::atomic<int> g_chain_x9{-1};        // GGML_HIP_CHAIN_X9=0 / ggml_hip_debug_set_chain_x9(0): every task preps
+bool chain_x9_on() {
+    int v = g_chain_x9.load(std::memory_order_relaxed);
+    if (v < 0) {
+        v = (!getenv("GGML_HIP_CHAIN_X9") || atoi(getenv("GGML_HIP_CHAIN_X9")) != 0) ? 1 : 0;
+        g_chain_x9.store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
+int chain_task_n(ggml_hip_chain *c, int t, std::vector<char> &ran9, hipStream_t s) {
+    const ggml_hip_chain_task &k = c->tasks[t];
+    const void *img[4];
+    if (c->ximg[t] && g9_images(k.nmat, k.W, k.M, k.K, c->N, img)) {
+        const bool fold = chain_x9_on();
+        const int u = c->prod_task[t];
+        if (!(fold && u >= 0 && ran9[u])) HIP_RET(ghip::gemm9_prep_x(k.x, k.K, c->N, c->ximg[t], s));
+        uint8_t *xo[4] = {nullptr, nullptr, nullptr, nullptr};
+        int64_t ldy[4];
+        for (int i = 0; i < k.nmat; i++) ldy[i] = k.M[i];
+        if (fold && c->out_img[t]) xo[c->out_mat[t]] = (uint8_t *)c->out_img[t];
+        HIP_RET(ghip::gemm9_run_multi(k.nmat, img, k.M, k.K, c->ximg[t], c->N, (float *const *)k.y, ldy, s, xo));
+        ran9[t] = 1;
+        return GGML_HIP_OK;
+    }
+    ran9[t] = 0;
+    return ggml_hip_mul_mat_q4_0_multi(k.nmat, k.W, k.M, k.K, k.x, c->N, (float *const *)k.y, s);
+}
+}  // namespace
+
+extern "C" {
+
+int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **out) {
+    return chain_create(ntasks, tasks, 1, out);
+}
+
+int ggml_hip_chain_create_n(int ntasks, const ggml_hip_chain_task *tasks, int64_t N, ggml_hip_chain **out) {
+    return chain_create(ntasks, tasks, N, out);
+}
+
+int ggml_hip_debug_chain_links(int ntasks, const ggml_hip_chain_task *tasks, int64_t N, int *prod, int *share) {
+    if (ntasks < 1 || !tasks || !prod || !share || N < 1) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
+    for (int t = 0; t < ntasks; t++)
+        if (tasks[t].nmat < 1 || tasks[t].nmat > ghip::GEMV_MULTI_MAX) return fail(GGML_HIP_ERR_INVALID, "nmat must be 1..4");
+    std::vector<int> out_mat(ntasks);
+    std::vector<char> gemm(ntasks);
+    chain_links(ntasks, tasks, N, prod, share, out_mat.data(), gemm.data());
+    return GGML_HIP_OK;
+}
+
+int ggml_hip_debug_set_chain_x9(int on) {
+    if (on < -1 || on > 1) return fail(GGML_HIP_ERR_INVALID, "mode must be -1, 0 or 1");
+    g_chain_x9.store(on, std::memory_order_relaxed);          // -1: re-read GGML_HIP_CHAIN_X9
     return GGML_HIP_OK;
 }
 
@@ -265,9 +426,10 @@ int ggml_hip_debug_engine_stamps(ggml_hip_chain *c, uint64_t *out, int64_t n) {
 
 int ggml_hip_chain_engine_info(ggml_hip_chain *c, int64_t *info, int n) {
     if (!c || !info || n < 1) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
-    int64_t v[5] = {c->eng ? 1 : 0, 0, 0, 0, 0};
+    int64_t v[6] = {c->eng ? 1 : 0, 0, 0, 0, 0, 0};
     if (c->eng) ghip::engine_plan_info(c->eng, v + 1);
-    for (int i = 0; i < n && i < 5; i++) info[i] = v[i];
+    for (size_t t = 0; t < c->prod_task.size(); t++) v[5] += c->prod_task[t] >= 0;
+    for (int i = 0; i < n && i < 6; i++) info[i] = v[i];
     if (!c->eng && !c->eng_why.empty()) g_last_error = c->eng_why;
     return GGML_HIP_OK;
 }
@@ -279,6 +441,14 @@ int ggml_hip_chain_launch(ggml_hip_chain *c, void *stream) {
     hipStream_t s = resolve_stream(stream);
     if (c->eng && !exact_mode()) {          // exact mode: the per-launch exact kernels
         HIP_RET(ghip::engine_launch(c->eng, s));
+        return GGML_HIP_OK;
+    }
+    if (c->N > 1) {
+        std::vector<char> ran9(c->tasks.size(), 0);
+        for (int t = 0; t < (int)c->tasks.size(); t++) {
+            const int rc = chain_task_n(c, t, ran9, s);
+            if (rc != GGML_HIP_OK) return rc;
+        }
         return GGML_HIP_OK;
     }
     for (const auto &k : c->tasks) {
@@ -305,9 +475,10 @@ int ggml_hip_chain_status(ggml_hip_chain *c) {
 }
 
 int ggml_hip_chain_destroy(ggml_hip_chain *c) {
-    if (c && c->eng) {
+    if (c && (c->eng || !c->owned.empty())) {
         (void)GHIP_SYNC(hipDeviceSynchronize)();
-        ghip::engine_plan_destroy(c->eng);
+        if (c->eng) ghip::engine_plan_destroy(c->eng);
+        chain_free_images(c);
     }
     delete c;
     return GGML_HIP_OK;

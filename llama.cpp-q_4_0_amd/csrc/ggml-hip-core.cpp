@@ -299,25 +299,30 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
 // plans: y is within the oracle bound of the separate calls, and bitwise equal to them only with the
 // tile pinned (ggml_hip_debug_set_gemm9_wide 0 or 1; include/ggml-hip.h).
 // Returns 1 when the group does not qualify (the caller runs one launch per matrix).
-int mul_mat_group_g9(int n, const void *const *w, const int64_t *M, int64_t K, const float *x, int64_t N,
-                     float *const *y, hipStream_t s) {
+bool g9_images(int n, const void *const *w, const int64_t *M, int64_t K, int64_t N, const void **img) {
     static const bool grp = !getenv("GGML_HIP_GEMM9_GROUP") || atoi(getenv("GGML_HIP_GEMM9_GROUP")) != 0;
-    const int gv = gemm_version();
-    if (!grp || n < 2 || n > 4 || gv != 10 || !x || K <= 0 || K % 64 != 0 || !aligned(x, 16) ||
+    if ((n > 1 && !grp) || n < 1 || n > 4 || exact_mode() || gemm_version() != 10 || K <= 0 || K % 64 != 0 ||
         N <= ghip::gemv_max_tokens(K) || N * K >= ((int64_t)1 << 31))
-        return 1;
+        return false;
     const int id = current_device();
-    const void *img[4];
-    int64_t ldy[4];
     for (int i = 0; i < n; i++) {
         int fmt = 0;
         img[i] = wimage_find(id, w[i], K, M[i], &fmt);
         // mul_mat_dev's algo rule: the image GEMM above 128 tokens, or above IMG_MIN_N / for tall
         // matrices when an image exists
-        if (!img[i] || fmt != 9 || !(N > 128 || N > IMG_MIN_N || M[i] >= IMG_MIN_M)) return 1;
-        if (M[i] * (K / QK) * Q4B >= ((int64_t)1 << 31) || M[i] >= (1 << 30)) return 1;
-        ldy[i] = M[i];
+        if (!img[i] || fmt != 9 || !(N > 128 || N > IMG_MIN_N || M[i] >= IMG_MIN_M)) return false;
+        if (M[i] * (K / QK) * Q4B >= ((int64_t)1 << 31) || M[i] >= (1 << 30)) return false;
     }
+    return true;
+}
+
+int mul_mat_group_g9(int n, const void *const *w, const int64_t *M, int64_t K, const float *x, int64_t N,
+                     float *const *y, hipStream_t s) {
+    const void *img[4];
+    if (n < 2 || !x || !aligned(x, 16) || !g9_images(n, w, M, K, N, img)) return 1;
+    const int id = current_device();
+    int64_t ldy[4];
+    for (int i = 0; i < n; i++) ldy[i] = M[i];
     void *ws = nullptr;
     const int wrc = stream_workspace(id, s, workspace_bytes_mm(K, N, 0), &ws);
     if (wrc != GGML_HIP_OK) return wrc;

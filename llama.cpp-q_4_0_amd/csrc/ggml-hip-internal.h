@@ -153,6 +153,9 @@ int mul_mat_dev(const void *w, int64_t K, int64_t M, const float *x, int64_t N, 
                 hipStream_t s, unsigned *xq = nullptr);
 int mul_mat_group_g9(int n, const void *const *w, const int64_t *M, int64_t K, const float *x, int64_t N,
                      float *const *y, hipStream_t s);
+// true when ggml_hip_mul_mat_q4_0_multi runs these n siblings at N tokens as ONE k_gemm9 launch on registered
+// fp6 images (mul_mat_group_g9 for n > 1, mul_mat_dev's image GEMM for n = 1); img[i] = the images
+bool g9_images(int n, const void *const *w, const int64_t *M, int64_t K, int64_t N, const void **img);
 
 // tensor helpers
 bool is_contiguous(const tensor *t);

@@ -732,7 +732,33 @@ struct G9Mats {
     int n, ny, xcd;
     int nfull;                  // tiles [0, nfull) run whole; each later tile runs as two 64-row halves
     int toff;                   // 128 x 64 launch after a 128 x 128 one: its tiles start at this index (xcd order)
+    // prefill chains (ggml_hip_chain_create_n): matrix i's y is the next launch's x, and the epilogue writes that
+    // launch's x image from the f32 values it stores (null: no image; M[i] % 64 == 0, image Np = this launch's)
+    uint8_t *xo[4];
 };
+
+// The epilogue's x image (prefill chains): the workgroup's f32 outputs staged in LDS as [token][row] (row
+// stride G9_TS floats), then 8 lanes per (token, 32-row block) run x9_store_lane on them, exactly what
+// k_prep9_x does with the same floats read from y: the image is bitwise gemm9_prep_x's of y.  ntok x nrow
+// is the workgroup's tile (rows from its first, m0 = the tile's first row of the matrix); every thread of
+// the workgroup calls it.
+static constexpr int G9_TS = 136;                   // 544 B: 16-byte aligned rows, tokens 4 apart on other banks
+template <int NTOK, int NROW>
+__device__ __forceinline__ void g9_ximage_out(const float *T, int m0, int n0, int M, int N, int nbo, uint8_t *xo,
+                                              int64_t Np) {
+    constexpr int ITEMS = NTOK * (NROW / 32), PER = G9_THREADS / 8;
+    uint16_t *xod = reinterpret_cast<uint16_t *>(xo + (int64_t)nbo * Np * 48);
+    const int lane = threadIdx.x & 63, sub = lane & 7;
+#pragma unroll 1
+    for (int base = 0; base < ITEMS; base += PER) {         // uniform trip count: x9_store_lane uses DPP
+        const int it = base + (int)(threadIdx.x >> 3);
+        const int blk = it / NTOK, tok = it - blk * NTOK;
+        const bool live = it < ITEMS && n0 + tok < N && m0 + 32 * blk + 32 <= M;
+        float4 v = {0.f, 0.f, 0.f, 0.f};
+        if (live) v = *reinterpret_cast<const float4 *>(T + tok * G9_TS + 32 * blk + 4 * sub);
+        x9_store_lane(v, sub, n0 + tok, (m0 >> 5) + blk, live, xo, xod, Np);
+    }
+}
 
 // Timing-only diagnostic builds (tools/build_variant.sh FILE=q4_0_gemm -DGEMM9_KO=n; results invalid):
 // 1 = no LDS DMAs at all (compute only), 2 = no x code DMAs, 3 = no weight code DMAs.
@@ -932,6 +958,22 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
             }
         }
     }
+    uint8_t *xo = mi == 0 ? mats.xo[0] : mi == 1 ? mats.xo[1] : mi == 2 ? mats.xo[2] : mats.xo[3];
+    if (xo) {                                                   // workgroup-uniform
+        __syncthreads();                                        // red's reads are done
+        float *T = reinterpret_cast<float *>(smem);
+        if (wave < 4) {
+            const int l0 = r0 - (HALF ? 64 * hsel : 0);         // the row within this workgroup's rows
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int tl = 32 * (q & 1) + (i & 3) + 8 * (i >> 2) + 4 * h;
+                T[tl * G9_TS + l0] = acc0[i];
+                if constexpr (!HALF) T[tl * G9_TS + l0 + 32] = acc1[i];
+            }
+        }
+        __syncthreads();
+        g9_ximage_out<G9_BN, HALF ? 64 : G9_BM>(T, m0 + (HALF ? 64 * hsel : 0), n0, M, N, M >> 5, xo, Np);
+    }
 }
 
 // The larger tile (round 5, verdict r4 item 3): 128 rows x 128 tokens per workgroup, half the LDS-DMA bytes
@@ -1102,6 +1144,20 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9w_q4_0(const G9Mats mats
             }
         }
     }
+    uint8_t *xo = mi == 0 ? mats.xo[0] : mi == 1 ? mats.xo[1] : mi == 2 ? mats.xo[2] : mats.xo[3];
+    if (xo) {                                                   // workgroup-uniform; the last sync drained the DMAs
+        float *T = reinterpret_cast<float *>(smem);
+        if (wave < 8) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int tl = 32 * tq + (i & 3) + 8 * (i >> 2) + 4 * h;
+                T[tl * G9_TS + r0] = acc0[i];
+                T[tl * G9_TS + r1] = acc1[i];
+            }
+        }
+        __syncthreads();
+        g9_ximage_out<W9_BN, G9_BM>(T, m0, n0, M, N, M >> 5, xo, Np);
+    }
 }
 
 
@@ -1155,11 +1211,17 @@ hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int
 }
 
 hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int64_t K, const void *xws, int64_t N,
-                           float *const *yv, const int64_t *ldyv, hipStream_t s) {
+                           float *const *yv, const int64_t *ldyv, hipStream_t s, uint8_t *const *xo) {
     const int nb = (int)(K / QK);
     const int64_t Np = gemm9_np(N), Ny = (N + G9_BN - 1) / G9_BN;
     if (n < 1 || n > 4 || N <= 0 || nb <= 0) return hipErrorInvalidValue;
     G9Mats mats{};
+    for (int i = 0; i < n && xo; i++) {
+        if (!xo[i]) continue;
+        if (Mv[i] % 64 != 0 || ldyv[i] != Mv[i] || !x9_fits(Mv[i], Np) || (Mv[i] / QK) * Np * 48 >= ((int64_t)1 << 31))
+            return hipErrorInvalidValue;
+        mats.xo[i] = xo[i];
+    }
     mats.n = n;
     mats.ny = (int)Ny;
     mats.tb[0] = 0;

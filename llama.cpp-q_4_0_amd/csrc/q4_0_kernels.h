@@ -110,9 +110,11 @@ size_t gemm9_x_bytes(int64_t K, int64_t N);
 size_t gemm9_w_bytes(int64_t K, int64_t M);
 hipError_t gemm9_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStream_t s);
 hipError_t gemm9_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStream_t s);
-// one launch over the row tiles of n (1..4) sibling weight images that share the x image
+// one launch over the row tiles of n (1..4) sibling weight images that share the x image; xo (optional, per
+// matrix, null entries allowed): the epilogue also writes matrix i's y as the x image of a next launch (K = M[i],
+// same N; bitwise gemm9_prep_x of y; M[i] % 64 == 0, ldy[i] == M[i], gemm9_x_bytes(M[i], N) bytes)
 hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *M, int64_t K, const void *xws, int64_t N,
-                           float *const *y, const int64_t *ldy, hipStream_t s);
+                           float *const *y, const int64_t *ldy, hipStream_t s, uint8_t *const *xo = nullptr);
 hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,
                      hipStream_t s);
 // the 128 x 128 tile (k_gemm9w): -1 auto by rounds of CUs (GGML_HIP_GEMM9_WIDE overrides), 0 never, 1 always

@@ -109,6 +109,9 @@ def _bind(L):
         "ggml_hip_graph_launch": ([vp, vp], i32),
         "ggml_hip_graph_destroy": ([vp], i32),
         "ggml_hip_chain_create": ([i32, vp, vp], i32),
+        "ggml_hip_chain_create_n": ([i32, vp, i64, vp], i32),
+        "ggml_hip_debug_set_chain_x9": ([i32], i32),
+        "ggml_hip_debug_chain_links": ([i32, vp, i64, vp, vp], i32),
         "ggml_hip_chain_launch": ([vp, vp], i32),
         "ggml_hip_chain_status": ([vp], i32),
         "ggml_hip_chain_destroy": ([vp], i32),
@@ -255,10 +258,11 @@ def _ptr(b):
 
 
 class Chain:
-    """A decode chain (ggml_hip_chain_*): tasks = [(ws, Ms, K, x, ys), ...] run in stream order, one
-    sibling GEMV per task; task t reads x after every earlier task wrote its y."""
+    """A chain (ggml_hip_chain_*): tasks = [(ws, Ms, K, x, ys), ...] run in stream order, one sibling
+    launch per task; task t reads x after every earlier task wrote its y.  N = 1: decode (GEMVs, optional
+    engine); N > 1: ggml_hip_chain_create_n (prefill: GEMM epilogues write the next task's x image)."""
 
-    def __init__(self, tasks, engine=None):
+    def __init__(self, tasks, engine=None, N=1):
         L = load()
         arr = (ChainTask * len(tasks))()
         for t, (ws, Ms, K, x, ys) in enumerate(tasks):
@@ -270,7 +274,10 @@ class Chain:
                 arr[t].M[i] = Ms[i]
                 arr[t].y[i] = _ptr(ys[i])
         self.h = ctypes.c_void_p()
-        check(L.ggml_hip_chain_create(len(tasks), arr, ctypes.byref(self.h)), "chain_create")
+        if N == 1:
+            check(L.ggml_hip_chain_create(len(tasks), arr, ctypes.byref(self.h)), "chain_create")
+        else:
+            check(L.ggml_hip_chain_create_n(len(tasks), arr, N, ctypes.byref(self.h)), "chain_create_n")
         if engine is not None:
             self.set_engine(engine)
 
@@ -283,10 +290,11 @@ class Chain:
         return rc == 1
 
     def engine_info(self):
-        """{on, units, max_stream_bytes, weight_bytes, cus} of the engine's plan (on = 0: per-launch path)"""
-        v = (ctypes.c_int64 * 5)()
-        check(load().ggml_hip_chain_engine_info(self.h, v, 5), "chain_engine_info")
-        return dict(zip(("on", "units", "max_stream_bytes", "weight_bytes", "cus"), list(v)))
+        """{on, units, max_stream_bytes, weight_bytes, cus} of the engine's plan (on = 0: per-launch path), and
+        epilogue_images: tasks of an N-token chain whose x image a producer's GEMM epilogue writes"""
+        v = (ctypes.c_int64 * 6)()
+        check(load().ggml_hip_chain_engine_info(self.h, v, 6), "chain_engine_info")
+        return dict(zip(("on", "units", "max_stream_bytes", "weight_bytes", "cus", "epilogue_images"), list(v)))
 
     def launch(self, stream=None):
         check(load().ggml_hip_chain_launch(self.h, stream), "chain_launch")

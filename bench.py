@@ -936,15 +936,15 @@ def run_launch(gh, L, kind, a, xs, stream):
         gh.check(L.ggml_hip_mul_mat_q4_0_ex(buf.ptr, K, m_loc, xs[K].ptr, 1, yb.ptr, m_loc, 1, stream))
 
 
-def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0, 1, 2), (3,), (4, 5), (6,))):
+def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=10, warm=3, groups=((0, 1, 2), (3,), (4, 5), (6,))):
     """N-token prefill through `layers` layers of the stack (7 mul_mats each), sibling groups as in decode
     (wq|wk|wv and w1|w3 share src1: one launch per group, ggml_hip_mul_mat_q4_0_multi's grouping).
     Headline: the layers as ONE dependent chain (ggml_hip_chain_create_n), the decode's data dependencies at N
     tokens: wq|wk|wv read the previous layer's w2 output (layer 0: a fixed N x 4096 input), wo reads q, w1|w3
-    read wo's output, w2 reads w1's output; every k_gemm9 epilogue writes the next launch's fp6 x image beside
-    its y, so the chain runs ONE k_prep9_x (verdict r5 item 6).  Beside it: the same chain with every image
-    built by k_prep9_x (the epilogue fold off), and the round-5 figure (each group on a fixed input x, one
-    k_prep9_x per group).  GB/s = (W + 4KN + 4MN) / t."""
+    read wo's output, w2 reads w1's output (verdict r5 item 6); each task's fp6 x image by k_prep9_x.  Beside
+    it: the same chain with each k_gemm9 epilogue writing the next launch's x image (opt-in: bitwise the same,
+    measured slower), and the round-5 figure (each group on a fixed input x).  GB/s = (W + 4KN + 4MN) / t
+    (SURVEY.md §8d config 3)."""
     mats = [m for row in stack.mats[:layers] for m in row]
     ybuf = {}
     calls = []
@@ -972,7 +972,8 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0,
             gh.check(L.ggml_hip_mul_mat_q4_0_multi(n, wp, mp, K, xs[K].ptr, N, yp, stream))
 
     def timed(fn=run):
-        fn()
+        for _ in range(warm):           # clocks and TLBs settle over the first passes (tools/prefill_chain_ab.py)
+            fn()
         gh.check(L.ggml_hip_stream_synchronize(stream))
         a, b = gh.Event(), gh.Event()
         a.record(stream)
@@ -987,20 +988,21 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0,
 
     def chain_timed():
         ch = gh.Chain(chain_tasks, N=N)
-        chain["epilogue_images"] = ch.engine_info()["epilogue_images"]
+        chain["epilogue_links"] = ch.engine_info()["epilogue_images"]
         go = lambda: ch.launch(stream)
-        t_fold = timed(go)
-        last = ybuf[6].download((N, 4096), np.float32, stream)
-        gh.check(L.ggml_hip_debug_set_chain_x9(0))
+        gh.check(L.ggml_hip_debug_set_chain_x9(0))         # the default: every x image by k_prep9_x
+        t_prep = timed(go)
+        last_prep = ybuf[6].download((N, 4096), np.float32, stream)
+        gh.check(L.ggml_hip_debug_set_chain_x9(1))         # opt-in: the producers' epilogues write them
         try:
-            chain["t_prep"] = timed(go)
-            last_prep = ybuf[6].download((N, 4096), np.float32, stream)
+            chain["t_fold"] = timed(go)
+            last = ybuf[6].download((N, 4096), np.float32, stream)
         finally:
             gh.check(L.ggml_hip_debug_set_chain_x9(-1))
-        chain["bitwise_vs_prep"] = bool(np.array_equal(last.view(np.uint32), last_prep.view(np.uint32)))
+        chain["bitwise_fold_vs_prep"] = bool(np.array_equal(last.view(np.uint32), last_prep.view(np.uint32)))
         chain["t_indep"] = timed(run)
         del ch
-        return t_fold
+        return t_prep
 
     # default path: each weight's image built once, as the hook does on a resident weight's first
     # prefill (ggml_hip_weight_image_create): fp6 images + k_gemm9 (GEMM version 10, the
@@ -1031,22 +1033,22 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0,
     # v_mfma_scale_f32_32x32x64_f8f6f4 with e2m3 operands runs at ~10 PF dense (MI355X_MICROARCH.md, FP6 row);
     # k_gemm9 puts each q8_0 value into it as TWO e2m3 digits (q = 16 (q >> 4) + (q & 15), one per K half), so
     # one instruction advances the algorithm's K by 32, not 64: the effective peak of 2*M*K*N is 5 POP/s.
-    # achieved = 2*M*K*N over the dependent layer chain (its one x image prep included); kernel_only from the
-    # newest committed rocprofv3 summary of this bench (k_gemm9* durations of the fp6 passes: 1 warm-up + `reps`
-    # timed of the folded chain, then the same of the prep chain and of the fixed-input groups)
+    # achieved = 2*M*K*N over the dependent layer chain (its x image preps included); kernel_only from the
+    # newest committed rocprofv3 summary of this bench (k_gemm9* durations of the fp6 passes: `warm` + `reps`
+    # of the chain, then the same of the chain with the epilogue fold and of the fixed-input groups)
     roof = {"bound": "mfma", "kernel": "k_gemm9_q4_0 / k_gemm9w_q4_0",
             "instruction": "v_mfma_scale_f32_32x32x64_f8f6f4 (e2m3 x e2m3, block scales 2^1 / 2^5)",
             "instruction_peak": 10000.0, "effective_peak": 5000.0, "unit": "TOP/s",
             "peak_note": "10 PF fp6 dense; two e2m3 digits per q8_0 value -> 5 POP/s of the algorithm's 2*M*K*N",
             "achieved": round(ops / t / 1e12, 1), "frac": round(ops / t / 1e12 / 5000.0, 4),
-            "timing": "the 4-layer dependent prefill chain (HIP events over `reps` passes), its x image prep included"}
+            "timing": "the 4-layer dependent prefill chain (HIP events over `reps` passes after `warm`), x image preps included"}
     prof = newest_profile("_bench_rocprofv3_kernel_stats.csv")
     if prof:
         try:
             st = rocprof_stats(prof)
             g9 = sum(tt_ for k, (c, tt_) in st.items() if "k_gemm9" in k)
             if g9 > 0:
-                passes = 3 * (reps + 1)
+                passes = 3 * (reps + warm)
                 roof["kernel_only_TOPs"] = round(ops * passes / (g9 * 1e-9) / 1e12, 1)
                 roof["kernel_only_frac"] = round(ops * passes / (g9 * 1e-9) / 1e12 / 5000.0, 4)
                 roof["kernel_only_source"] = (f"{os.path.relpath(prof, ROOT)}: sum of k_gemm9* durations over "
@@ -1058,15 +1060,15 @@ def prefill_bench(gh, L, stack, xs, ys, stream, N, layers=4, reps=3, groups=((0,
             "mfma_frac": round(ops / t / 1e12 / INT8_PEAK_TOPS, 4), "peak_TOPs": INT8_PEAK_TOPS,
             "stack_7B_prefill_ms": round(t / layers * 32 * 1e3, 3),
             "dependency": ("one dependent chain (ggml_hip_chain_create_n): wq|wk|wv <- previous w2 (layer 0: fixed "
-                           "N x 4096 input), wo <- wq, w1|w3 <- wo, w2 <- w1; each k_gemm9 epilogue writes the next "
-                           f"launch's fp6 x image ({chain.get('epilogue_images')} of {len(chain_tasks)} tasks), one "
-                           "k_prep9_x per chain"),
-            "chain_bitwise_vs_prep_images": chain.get("bitwise_vs_prep"),
+                           "N x 4096 input), wo <- wq, w1|w3 <- wo, w2 <- w1; each task's fp6 x image by k_prep9_x "
+                           "from its producer's y (the default; the epilogue fold below is opt-in)"),
+            "chain_epilogue_images": dict(alt("the same chain, each k_gemm9 epilogue writing the next launch's x image "
+                                              f"({chain.get('epilogue_links')} of {len(chain_tasks)} tasks; "
+                                              "ggml_hip_debug_set_chain_x9(1))", chain["t_fold"]),
+                                          bitwise_vs_default=chain.get("bitwise_fold_vs_prep")),
             "kernel": "k_gemm9_q4_0 / k_gemm9w_q4_0: exact block sums on the block-scaled fp6 MFMA, 128x64 or "
                       "128x128 workgroup tiles chosen per launch by rounds of CUs, per-weight e2m3 images built "
                       f"once (26 B per 32 weights; image bytes {image_bytes} for {layers} layers)",
-            "chain_prep_images": alt("the same chain, every x image by k_prep9_x (ggml_hip_debug_set_chain_x9(0))",
-                                     chain["t_prep"]),
             "independent_x": alt("each group on a fixed input x, one k_prep9_x per group (the round-5 figure)",
                                  chain["t_indep"]),
             "int8_images": alt("k_gemm8_q4_0: i8 MFMA on per-weight int8 images, fixed-input groups (34 B per 32 "

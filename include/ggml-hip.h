@@ -211,12 +211,13 @@ typedef struct ggml_hip_chain ggml_hip_chain;
 int ggml_hip_chain_create(int ntasks, const ggml_hip_chain_task *tasks, ggml_hip_chain **chain);
 /* N-token chains (prefill): x of a task is f32 [N][K], y[i] f32 [N][M[i]]; otherwise as above, bitwise n
  * separate ggml_hip_mul_mat_q4_0_multi calls at N.  A task whose siblings take one k_gemm9 launch on fp6
- * weight images (ggml_hip_weight_image_create) reads a chain-owned x image; when its x is exactly y[i] of an
- * earlier such task (M[i] == K, nothing in between writes it), that task's GEMM epilogue writes the image
- * beside y (no k_prep9_x launch).  Allocates the images (gemm9 x bytes per task) at create. */
+ * weight images (ggml_hip_weight_image_create) reads a chain-owned x image (gemm9 x bytes per task,
+ * allocated at create), built by k_prep9_x; with the epilogue fold on (ggml_hip_debug_set_chain_x9(1)), a
+ * task whose x is exactly y[i] of an earlier such task (M[i] == K, nothing in between writes it) gets it
+ * from that task's GEMM epilogue instead (bitwise the same; measured slower, so off by default). */
 int ggml_hip_chain_create_n(int ntasks, const ggml_hip_chain_task *tasks, int64_t N, ggml_hip_chain **chain);
-/* debug: 0 = N-token chains build every x image with k_prep9_x (A/B), 1 = epilogue images (default),
- * -1 = GGML_HIP_CHAIN_X9 */
+/* debug: 1 = N-token chains take x images from the producers' GEMM epilogues, 0 = every image by
+ * k_prep9_x (default), -1 = GGML_HIP_CHAIN_X9 (1 turns the fold on) */
 int ggml_hip_debug_set_chain_x9(int on);
 /* debug, no device needed: the epilogue links ggml_hip_chain_create_n would plan; prod[t] = the task whose
  * epilogue writes task t's x image (-1: k_prep9_x), share[t] = the earlier consumer whose image t reads (-1) */

@@ -342,11 +342,16 @@ int chain_create(int ntasks, const ggml_hip_chain_task *tasks, int64_t N, ggml_h
 // it as one (g9_images), the image from the producer's epilogue when the producer ran on k_gemm9 in this pass
 // (else k_prep9_x), and this launch's epilogue writing the images its consumers read; otherwise the plain
 // sibling call.  Either way y is bitwise ggml_hip_mul_mat_q4_0_multi's.
-std::atomic<int> g_chain_x9{-1};        // GGML_HIP_CHAIN_X9=0 / ggml_hip_debug_set_chain_x9(0): every task preps
+// GGML_HIP_CHAIN_X9=1 / ggml_hip_debug_set_chain_x9(1): the producers' epilogues write the consumers' x images.
+// Off by default: bitwise the same y, but measured 0.7-2.6 % slower over the bench's 4-layer chain
+// (profiles/r06_prefill_chain_ab.txt): the image conversion at the end of every tile runs with the tile's
+// workgroup alone on its CU (one 154 KB workgroup per CU), +1.3-5 us per launch, while k_prep9_x spreads the
+// same work over the whole GPU in ~5 us.
+std::atomic<int> g_chain_x9{-1};
 bool chain_x9_on() {
     int v = g_chain_x9.load(std::memory_order_relaxed);
     if (v < 0) {
-        v = (!getenv("GGML_HIP_CHAIN_X9") || atoi(getenv("GGML_HIP_CHAIN_X9")) != 0) ? 1 : 0;
+        v = (getenv("GGML_HIP_CHAIN_X9") && atoi(getenv("GGML_HIP_CHAIN_X9")) == 1) ? 1 : 0;
         g_chain_x9.store(v, std::memory_order_relaxed);
     }
     return v == 1;

@@ -1123,6 +1123,14 @@ int ggml_hip_debug_launch_stats(long long *out, int enable) {
     return GGML_HIP_OK;
 }
 
+// not in the public header: a busy wait of ns nanoseconds after every eager launch (0 = none): the end-to-end
+// token time's sensitivity to the host's per-launch cost (tools/e2e_llama.py modes "-padN")
+int ggml_hip_debug_set_launch_pad(int ns) {
+    flush_deferred();
+    ghip::g_launch_pad_ns.store(ns < 0 ? 0 : ns, std::memory_order_relaxed);
+    return GGML_HIP_OK;
+}
+
 // not in the public header: the decode norm chain folded into the GEMV prologue on (1) / off (0)
 int ggml_hip_debug_set_norm_fold(int on) {
     flush_deferred();

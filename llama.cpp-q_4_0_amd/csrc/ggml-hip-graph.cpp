@@ -484,6 +484,11 @@ void rec_stats(long long *runs, long long *kernels, long long *updated, long lon
 }
 
 std::atomic<bool> g_launch_prof{false};
+std::atomic<int> g_launch_pad_ns{getenv("GGML_HIP_LAUNCH_PAD_NS") ? atoi(getenv("GGML_HIP_LAUNCH_PAD_NS")) : 0};
+void launch_pad() {
+    const long long until = launch_prof_now() + g_launch_pad_ns.load(std::memory_order_relaxed);
+    while (launch_prof_now() < until) {}
+}
 static std::atomic<long long> g_lp_count{0}, g_lp_ns{0};
 long long launch_prof_now() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();

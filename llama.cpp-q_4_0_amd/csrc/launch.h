@@ -48,6 +48,10 @@ extern std::atomic<bool> g_launch_prof;   // read by the launcher thread, writte
 void launch_prof_add(long long ns);
 long long launch_prof_now();
 void launch_prof_read(long long *count, long long *ns, bool reset);
+// diagnostic (GGML_HIP_LAUNCH_PAD_NS): a busy wait of this many ns after every eager launch, to measure how
+// the end-to-end token time depends on the host's per-launch cost (tools/run.sh PARTS=e2e_pad)
+extern std::atomic<int> g_launch_pad_ns;
+void launch_pad();
 
 template <typename... P, typename... A>
 inline void launch_k(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t s, A &&...a) {
@@ -61,6 +65,7 @@ inline void launch_k(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStre
             return;
         }
         hipLaunchKernelGGL(k, grid, block, lds, s, std::forward<A>(a)...);
+        if (__builtin_expect(g_launch_pad_ns.load(std::memory_order_relaxed) > 0, 0)) launch_pad();
         return;
     }
     // convert every argument to the parameter's exact type, then hand the recorder their addresses

@@ -741,22 +741,37 @@ struct G9Mats {
 // stride G9_TS floats), then 8 lanes per (token, 32-row block) run x9_store_lane on them, exactly what
 // k_prep9_x does with the same floats read from y: the image is bitwise gemm9_prep_x's of y.  ntok x nrow
 // is the workgroup's tile (rows from its first, m0 = the tile's first row of the matrix); every thread of
-// the workgroup calls it.
+// the workgroup calls it, BEFORE the tile's y stores: the compiler puts s_waitcnt vmcnt(0) ahead of any LDS
+// read while global stores may be in flight (it cannot tell them from the LDS DMAs), so every T read is
+// issued first, with nothing outstanding, and the image stores last (+15-20 % per launch the other way round).
 static constexpr int G9_TS = 136;                   // 544 B: 16-byte aligned rows, tokens 4 apart on other banks
+// a workgroup barrier for LDS only (__syncthreads() also waits for outstanding global memory operations);
+// the asm clobbers keep the compiler's LDS accesses on their side of it
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 template <int NTOK, int NROW>
 __device__ __forceinline__ void g9_ximage_out(const float *T, int m0, int n0, int M, int N, int nbo, uint8_t *xo,
                                               int64_t Np) {
-    constexpr int ITEMS = NTOK * (NROW / 32), PER = G9_THREADS / 8;
+    constexpr int ITEMS = NTOK * (NROW / 32), PER = G9_THREADS / 8, IT = (ITEMS + PER - 1) / PER;
     uint16_t *xod = reinterpret_cast<uint16_t *>(xo + (int64_t)nbo * Np * 48);
-    const int lane = threadIdx.x & 63, sub = lane & 7;
-#pragma unroll 1
-    for (int base = 0; base < ITEMS; base += PER) {         // uniform trip count: x9_store_lane uses DPP
-        const int it = base + (int)(threadIdx.x >> 3);
+    const int sub = threadIdx.x & 7;
+    float4 v[IT];
+    bool live[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const int it = k * PER + (int)(threadIdx.x >> 3);
         const int blk = it / NTOK, tok = it - blk * NTOK;
-        const bool live = it < ITEMS && n0 + tok < N && m0 + 32 * blk + 32 <= M;
-        float4 v = {0.f, 0.f, 0.f, 0.f};
-        if (live) v = *reinterpret_cast<const float4 *>(T + tok * G9_TS + 32 * blk + 4 * sub);
-        x9_store_lane(v, sub, n0 + tok, (m0 >> 5) + blk, live, xo, xod, Np);
+        live[k] = it < ITEMS && n0 + tok < N && m0 + 32 * blk + 32 <= M;
+        v[k] = live[k] ? *reinterpret_cast<const float4 *>(T + tok * G9_TS + 32 * blk + 4 * sub) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < IT; k++) {                          // every lane calls x9_store_lane (DPP)
+        const int it = k * PER + (int)(threadIdx.x >> 3);
+        const int blk = it / NTOK, tok = it - blk * NTOK;
+        x9_store_lane(v[k], sub, n0 + tok, (m0 >> 5) + blk, live[k], xo, xod, Np);
     }
 }
 
@@ -938,6 +953,8 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
         }
     }
     __syncthreads();
+    uint8_t *xo = mi == 0 ? mats.xo[0] : mi == 1 ? mats.xo[1] : mi == 2 ? mats.xo[2] : mats.xo[3];
+    float *T = red + 8 * 256 * 4;                               // the epilogue's stage, after red (32 KB)
     if (wave < 4) {
 #pragma unroll
         for (int i = 0; i < 16; i += 4) {
@@ -948,6 +965,21 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
                 acc1[i] += o1.x; acc1[i + 1] += o1.y; acc1[i + 2] += o1.z; acc1[i + 3] += o1.w;
             }
         }
+        if (xo) {
+            const int l0 = r0 - (HALF ? 64 * hsel : 0);         // the row within this workgroup's rows
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int tl = 32 * (q & 1) + (i & 3) + 8 * (i >> 2) + 4 * h;
+                T[tl * G9_TS + l0] = acc0[i];
+                if constexpr (!HALF) T[tl * G9_TS + l0 + 32] = acc1[i];
+            }
+        }
+    }
+    if (xo) {                                                   // workgroup-uniform
+        lds_barrier();
+        g9_ximage_out<G9_BN, HALF ? 64 : G9_BM>(T, m0 + (HALF ? 64 * hsel : 0), n0, M, N, M >> 5, xo, Np);
+    }
+    if (wave < 4) {
         const int row0 = m0 + r0, row1 = m0 + r1;
 #pragma unroll
         for (int i = 0; i < 16; i++) {
@@ -957,22 +989,6 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9_q4_0(const G9Mats mats,
                 if (!HALF && row1 < M) y[(int64_t)tk * ldy + row1] = acc1[i];
             }
         }
-    }
-    uint8_t *xo = mi == 0 ? mats.xo[0] : mi == 1 ? mats.xo[1] : mi == 2 ? mats.xo[2] : mats.xo[3];
-    if (xo) {                                                   // workgroup-uniform
-        __syncthreads();                                        // red's reads are done
-        float *T = reinterpret_cast<float *>(smem);
-        if (wave < 4) {
-            const int l0 = r0 - (HALF ? 64 * hsel : 0);         // the row within this workgroup's rows
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int tl = 32 * (q & 1) + (i & 3) + 8 * (i >> 2) + 4 * h;
-                T[tl * G9_TS + l0] = acc0[i];
-                if constexpr (!HALF) T[tl * G9_TS + l0 + 32] = acc1[i];
-            }
-        }
-        __syncthreads();
-        g9_ximage_out<G9_BN, HALF ? 64 : G9_BM>(T, m0 + (HALF ? 64 * hsel : 0), n0, M, N, M >> 5, xo, Np);
     }
 }
 
@@ -1133,17 +1149,6 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9w_q4_0(const G9Mats mats
     }
     epi(acc0, S0, P0);
     epi(acc1, S1, P1);
-    if (wave < 8) {
-        const int row0 = m0 + r0, row1 = m0 + r1;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int tk = n0 + 32 * tq + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (tk < N) {
-                if (row0 < M) y[(int64_t)tk * ldy + row0] = acc0[i];
-                if (row1 < M) y[(int64_t)tk * ldy + row1] = acc1[i];
-            }
-        }
-    }
     uint8_t *xo = mi == 0 ? mats.xo[0] : mi == 1 ? mats.xo[1] : mi == 2 ? mats.xo[2] : mats.xo[3];
     if (xo) {                                                   // workgroup-uniform; the last sync drained the DMAs
         float *T = reinterpret_cast<float *>(smem);
@@ -1155,8 +1160,19 @@ __global__ __launch_bounds__(G9_THREADS, 1) void k_gemm9w_q4_0(const G9Mats mats
                 T[tl * G9_TS + r1] = acc1[i];
             }
         }
-        __syncthreads();
+        lds_barrier();
         g9_ximage_out<W9_BN, G9_BM>(T, m0, n0, M, N, M >> 5, xo, Np);
+    }
+    if (wave < 8) {
+        const int row0 = m0 + r0, row1 = m0 + r1;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int tk = n0 + 32 * tq + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (tk < N) {
+                if (row0 < M) y[(int64_t)tk * ldy + row0] = acc0[i];
+                if (row1 < M) y[(int64_t)tk * ldy + row1] = acc1[i];
+            }
+        }
     }
 }
 

@@ -1,11 +1,11 @@
 // Host cost of a raw AQL kernel dispatch (verdict r5 item 3: "measure a raw HSA AQL dispatch from the host before
 // building a hook-path submission on it"), beside hipLaunchKernelGGL on the same empty kernel:
-//   * the kernel object from a code object loaded through HSA (tools/aql_kernel.hip compiled with --genco),
+//   * the kernel object from a code object loaded through HSA (tools/aql_kernel.hip as a bare ELF, --no-gpu-bundle-output),
 //   * an own HSA queue (hsa_queue_create, single producer), kernarg ring in the kernarg memory pool,
 //   * per dispatch: reserve the write index, fill the packet + kernargs, publish the header with a release store,
 //     ring the doorbell.
 // 20,000 dispatches per path in batches of 200 (waits between batches untimed), host wall time per dispatch.
-//   hipcc --genco --offload-arch=gfx950 tools/aql_kernel.hip -o tools/aql_kernel.hsaco
+//   hipcc --offload-arch=gfx950 --cuda-device-only --no-gpu-bundle-output -c -O2 tools/aql_kernel.hip -o tools/aql_kernel.hsaco
 //   hipcc -O2 --offload-arch=gfx950 tools/aql_dispatch_cost.hip -o tools/aql_dispatch_cost -lhsa-runtime64
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
@@ -92,7 +92,7 @@ int main(int argc, char **argv) {
     hsa_queue_t *q;
     CKH(hsa_queue_create(g_gpu, 4096, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &q));
     const uint32_t qmask = q->size - 1;
-    const size_t slot = 256;
+    const size_t slot = ka_size <= 256 ? 256 : ((size_t)ka_size + 255) & ~(size_t)255;   // hidden args included
     char *karg = nullptr;
     CKH(hsa_amd_memory_pool_allocate(g_kernarg_pool, slot * q->size, 0, (void **)&karg));
     CKH(hsa_amd_agents_allow_access(1, &g_gpu, nullptr, karg));
@@ -107,6 +107,7 @@ int main(int argc, char **argv) {
         hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & qmask);
         Args a{y, (const unsigned char *)y, (const unsigned char *)y, (const unsigned char *)y, i, 2, 3, 4, 5, 6, y, 7L};
         char *ka = karg + (idx & qmask) * slot;
+        memset(ka, 0, slot);                       // hidden arguments zero (the kernel reads none)
         memcpy(ka, &a, sizeof a);
         p->workgroup_size_x = 1024;
         p->workgroup_size_y = 1;

@@ -1,5 +1,5 @@
 // The empty kernel tools/aql_dispatch_cost.hip dispatches through its own AQL queue (same argument list as its
-// hipLaunchKernelGGL twin). Built as a bare code object: hipcc --genco --offload-arch=gfx950 tools/aql_kernel.hip
+// hipLaunchKernelGGL twin).  A bare code object ELF (not an offload bundle): see tools/aql_dispatch_cost.hip
 #include <hip/hip_runtime.h>
 
 extern "C" __global__ void k_empty_aql(const float *x, const unsigned char *w0, const unsigned char *w1,

@@ -148,6 +148,10 @@ def main():
             # "-nokq": the decode KQ as its own launch
             L.ggml_hip_debug_set_kq_fold.argtypes = [ctypes.c_int]
             gh.check(L.ggml_hip_debug_set_kq_fold(0 if "-nokq" in mode else 1))
+            # "-padN": a busy wait of N ns after every eager launch (the token time's dependence on launch cost)
+            pad = int(mode.split("-pad")[1].split("-")[0]) if "-pad" in mode else 0
+            L.ggml_hip_debug_set_launch_pad.argtypes = [ctypes.c_int]
+            gh.check(L.ggml_hip_debug_set_launch_pad(pad))
             g0 = np.zeros(5, np.int64)
             L.ggml_hip_debug_graph_stats(g0.ctypes.data, 0)
             L.ggml_hip_debug_op_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
@@ -190,10 +194,14 @@ def main():
                 scale = float(np.abs(lg_cpu).max())
                 r["last_logits_vs_cpu"] = ("bitwise" if np.array_equal(lg8.view(np.uint32), lg_cpu.view(np.uint32))
                                            else f"max |d|/max|y| {float(np.abs(lg8 - lg_cpu).max()) / scale:.2e}")
-            res[f"offload_{mode}"] = r
+            key, k = f"offload_{mode}", 2
+            while key in res:                      # a mode listed twice (interleaved repeats)
+                key, k = f"offload_{mode}#{k}", k + 1
+            res[key] = r
             print(mode, r, file=sys.stderr, flush=True)
         gh.check(L.ggml_hip_set_exact(0))
         gh.check(L.ggml_hip_debug_set_graph(0))
+        gh.check(L.ggml_hip_debug_set_launch_pad(0))
     finally:
         os.remove(model)
         os.rmdir(d)

@@ -55,8 +55,21 @@ if has aql; then     # host cost per dispatch: hipLaunchKernelGGL vs a raw AQL p
   step aql 120 ./tools/aql_dispatch_cost tools/aql_kernel.hsaco
   cat "$O/aql.log"
 fi
+if has pchain; then  # prefill chain A/B (fixed x, dependent calls, chain with k_prep9_x, chain with epilogue images)
+  step pchain 300 python tools/prefill_chain_ab.py ${PCHAIN_ROUNDS:-4}
+  tail -1 "$O/pchain.log" | cut -c1-400
+  for m in chain_fold chain_prep; do   # per-kernel durations of each chain form
+    step pchain_$m 300 rocprofv3 --kernel-trace --stats -d "$O/$m" -o run --output-format csv -- \
+        python3 tools/prefill_chain_ab.py 1 $m
+  done
+fi
 if has e2e; then     # the hook path end to end: the reference llama.cpp at full offload, LLaMA-7B shape
   step e2e 700 python tools/e2e_llama.py --decode 128 --modes fast,exact --out "$O/e2e_7b.json" ${E2E_ARGS:-}
+fi
+if has e2e_pad; then # the token time against a padded per-launch host cost (verdict r5 item 3: does submission bind?)
+  step e2e_pad 900 python tools/e2e_llama.py --decode 64 --no-cpu \
+      --modes fast,fast-pad1000,fast-pad2000,fast-pad3000,fast,fast-pad1000,fast-pad2000,fast-pad3000 --out "$O/e2e_pad.json"
+  python3 -c "import json; r=json.load(open('$O/e2e_pad.json')); print({k: v['decode_tok_s'] for k, v in r.items() if k.startswith('offload')})"
 fi
 if has e2e_variant; then
   # a variant library through GGML_HIP_LIB, then the reference llama.cpp through the shim (the round-5 abort at

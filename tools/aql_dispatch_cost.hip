@@ -155,6 +155,73 @@ int main(int argc, char **argv) {
                    ns / (batches * per) / 1e3);
         }
     }
+    // Device side: the time per DEPENDENT dispatch (barrier bit) of the same empty 256 x 1024 grid, back to back:
+    // HIP (hipLaunchKernelGGL, events around 2,000 launches) against 2,000 AQL packets written first and released by
+    // one doorbell, with system-scope and with agent-scope acquire/release fences (what the CP does at every kernel
+    // boundary: HIP's packets carry system scope), and without the barrier bit (no ordering, for reference).
+    {
+        const int n = 2000;
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        for (int round = 0; round < 3; round++) {
+            CK(hipEventRecord(e0, s));
+            for (int i = 0; i < n; i++)
+                hipLaunchKernelGGL(k_empty_hip, dim3(256), dim3(1024), 0, s, (const float *)y, (const unsigned char *)y,
+                                   (const unsigned char *)y, (const unsigned char *)y, i, 2, 3, 4, 5, 6, y, 7L);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms = 0.f;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("round %d device, hipLaunchKernelGGL back to back   %.3f us per kernel\n", round, ms * 1e3f / n);
+            const char *names[3] = {"AQL, barrier, system-scope fences", "AQL, barrier, agent-scope fences ",
+                                    "AQL, no barrier, agent-scope      "};
+            for (int mode = 0; mode < 3; mode++) {
+                const uint16_t scope = mode == 0 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+                const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                        ((mode < 2 ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
+                                        (scope << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                        (scope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+                // the last packet: barrier + system scope so the signal sees everything
+                const uint16_t last_header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                             (1 << HSA_PACKET_HEADER_BARRIER) |
+                                             (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                             (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+                const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+                hsa_signal_store_relaxed(done, 1);
+                uint64_t first = 0, idx = 0;
+                for (int i = 0; i < n; i++) {
+                    idx = hsa_queue_add_write_index_relaxed(q, 1);
+                    if (i == 0) first = idx;
+                    while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {}
+                    hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & qmask);
+                    Args a{y, (const unsigned char *)y, (const unsigned char *)y, (const unsigned char *)y, i, 2, 3, 4, 5, 6, y, 7L};
+                    char *ka = karg + (idx & qmask) * slot;
+                    memset(ka, 0, slot);
+                    memcpy(ka, &a, sizeof a);
+                    p->workgroup_size_x = 1024; p->workgroup_size_y = 1; p->workgroup_size_z = 1;
+                    p->grid_size_x = 256 * 1024; p->grid_size_y = 1; p->grid_size_z = 1;
+                    p->private_segment_size = prv;
+                    p->group_segment_size = grp;
+                    p->kernel_object = kobj;
+                    p->kernarg_address = ka;
+                    p->completion_signal = i == n - 1 ? done : hsa_signal_t{0};
+                    __atomic_store_n((uint32_t *)p, (uint32_t)(i == n - 1 ? last_header : header) | ((uint32_t)setup << 16),
+                                     __ATOMIC_RELEASE);
+                }
+                (void)first;
+                const auto t0 = std::chrono::steady_clock::now();
+                hsa_signal_store_screlease(q->doorbell_signal, idx);            // one doorbell for all
+                if (hsa_signal_wait_scacquire(done, HSA_SIGNAL_CONDITION_LT, 1, 5000000000ull, HSA_WAIT_STATE_ACTIVE) != 0) {
+                    printf("AQL batch did not complete\n");
+                    return 1;
+                }
+                const auto t1 = std::chrono::steady_clock::now();
+                printf("round %d device, %s %.3f us per kernel\n", round, names[mode],
+                       std::chrono::duration<double, std::micro>(t1 - t0).count() / n);
+            }
+        }
+    }
     CK(hipStreamSynchronize(s));
     hsa_signal_destroy(done);
     hsa_queue_destroy(q);

@@ -239,10 +239,6 @@ int ggml_hip_chain_destroy(ggml_hip_chain *chain);
  * create.  info: [0] engine on, [1] work units, [2] largest per-CU stream (bytes), [3] weight bytes, [4] CUs,
  * [5] (N-token chains) tasks whose x image a producer's GEMM epilogue writes. */
 int ggml_hip_chain_set_engine(ggml_hip_chain *chain, int mode);
-/* Weight prefetcher beside a per-launch decode chain (N = 1): one wave per CU streams the chain's weights in
- * consumption order into the Infinity Cache, at most `lookahead` launches ahead of the chain (0 = off), on a
- * stream of its own forked from and joined to the launch stream.  Same y bitwise (it only reads). */
-int ggml_hip_chain_set_prefetch(ggml_hip_chain *chain, int lookahead);
 int ggml_hip_chain_engine_info(ggml_hip_chain *chain, int64_t *info, int n);
 
 /* ------------------------------------------------------------------------------------------

@@ -187,11 +187,6 @@ struct ggml_hip_chain {
     // (null: none) from the y of matrix out_mat.  Consumers of one producer's output share its image.
     std::vector<void *> ximg, out_img, owned;
     std::vector<int> prod_task, out_mat;
-    // weight prefetcher beside the per-launch decode chain (ggml_hip_chain_set_prefetch)
-    int pf_lookahead = 0, pf_n = 0;
-    ghip::PrefetchEnt *pf_ents = nullptr;   // device
-    hipStream_t pf_stream = nullptr;
-    hipEvent_t pf_fork = nullptr, pf_join = nullptr;
 };
 
 namespace {
@@ -301,17 +296,6 @@ int chain_plan_images(ggml_hip_chain *c) {
         if (c->prod_task[t] >= 0) c->out_img[c->prod_task[t]] = p;
     }
     return GGML_HIP_OK;
-}
-
-void chain_prefetch_off(ggml_hip_chain *c) {
-    if (c->pf_ents) (void)hipFree(c->pf_ents);
-    if (c->pf_stream) (void)hipStreamDestroy(c->pf_stream);
-    if (c->pf_fork) (void)hipEventDestroy(c->pf_fork);
-    if (c->pf_join) (void)hipEventDestroy(c->pf_join);
-    c->pf_ents = nullptr;
-    c->pf_stream = nullptr;
-    c->pf_fork = c->pf_join = nullptr;
-    c->pf_lookahead = c->pf_n = 0;
 }
 
 int chain_create(int ntasks, const ggml_hip_chain_task *tasks, int64_t N, ggml_hip_chain **out) {
@@ -472,59 +456,10 @@ int ggml_hip_chain_launch(ggml_hip_chain *c, void *stream) {
         }
         return GGML_HIP_OK;
     }
-    const bool pf = c->pf_lookahead > 0 && !exact_mode();
-    if (pf) {                               // the prefetcher on its own stream, forked from and joined to s
-        uint32_t *prog = ghip::gemv_progress_ptr();
-        if (!prog) return fail(GGML_HIP_ERR_DEVICE, "GEMV progress counter not found");
-        ghip::rec_flush_at("chain prefetch");
-        HIP_RET(hipMemsetAsync(prog, 0, 4, s));
-        HIP_RET(hipEventRecord(c->pf_fork, s));
-        HIP_RET(hipStreamWaitEvent(c->pf_stream, c->pf_fork, 0));
-        HIP_RET(ghip::weight_prefetch(c->pf_ents, c->pf_n, c->pf_lookahead, g_dev[c->device].info.num_cus, 2000000u,
-                                      c->pf_stream));
-    }
     for (const auto &k : c->tasks) {
         const int rc = ggml_hip_mul_mat_q4_0_multi(k.nmat, k.W, k.M, k.K, k.x, 1, (float *const *)k.y, s);
         if (rc != GGML_HIP_OK) return rc;
     }
-    if (pf) {
-        HIP_RET(hipEventRecord(c->pf_join, c->pf_stream));
-        HIP_RET(hipStreamWaitEvent(s, c->pf_join, 0));
-    }
-    return GGML_HIP_OK;
-}
-
-int ggml_hip_chain_set_prefetch(ggml_hip_chain *c, int lookahead) {
-    ensure_init();
-    if (!c || lookahead < 0) return fail(GGML_HIP_ERR_INVALID, "bad arguments");
-    if (current_device() != c->device) return fail(GGML_HIP_ERR_INVALID, "chain belongs to another device");
-    if (c->pf_ents) {
-        HIP_RET(GHIP_SYNC(hipDeviceSynchronize)());
-        chain_prefetch_off(c);
-    }
-    if (lookahead == 0) return GGML_HIP_OK;
-    if (c->N != 1) return fail(GGML_HIP_ERR_INVALID, "the weight prefetcher runs beside N = 1 (decode) chains");
-    std::vector<ghip::PrefetchEnt> e;
-    for (size_t t = 0; t < c->tasks.size(); t++) {
-        const ggml_hip_chain_task &k = c->tasks[t];
-        for (int i = 0; i < k.nmat; i++) {
-            const uint64_t bytes = (uint64_t)k.M[i] * (uint64_t)(k.K / QK) * Q4B;
-            if (bytes >= ((uint64_t)1 << 31)) return fail(GGML_HIP_ERR_UNSUPPORTED, "matrix too large for the prefetcher");
-            e.push_back({(const uint8_t *)k.W[i], (uint32_t)bytes, (uint32_t)t});
-        }
-    }
-    ghip::rec_flush_at("chain prefetch");
-    if (hipMalloc(&c->pf_ents, e.size() * sizeof(ghip::PrefetchEnt)) != hipSuccess ||
-        hipMemcpy(c->pf_ents, e.data(), e.size() * sizeof(ghip::PrefetchEnt), hipMemcpyHostToDevice) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->pf_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->pf_join, hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
-        chain_prefetch_off(c);
-        return fail(GGML_HIP_ERR_NOMEM, "prefetch plan allocation failed");
-    }
-    c->pf_n = (int)e.size();
-    c->pf_lookahead = lookahead;
     return GGML_HIP_OK;
 }
 
@@ -545,11 +480,10 @@ int ggml_hip_chain_status(ggml_hip_chain *c) {
 }
 
 int ggml_hip_chain_destroy(ggml_hip_chain *c) {
-    if (c && (c->eng || !c->owned.empty() || c->pf_ents)) {
+    if (c && (c->eng || !c->owned.empty())) {
         (void)GHIP_SYNC(hipDeviceSynchronize)();
         if (c->eng) ghip::engine_plan_destroy(c->eng);
         chain_free_images(c);
-        chain_prefetch_off(c);
     }
     delete c;
     return GGML_HIP_OK;

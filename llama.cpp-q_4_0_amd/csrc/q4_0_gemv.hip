@@ -132,10 +132,6 @@ __device__ __forceinline__ double wave_sum_d64(double v) {   // every lane gets 
     return v;
 }
 
-// GEMV launches started since the last reset (lane 0 of workgroup 0 adds 1 at its start): the pace the weight
-// prefetcher beside a decode chain keeps (k_weight_prefetch)
-__device__ uint32_t g_gemv_progress;
-
 #ifdef GEMV_STAMPS
 // diagnostic builds only (tools/build_variant.sh ... -DGEMV_STAMPS): per-wave s_memrealtime stamps of the
 // launches whose M equals g_gemv_stamp_m: [wave][4] = start, x in LDS, end, HW_ID | XCC_ID << 32
@@ -164,7 +160,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_gemv_q4_0(const float *__restric
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (blockIdx.x == 0 && tid == 0) __hip_atomic_fetch_add(&g_gemv_progress, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the y / ldy choice at a row's end is written as sums of deltas selected by (row >=
     // row_begin[i]) so that it compiles to s_cselect (a ternary chain over four struct fields is
     // turned into a lookup table in scratch by the optimizer)
@@ -904,58 +899,6 @@ hipError_t gemv_q4_0_multi_norm(int nmat, const void *const *W, const int64_t *M
         if (ppl == 3) return launch_gemv_norm<3, 3>(m, K, b, dev, s, nrm, rd, epi);
     }
     return hipErrorInvalidValue;        // K > 12288: chunked items are not instantiated with the prologue
-}
-
-// ---------------------------------------------------------------------------------------------
-// Weight prefetcher beside a decode chain (ggml_hip_chain_set_prefetch): a GEMV whose weights are already in the
-// Infinity Cache runs 15 % shorter per layer (tools/mall_probe.py: q|k|v 7.86 -> 6.55 us, w1|w3 11.0 -> 9.2), so one
-// wave per CU streams the chain's weights in consumption order into the cache (LDS-DMA into a 1 KiB sink that is
-// never read), at most `lookahead` launches ahead of the chain: entry e (the weights of launch L) waits until
-// launch L - lookahead has started (g_gemv_progress).  The HBM is busy in the chain's launch boundaries too.
-// Every wait is bounded (timeout: the wave exits; the chain never waits for the prefetcher).
-__global__ __launch_bounds__(64) void k_weight_prefetch(const PrefetchEnt *__restrict__ ents, int n, int lookahead,
-                                                        uint32_t timeout_ticks) {
-    __shared__ __attribute__((aligned(16))) uint8_t sink[1024];
-    const int lane = threadIdx.x;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t seen = 0;
-    int inflight = 0;
-    for (int e = 0; e < n; e++) {
-        const uint8_t *p = ents[e].p;
-        const uint32_t bytes = ents[e].bytes;
-        const int need = (int)ents[e].launch - lookahead + 1;
-        while ((int)seen < need) {
-            seen = __hip_atomic_load(&g_gemv_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((int)seen >= need) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) return;
-            __builtin_amdgcn_s_sleep(4);
-        }
-        const uint32_t per = (((bytes + gridDim.x - 1) / gridDim.x) + 1023u) & ~1023u;
-        const uint32_t lo = blockIdx.x * per;
-        if (lo >= bytes) continue;
-        const uint32_t hi = lo + per < bytes ? lo + per : bytes;
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(p, bytes);          // bounds-checked: no read past the matrix
-        for (uint32_t off = lo; off < hi; off += 1024) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t *)sink, 16, (int)(off + lane * 16), 0, 0, 0);
-            if (++inflight == 48) {
-                asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-                inflight = 32;
-            }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-uint32_t *gemv_progress_ptr() {
-    void *p = nullptr;
-    return hipGetSymbolAddress(&p, HIP_SYMBOL(g_gemv_progress)) == hipSuccess ? (uint32_t *)p : nullptr;
-}
-
-hipError_t weight_prefetch(const PrefetchEnt *ents, int n, int lookahead, int cus, uint32_t timeout_ticks, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    (void)hipGetLastError();
-    launch_k(k_weight_prefetch, dim3((unsigned)cus), dim3(64), 0, s, ents, n, lookahead, timeout_ticks);
-    return hipGetLastError();
 }
 
 }  // namespace ghip

@@ -34,15 +34,6 @@ hipError_t dequantize_q4_0(const void *wq, int64_t K, int64_t M, float *w, hipSt
 // Decode / small-batch path: fused q8_0 quantize of x (in LDS) + q4_0.q8_0 GEMV.
 // N <= gemv_max_tokens(K).
 int gemv_max_tokens(int64_t K);
-// weight prefetcher beside a decode chain (q4_0_gemv.hip): entries in consumption order, `launch` = the chain's
-// GEMV launch index that reads them; g_gemv_progress counts GEMV launches started since it was zeroed
-struct PrefetchEnt {
-    const uint8_t *p;
-    uint32_t bytes;
-    uint32_t launch;
-};
-uint32_t *gemv_progress_ptr();
-hipError_t weight_prefetch(const PrefetchEnt *ents, int n, int lookahead, int cus, uint32_t timeout_ticks, hipStream_t s);
 hipError_t gemv_q4_0(const void *W, int64_t K, int64_t M, const float *x, int64_t N,
                      float *y, int64_t ldy, const DeviceInfo &dev, hipStream_t s);
 

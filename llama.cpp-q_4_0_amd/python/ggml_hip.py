@@ -116,7 +116,6 @@ def _bind(L):
         "ggml_hip_chain_status": ([vp], i32),
         "ggml_hip_chain_destroy": ([vp], i32),
         "ggml_hip_chain_set_engine": ([vp, i32], i32),
-        "ggml_hip_chain_set_prefetch": ([vp, i32], i32),
         "ggml_hip_chain_engine_info": ([vp, vp, i32], i32),
         "ggml_hip_last_error": ([], cp),
         "ggml_hip_version": ([], cp),
@@ -289,10 +288,6 @@ class Chain:
         if rc < 0:
             check(rc, "chain_set_engine")
         return rc == 1
-
-    def set_prefetch(self, lookahead):
-        """the weight prefetcher beside the per-launch chain, `lookahead` launches ahead (0 = off)"""
-        check(load().ggml_hip_chain_set_prefetch(self.h, int(lookahead)), "chain_set_prefetch")
 
     def engine_info(self):
         """{on, units, max_stream_bytes, weight_bytes, cus} of the engine's plan (on = 0: per-launch path), and

@@ -365,47 +365,3 @@ def test_engine_against_oracle():
             y_ref = O.mul_mat(wq[t][i], K, xin.reshape(1, K), nthreads=1)
             _, s_abs = block_terms(wq[t][i], xq, K)
             check_y(y, y_ref, s_abs, rtol=1e-3, atol_blocks=1e-6)
-
-
-# ---- the weight prefetcher beside the per-launch chain (ggml_hip_chain_set_prefetch) ----------------------------
-@pytest.mark.parametrize("lookahead", [1, 4])
-def test_prefetch_chain_bitwise_eager_and_graph(lookahead):
-    """The prefetcher only reads (LDS-DMA into a sink): the chain's y stay bitwise the separate calls', eager and
-    captured into a graph (fork / join with the prefetcher's stream), over replays with fresh inputs."""
-    c = ChainCase(llama_layers(2), seed=11)
-    ch = ggml_hip.Chain(c.tasks(0))
-    ch.set_prefetch(lookahead)
-    for rep in range(2):
-        c.randomize(110 + rep)
-        ch.launch()
-        c.run_separate()
-        assert ch.status() == 0
-        assert_bitwise(c.outputs(0), c.outputs(1))
-    g = ggml_hip.Graph(None)
-    with g:
-        ch.launch(ggml_hip.load().ggml_hip_default_stream())
-    for rep in range(2):
-        c.randomize(112 + rep)
-        g.launch()
-        c.run_separate()
-        assert ch.status() == 0
-        assert_bitwise(c.outputs(0), c.outputs(1))
-    del g
-    ch.set_prefetch(0)                                   # off again: the plain path
-    c.randomize(114)
-    ch.launch()
-    c.run_separate()
-    assert_bitwise(c.outputs(0), c.outputs(1))
-
-
-def test_prefetch_declines_prefill_chains():
-    import ctypes
-    L = ggml_hip.load()
-    w, x, y = DB(18 * 2 * 64), DB(64 * 4 * 100), DB(64 * 4 * 100)
-    t = (ggml_hip.ChainTask * 1)()
-    t[0].nmat, t[0].K, t[0].x = 1, 64, x.ptr
-    t[0].W[0], t[0].M[0], t[0].y[0] = w.ptr, 64, y.ptr
-    h = ctypes.c_void_p()
-    assert L.ggml_hip_chain_create_n(1, t, 100, ctypes.byref(h)) == ggml_hip.OK
-    assert L.ggml_hip_chain_set_prefetch(h, 4) == ggml_hip.ERR_INVALID
-    assert L.ggml_hip_chain_destroy(h) == ggml_hip.OK

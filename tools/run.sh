@@ -63,14 +63,6 @@ if has pchain; then  # prefill chain A/B (fixed x, dependent calls, chain with k
         python3 tools/prefill_chain_ab.py 1 $m
   done
 fi
-if has mall; then    # GEMV per launch with HBM-streamed vs Infinity-Cache-resident weights (tools/mall_probe.py)
-  step mall 300 python tools/mall_probe.py
-  tail -1 "$O/mall.log" | cut -c1-600
-fi
-if has prefetch; then  # the decode chain with the weight prefetcher beside it (tools/prefetch_ab.py)
-  step prefetch 300 python tools/prefetch_ab.py ${PF_ROUNDS:-3} ${PF_LOOKS:-2,4,8}
-  tail -1 "$O/prefetch.log" | cut -c1-900
-fi
 if has e2e; then     # the hook path end to end: the reference llama.cpp at full offload, LLaMA-7B shape
   step e2e 700 python tools/e2e_llama.py --decode 128 --modes fast,exact --out "$O/e2e_7b.json" ${E2E_ARGS:-}
 fi

@@ -63,6 +63,10 @@ if has pchain; then  # prefill chain A/B (fixed x, dependent calls, chain with k
         python3 tools/prefill_chain_ab.py 1 $m
   done
 fi
+if has mall; then    # GEMV per launch with HBM-streamed vs Infinity-Cache-resident weights (tools/mall_probe.py)
+  step mall 300 python tools/mall_probe.py
+  tail -1 "$O/mall.log" | cut -c1-600
+fi
 if has e2e; then     # the hook path end to end: the reference llama.cpp at full offload, LLaMA-7B shape
   step e2e 700 python tools/e2e_llama.py --decode 128 --modes fast,exact --out "$O/e2e_7b.json" ${E2E_ARGS:-}
 fi

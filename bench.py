@@ -427,7 +427,20 @@ def main():
         barrier()
         return time.perf_counter() - t0
 
-    elapsed_launches = timed(run_step)
+    # the per-launch chain two ways, interleaved twice, best of each: replayed as one HIP graph per token, and
+    # issued eagerly from the host (128 launches at ~2.7 us of host time each stay ahead of the ~0.93 ms device
+    # step; tools/prefetch_ab.py measured the eager form 1-2 % faster on the device)
+    if graph is not None:
+        t_graph, t_eager = [], []
+        for _ in range(2):
+            t_graph.append(timed(run_step))
+            t_eager.append(timed(decode_step))
+        elapsed_graph, elapsed_eager = min(t_graph), min(t_eager)
+        eager_wins = elapsed_eager < elapsed_graph
+        elapsed_launches = min(elapsed_graph, elapsed_eager)
+    else:
+        elapsed_graph, elapsed_eager, eager_wins = None, timed(run_step), True
+        elapsed_launches = elapsed_eager
     last = yb[6].download((LAYER[6][2],), np.float32, stream=stream)          # the step's last output
     finite = bool(np.all(np.isfinite(last)))
     if not finite:
@@ -465,14 +478,19 @@ def main():
                    "graph": graph is not None,
                    "decode_path": ("persistent LDS-DMA engine: ONE launch per token (ggml_hip_chain_set_engine), "
                                    "outputs bitwise the per-launch GEMVs'" if use_engine else
-                                   "per-launch GEMVs, one HIP graph per token"),
+                                   "per-launch GEMVs, " + ("issued eagerly (faster than the per-token HIP graph here)"
+                                                           if eager_wins else "one HIP graph per token")),
                    "launches_per_layer": 0.0 if use_engine else len(groups),
                    "sibling_batching": "wq|wk|wv and w1|w3 share src1 -> one launch each" if batch else "off",
                    "collectives_per_layer": 0, "parallelism": "single GPU", "activations_finite": finite},
     }
     result["config"]["runtime_libs"] = gh.mapped_runtime_libs()
-    result["launches_graph"] = {"tok_s": round(args.steps / elapsed_launches * 32 / args.layers, 2),
-                                "ms_per_step": round(elapsed_launches / args.steps * 1e3, 4),
+    if elapsed_graph is not None:
+        result["launches_graph"] = {"tok_s": round(args.steps / elapsed_graph * 32 / args.layers, 2),
+                                    "ms_per_step": round(elapsed_graph / args.steps * 1e3, 4),
+                                    "launches_per_layer": len(groups)}
+    result["launches_eager"] = {"tok_s": round(args.steps / elapsed_eager * 32 / args.layers, 2),
+                                "ms_per_step": round(elapsed_eager / args.steps * 1e3, 4),
                                 "launches_per_layer": len(groups)}
     if engine is not None:
         result["engine"] = {k: v for k, v in engine.items() if k != "elapsed_s"}
@@ -729,7 +747,7 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, ms_per_step, n_la
                     isolated=True, reps=10):
     """The decode roofline, priced on the TIMED step itself (verdict r5 item 5: the dominant kernel's time per step
     cannot exceed the step).  Every launch of a step is the decode GEMV (k_gemv_q4_0<1,...>): 4 sibling launches
-    per layer, back to back in one HIP graph, so achieved = the step's algorithmic bytes / ms_per_step (the launch
+    per layer, back to back (one HIP graph per token, or issued eagerly: the faster), so achieved = the step's algorithmic bytes / ms_per_step (the launch
     boundaries inside the step are charged to the GEMVs; avg_launch_us = step / launches).  Algorithmic bytes of a
     launch = sum over its matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y).  Beside it:
       rocprof_check: from the newest committed rocprofv3 summary of this bench's own timed replays
@@ -762,7 +780,7 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, ms_per_step, n_la
            "traffic": traffic, "traffic_source": src,
            "algorithmic_bytes_per_launch_mean": round(step_bytes / launches), "algorithmic_bytes_per_step": step_bytes,
            "launches_per_step": launches, "avg_launch_us": round(t_step / launches * 1e6, 3),
-           "timing": "the timed step: ms_per_step of the per-launch graph (barrier + synchronize around `steps` replays)",
+           "timing": "the timed step: ms_per_step of the per-launch chain, graph or eager, the faster (barrier + synchronize around `steps` steps)",
            "bytes_per_launch_def": "sum over the launch's matrices of 18*M*K/32 (q4_0) + 4*K (f32 x) + 4*M (f32 y)"}
     prof = newest_profile("_bench_rocprofv3_kernel_stats.csv")
     if prof:

@@ -40,6 +40,20 @@ static hsa_status_t find_agents(hsa_agent_t agent, void *) {
     if (t == HSA_DEVICE_TYPE_CPU && g_cpu.handle == 0) g_cpu = agent;
     return HSA_STATUS_SUCCESS;
 }
+static hsa_amd_memory_pool_t g_dev_pool{};
+static bool g_have_dev_pool = false;
+static hsa_status_t find_dev_pool(hsa_amd_memory_pool_t pool, void *) {    // the GPU's coarse-grained VRAM pool
+    hsa_amd_segment_t seg;
+    hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+    if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+    uint32_t flags = 0;
+    hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+    if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && !g_have_dev_pool) {
+        g_dev_pool = pool;
+        g_have_dev_pool = true;
+    }
+    return HSA_STATUS_SUCCESS;
+}
 static hsa_status_t find_kernarg_pool(hsa_amd_memory_pool_t pool, void *) {
     hsa_amd_segment_t seg;
     hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
@@ -96,6 +110,17 @@ int main(int argc, char **argv) {
     char *karg = nullptr;
     CKH(hsa_amd_memory_pool_allocate(g_kernarg_pool, slot * q->size, 0, (void **)&karg));
     CKH(hsa_amd_agents_allow_access(1, &g_gpu, nullptr, karg));
+    // kernargs in VRAM (what HIP does by default on this GPU family) for the device-side comparison, written by the
+    // CPU through the large-BAR mapping; skipped where the pool or the CPU access is not available
+    char *karg_dev = nullptr;
+    if (hsa_amd_agent_iterate_memory_pools(g_gpu, find_dev_pool, nullptr) == HSA_STATUS_SUCCESS && g_have_dev_pool &&
+        hsa_amd_memory_pool_allocate(g_dev_pool, slot * q->size, 0, (void **)&karg_dev) == HSA_STATUS_SUCCESS) {
+        if (hsa_amd_agents_allow_access(1, &g_cpu, nullptr, karg_dev) != HSA_STATUS_SUCCESS) {
+            hsa_amd_memory_pool_free(karg_dev);
+            karg_dev = nullptr;
+        }
+    }
+    printf("VRAM kernargs: %s\n", karg_dev ? "yes" : "no");
     hsa_signal_t done;
     CKH(hsa_signal_create(1, 0, nullptr, &done));
     printf("kernel object %#llx, kernarg %u B, group %u, private %u, queue size %u\n", (unsigned long long)kobj, ka_size,
@@ -174,12 +199,13 @@ int main(int argc, char **argv) {
             float ms = 0.f;
             CK(hipEventElapsedTime(&ms, e0, e1));
             printf("round %d device, hipLaunchKernelGGL back to back   %.3f us per kernel\n", round, ms * 1e3f / n);
-            const char *names[3] = {"AQL, barrier, system-scope fences", "AQL, barrier, agent-scope fences ",
-                                    "AQL, no barrier, agent-scope      "};
-            for (int mode = 0; mode < 3; mode++) {
-                const uint16_t scope = mode == 0 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+            const char *names[4] = {"AQL, barrier, system-scope fences", "AQL, barrier, agent-scope fences ",
+                                    "AQL, no barrier, agent-scope      ", "AQL, barrier, system, VRAM kernargs"};
+            for (int mode = 0; mode < (karg_dev ? 4 : 3); mode++) {
+                char *kbase = mode == 3 ? karg_dev : karg;
+                const uint16_t scope = (mode == 0 || mode == 3) ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
                 const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                        ((mode < 2 ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
+                                        ((mode != 2 ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
                                         (scope << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                         (scope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
                 // the last packet: barrier + system scope so the signal sees everything
@@ -196,9 +222,8 @@ int main(int argc, char **argv) {
                     while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {}
                     hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & qmask);
                     Args a{y, (const unsigned char *)y, (const unsigned char *)y, (const unsigned char *)y, i, 2, 3, 4, 5, 6, y, 7L};
-                    char *ka = karg + (idx & qmask) * slot;
-                    memset(ka, 0, slot);
-                    memcpy(ka, &a, sizeof a);
+                    char *ka = kbase + (idx & qmask) * slot;
+                    memcpy(ka, &a, sizeof a);                    // (the kernel reads no hidden argument)
                     p->workgroup_size_x = 1024; p->workgroup_size_y = 1; p->workgroup_size_z = 1;
                     p->grid_size_x = 256 * 1024; p->grid_size_y = 1; p->grid_size_z = 1;
                     p->private_segment_size = prv;

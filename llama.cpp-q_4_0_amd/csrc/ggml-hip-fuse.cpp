@@ -1081,12 +1081,12 @@ std::atomic<int> &graph_flag() {
     return f;
 }
 bool graph_enabled() { return graph_flag().load(std::memory_order_relaxed) != 0; }
-int graph_apply_mode() {           // 1: HIP graphs, 2: launcher thread (launch.h); returns the mode
+int graph_apply_mode() {           // 1: HIP graphs, 2: launcher thread, 3: own AQL queue (launch.h); returns the mode
     static int applied = -1;
     const int m = graph_flag().load(std::memory_order_relaxed);
     if (m != applied && m != 0) ghip::rec_set_mode(m);
     applied = m;
-    return m == 2 ? 2 : (m != 0 ? 1 : 0);
+    return m == 2 || m == 3 ? m : (m != 0 ? 1 : 0);
 }
 
 bool hook_holding() { return g_grp.n != 0 || g_pend.n != 0 || g_norm.on || g_kq; }
@@ -1120,6 +1120,13 @@ int ggml_hip_debug_launch_stats(long long *out, int enable) {
     flush_deferred();
     ghip::launch_prof_read(&out[0], &out[1], enable == 1);
     if (enable >= 0) ghip::g_launch_prof = enable != 0;
+    return GGML_HIP_OK;
+}
+
+// not in the public header: AQL launch mode counters: out[0] dispatches through the own queue, out[1] launches that
+// fell back to hipLaunchKernel
+int ggml_hip_debug_aql_stats(long long *out) {
+    ghip::aql_counts(&out[0], &out[1]);
     return GGML_HIP_OK;
 }
 
@@ -1160,7 +1167,8 @@ int ggml_hip_debug_set_x9_fold(int on) {
     return GGML_HIP_OK;
 }
 
-// not in the public header: launch recording for the hook path: 0 off, 1 HIP graphs, 2 launcher thread
+// not in the public header: launch recording for the hook path: 0 off, 1 HIP graphs, 2 launcher thread, 3 own AQL
+// queue (ggml-hip-aql.cpp)
 int ggml_hip_debug_set_graph(int on) {
     flush_deferred();
     graph_flag().store(on);

@@ -297,7 +297,7 @@ bool rec_active(hipStream_t s) {
 
 bool rec_pending() {
     REC_LOCK;
-    if (!rec().cur.items.empty()) return true;
+    if (!rec().cur.items.empty() || aql_pending()) return true;
     const Launcher &L = launcher();
     return L.started && L.head.load(std::memory_order_relaxed) != L.tail.load(std::memory_order_acquire);
 }
@@ -372,6 +372,14 @@ void rec_kernel(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s
         async_push(fn, grid, block, lds, nargs, args, sizes, aligns);
         return;
     }
+    if (r.mode == 3) {
+        if (aql_dispatch(fn, grid, block, lds, r.stream, nargs, args, sizes, aligns)) return;
+        aql_drain();                           // the queue's work first, then this launch through HIP, in order
+        aql_fallback_counted();
+        REC_CK(hipLaunchKernel(fn, grid, block, const_cast<void **>(args), lds, r.stream));
+        aql_stream_dirty();
+        return;
+    }
     Item it;
     it.fn = fn;
     it.grid = grid;
@@ -407,6 +415,8 @@ void rec_flush_at(const char *why) {
 void rec_flush() {
     REC_LOCK;
     async_drain();
+    if (aql_pending()) aql_drain();
+    aql_stream_dirty();                        // the caller's HIP call comes next (mode 3 waits for it)
     submit(false);
 }
 
@@ -462,7 +472,7 @@ void submit(bool chunk) {
 void rec_set_mode(int mode) {
     REC_LOCK;
     rec_flush();
-    rec().mode = mode == 2 ? 2 : 1;
+    rec().mode = mode == 2 || mode == 3 ? mode : 1;
 }
 
 void rec_enable(hipStream_t s, bool on) {

@@ -36,8 +36,17 @@ void rec_flush();
 void rec_flush_at(const char *why);      // the same, naming the caller (GGML_HIP_TRACE_GRAPH=1 prints it)
 // recording on / off for stream s (switching stream or turning it off submits what is pending)
 void rec_enable(hipStream_t s, bool on);
-// 1: runs submitted as cached HIP graphs; 2: a launcher thread issues the launches in order
+// 1: runs submitted as cached HIP graphs; 2: a launcher thread issues the launches in order; 3: each launch
+// goes straight into an own AQL queue (ggml-hip-aql.cpp)
 void rec_set_mode(int mode);
+// mode 3 (ggml-hip-aql.cpp): dispatch (false: the caller launches through HIP), drain, pending, HIP-work marker
+bool aql_dispatch(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, int nargs, void *const *args,
+                  const size_t *sizes, const size_t *aligns);
+void aql_drain();
+bool aql_pending();
+void aql_stream_dirty();
+void aql_fallback_counted();
+void aql_counts(long long *dispatches, long long *fallbacks);
 // counters: submitted runs, kernels in them, nodes updated in place, graphs instantiated, host ns
 // spent submitting (mode 2: waits for the launcher thread to drain, and the ns spent waiting)
 void rec_stats(long long *runs, long long *kernels, long long *updated, long long *built, long long *submit_ns);

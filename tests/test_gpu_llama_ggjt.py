@@ -405,3 +405,44 @@ def test_launch_recorder_bitwise_vs_eager(tmp_path, exact, mode):
     assert runs >= 120 and kernels >= 120 * 5 * hp["n_layer"], stats[1]   # >= 5 launches per decode layer
     assert updated > 0, stats[1]                  # n_past-dependent nodes change every step
     assert built * 10 < runs, stats[1]            # replayed, not re-instantiated per run
+
+
+@pytest.mark.parametrize("hp,n_prompt,n_decode", [(HP128, 40, 30), (G.HP, 8, 20)], ids=["head128", "head64"])
+def test_aql_launch_mode_bitwise(tmp_path, hp, n_prompt, n_decode):
+    """Launch mode 3 (ggml-hip-aql.cpp: the hook path's kernels into an own AQL queue, kernargs in VRAM) gives the
+    same logits bit for bit as eager hipLaunchKernel, prompt and decode, fast and exact kernels; the queue took the
+    launches (dispatch counter) and the fallbacks stay few."""
+    L = ggml_hip.load()
+    mp = str(tmp_path / "m.ggjt")
+    G.write(mp, hp=hp)
+    nv = hp["n_vocab"]
+    lib = ctypes.CDLL(HIP_LIB)
+    lib.refllama_bench.restype = ctypes.c_int
+    lib.refllama_bench.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    L.ggml_hip_debug_set_graph.argtypes = [ctypes.c_int]
+    L.ggml_hip_debug_aql_stats.argtypes = [ctypes.c_void_p]
+    prev = L.ggml_hip_get_exact()
+    out = {}
+    try:
+        for exact in (0, 1):
+            ggml_hip.check(L.ggml_hip_set_exact(exact), "set_exact")
+            for mode in (0, 3):
+                ggml_hip.check(L.ggml_hip_debug_set_graph(mode), "set_graph")
+                s0 = np.zeros(2, np.int64)
+                L.ggml_hip_debug_aql_stats(s0.ctypes.data)
+                lg = np.zeros(nv, np.float32)
+                res = np.zeros(3, np.float64)
+                assert lib.refllama_bench(mp.encode(), n_prompt, n_decode, 1, 99, 1024, 1, res.ctypes.data, lg.ctypes.data) == nv
+                s1 = np.zeros(2, np.int64)
+                L.ggml_hip_debug_aql_stats(s1.ctypes.data)
+                out[(exact, mode)] = (lg, s1 - s0)
+    finally:
+        L.ggml_hip_debug_set_graph(0)
+        L.ggml_hip_set_exact(prev)
+    for exact in (0, 1):
+        a, b = out[(exact, 0)][0], out[(exact, 3)][0]
+        assert np.isfinite(a).all()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f"exact={exact}"
+        disp, fb = out[(exact, 3)][1]
+        assert disp > n_decode * hp["n_layer"], (disp, fb)
+        assert fb <= disp // 10, (disp, fb)

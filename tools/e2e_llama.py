@@ -139,9 +139,10 @@ def main():
         L.ggml_hip_debug_graph_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
         for mode in args.modes.split(","):
             # modes: fast, exact; "-noepi" (below); suffix "-graph": launch recorder with HIP graphs (GGML_HIP_GRAPH=1),
-            # "-thread": launcher thread (GGML_HIP_GRAPH=2)
+            # "-thread": launcher thread (GGML_HIP_GRAPH=2), "-aql": own AQL queue (GGML_HIP_GRAPH=3)
             gh.check(L.ggml_hip_set_exact(1 if mode.startswith("exact") else 0))
-            gh.check(L.ggml_hip_debug_set_graph(1 if mode.endswith("-graph") else 2 if mode.endswith("-thread") else 0))
+            gh.check(L.ggml_hip_debug_set_graph(1 if mode.endswith("-graph") else 2 if mode.endswith("-thread") else
+                                                3 if "-aql" in mode else 0))
             # "-noepi": the decode q|k|v GEMV epilogue off (the held rope / copy nodes as their own batch)
             L.ggml_hip_debug_set_epi_fold.argtypes = [ctypes.c_int]
             gh.check(L.ggml_hip_debug_set_epi_fold(0 if "-noepi" in mode else 1))

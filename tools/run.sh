@@ -75,6 +75,11 @@ if has e2e_pad; then # the token time against a padded per-launch host cost (ver
       --modes fast,fast-pad1000,fast-pad2000,fast-pad3000,fast,fast-pad1000,fast-pad2000,fast-pad3000 --out "$O/e2e_pad.json"
   python3 -c "import json; r=json.load(open('$O/e2e_pad.json')); print({k: v['decode_tok_s'] for k, v in r.items() if k.startswith('offload')})"
 fi
+if has e2e_aql; then # launch mode 3 (own AQL queue) against eager launches, interleaved
+  step e2e_aql 900 python tools/e2e_llama.py --decode 128 --no-cpu \
+      --modes fast,fast-aql,fast,fast-aql,exact,exact-aql --out "$O/e2e_aql.json"
+  python3 -c "import json; r=json.load(open('$O/e2e_aql.json')); print({k: (v['decode_tok_s'], v.get('backend_host_ms_per_eval')) for k, v in r.items() if k.startswith('offload')})"
+fi
 if has e2e_variant; then
   # a variant library through GGML_HIP_LIB, then the reference llama.cpp through the shim (the round-5 abort at
   # teardown): the process must exit 0 after llama_free / llama_free_model, with ONE libggml_hip mapped

@@ -43,7 +43,7 @@ struct Aql {
     std::unordered_map<const void *, AqlKernel> kernels;
     uint64_t submitted = 0;               // dispatches since the last drain
     bool stream_dirty = true;             // HIP work may be pending on the backend stream
-    long long dispatches = 0, fallbacks = 0;
+    long long dispatches = 0, fallbacks = 0, drains = 0, stream_syncs = 0;
 };
 constexpr size_t SLOT = 1024;
 
@@ -166,9 +166,11 @@ bool aql_pending() { return aql().submitted > 0; }
 
 void aql_stream_dirty() { aql().stream_dirty = true; }
 
-void aql_counts(long long *dispatches, long long *fallbacks) {
-    *dispatches = aql().dispatches;
-    *fallbacks = aql().fallbacks;
+void aql_counts(long long *out) {
+    out[0] = aql().dispatches;
+    out[1] = aql().fallbacks;
+    out[2] = aql().drains;
+    out[3] = aql().stream_syncs;
 }
 
 // every dispatch so far complete (a barrier-AND packet with the completion signal, waited for on the host)
@@ -192,6 +194,7 @@ void aql_drain() {
         abort();
     }
     a.submitted = 0;
+    a.drains++;
 }
 
 // false: this launch cannot go through the queue (the caller launches it through HIP, in order)
@@ -228,9 +231,12 @@ bool aql_dispatch(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t
         u16[32] = (uint16_t)(grid.z > 1 || block.z > 1 ? 3 : grid.y > 1 || block.y > 1 ? 2 : 1);   // +64: grid dims
         u32[30] = (uint32_t)lds;                                                                       // +120
     }
+    bool after_hip = false;
     if (a.stream_dirty) {                                     // HIP work the kernel may depend on
         if (hipStreamSynchronize(s) != hipSuccess) return false;
         a.stream_dirty = false;
+        a.stream_syncs++;
+        after_hip = true;
     }
     const uint64_t idx = hsa_queue_add_write_index_relaxed(a.q, 1);
     while (idx - hsa_queue_load_read_index_scacquire(a.q) >= a.q->size - 1) {}
@@ -249,9 +255,12 @@ bool aql_dispatch(const void *fn, dim3 grid, dim3 block, size_t lds, hipStream_t
     p->kernarg_address = ka;
     p->completion_signal = hsa_signal_t{0};
     _mm_sfence();                                             // the write-combined kernarg stores land first
+    // fences: kernel -> kernel on this device needs agent scope only (a system-scope acquire invalidates the L2 at
+    // every kernel start); system scope to acquire what HIP's copies wrote, and at the drain (the host reads next)
+    const uint16_t acq = after_hip ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
     const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
-                            (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                            (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+                            (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                            (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
     const uint16_t setup = (uint16_t)((grid.z > 1 || block.z > 1 ? 3 : grid.y > 1 || block.y > 1 ? 2 : 1)
                                       << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS);
     __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);

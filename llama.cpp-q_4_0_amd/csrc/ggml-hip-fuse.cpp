@@ -1124,9 +1124,9 @@ int ggml_hip_debug_launch_stats(long long *out, int enable) {
 }
 
 // not in the public header: AQL launch mode counters: out[0] dispatches through the own queue, out[1] launches that
-// fell back to hipLaunchKernel
+// fell back to hipLaunchKernel, out[2] queue drains (host waits), out[3] host waits for the HIP stream
 int ggml_hip_debug_aql_stats(long long *out) {
-    ghip::aql_counts(&out[0], &out[1]);
+    ghip::aql_counts(out);
     return GGML_HIP_OK;
 }
 

@@ -46,7 +46,7 @@ void aql_drain();
 bool aql_pending();
 void aql_stream_dirty();
 void aql_fallback_counted();
-void aql_counts(long long *dispatches, long long *fallbacks);
+void aql_counts(long long *out);   // dispatches, fallbacks, drains, stream syncs
 // counters: submitted runs, kernels in them, nodes updated in place, graphs instantiated, host ns
 // spent submitting (mode 2: waits for the launcher thread to drain, and the ns spent waiting)
 void rec_stats(long long *runs, long long *kernels, long long *updated, long long *built, long long *submit_ns);

@@ -168,7 +168,14 @@ def main():
                 hp_lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhostprof.so"))
                 hp_lib.hostprof_stop.argtypes = [ctypes.c_char_p]
                 hp_lib.hostprof_start(50)
+            L.ggml_hip_debug_aql_stats.argtypes = [ctypes.c_void_p]
+            aq0 = np.zeros(4, np.int64)
+            L.ggml_hip_debug_aql_stats(aq0.ctypes.data)
             r, lg = bench(HIP_LIB, model, args.prompt, args.decode, args.threads_gpu, 99, 3, nv)
+            aq1 = np.zeros(4, np.int64)
+            L.ggml_hip_debug_aql_stats(aq1.ctypes.data)
+            if "-aql" in mode:       # per eval: dispatches, fallbacks, queue drains, HIP-stream waits
+                r["aql_per_eval"] = [round(float(v) / (3 + args.decode), 1) for v in (aq1 - aq0)]
             if args.hostprof:
                 r["hostprof_samples"] = hp_lib.hostprof_stop(f"{args.hostprof}.{mode}".encode())
             L.ggml_hip_debug_op_stats(st.ctypes.data, st.size, 1)

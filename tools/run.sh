@@ -78,7 +78,7 @@ fi
 if has e2e_aql; then # launch mode 3 (own AQL queue) against eager launches, interleaved
   step e2e_aql 900 python tools/e2e_llama.py --decode 128 --no-cpu \
       --modes fast,fast-aql,fast,fast-aql,exact,exact-aql --out "$O/e2e_aql.json"
-  python3 -c "import json; r=json.load(open('$O/e2e_aql.json')); print({k: (v['decode_tok_s'], v.get('backend_host_ms_per_eval')) for k, v in r.items() if k.startswith('offload')})"
+  python3 -c "import json; r=json.load(open('$O/e2e_aql.json')); print({k: (v['decode_tok_s'], v.get('backend_host_ms_per_eval'), v.get('aql_per_eval')) for k, v in r.items() if k.startswith('offload')})"
 fi
 if has e2e_variant; then
   # a variant library through GGML_HIP_LIB, then the reference llama.cpp through the shim (the round-5 abort at

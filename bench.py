@@ -430,22 +430,53 @@ def main():
     # the per-launch chain two ways, interleaved twice, best of each: replayed as one HIP graph per token, and
     # issued eagerly from the host (128 launches at ~2.7 us of host time each stay ahead of the ~0.93 ms device
     # step; tools/prefetch_ab.py measured the eager form 1-2 % faster on the device)
+    # A third form: the same eager launches through the library's own AQL queue (launch mode 3, ggml-hip-aql.cpp:
+    # 0.2-0.3 us of host time per dispatch, kernargs in VRAM, agent-scope fences between kernels); it must give the
+    # graph's outputs bit for bit to count
+    aql_ok = hasattr(L, "ggml_hip_debug_set_stream_launch_mode") and not args.eager
+
+    def timed_aql():                  # the stream's launches through the queue for the whole timed block
+        gh.check(L.ggml_hip_debug_set_stream_launch_mode(stream, 3))
+        try:
+            return timed(decode_step)
+        finally:
+            gh.check(L.ggml_hip_debug_set_stream_launch_mode(stream, 0))
+
     if graph is not None:
-        t_graph, t_eager = [], []
+        t_graph, t_eager, t_aql = [], [], []
         for _ in range(2):
             t_graph.append(timed(run_step))
             t_eager.append(timed(decode_step))
+            if aql_ok:
+                t_aql.append(timed_aql())
         elapsed_graph, elapsed_eager = min(t_graph), min(t_eager)
+        elapsed_aql = min(t_aql) if t_aql else None
         eager_wins = elapsed_eager < elapsed_graph
         elapsed_launches = min(elapsed_graph, elapsed_eager)
     else:
-        elapsed_graph, elapsed_eager, eager_wins = None, timed(run_step), True
+        elapsed_graph, elapsed_eager, eager_wins, elapsed_aql = None, timed(run_step), True, None
         elapsed_launches = elapsed_eager
     last = yb[6].download((LAYER[6][2],), np.float32, stream=stream)          # the step's last output
     finite = bool(np.all(np.isfinite(last)))
     if not finite:
         log("WARNING: the decode chain's last output is not finite")
     outs_launches = [yb[i].download((LAYER[i][2],), np.float32, stream=stream) for i in range(len(LAYER))]
+    aql_form = None
+    if elapsed_aql is not None:                # bitwise self-check of the AQL form against the graph's outputs
+        for i in range(len(LAYER)):
+            gh.check(L.ggml_hip_memset(yb[i].ptr, 0xFF, LAYER[i][2] * 4, stream))
+        gh.check(L.ggml_hip_debug_set_stream_launch_mode(stream, 3))
+        try:
+            decode_step()
+        finally:
+            gh.check(L.ggml_hip_debug_set_stream_launch_mode(stream, 0))
+        same = all(np.array_equal(yb[i].download((LAYER[i][2],), np.float32, stream=stream).view(np.uint32),
+                                  outs_launches[i].view(np.uint32)) for i in range(len(LAYER)))
+        aql_form = {"tok_s": round(args.steps / elapsed_aql * 32 / args.layers, 2),
+                    "ms_per_step": round(elapsed_aql / args.steps * 1e3, 4), "bitwise_vs_graph": bool(same)}
+        if same and elapsed_aql < elapsed_launches:
+            elapsed_launches = elapsed_aql
+            eager_wins = "aql"
     engine = None
     if args.decode != "launches" and graph is not None and batch:
         engine = engine_decode(gh, L, launch_args, yb, outs_launches, stream, timed)
@@ -478,8 +509,11 @@ def main():
                    "graph": graph is not None,
                    "decode_path": ("persistent LDS-DMA engine: ONE launch per token (ggml_hip_chain_set_engine), "
                                    "outputs bitwise the per-launch GEMVs'" if use_engine else
-                                   "per-launch GEMVs, " + ("issued eagerly (faster than the per-token HIP graph here)"
-                                                           if eager_wins else "one HIP graph per token")),
+                                   "per-launch GEMVs, " + (
+                                       "issued through the library's own AQL queue (launch mode 3; the fastest form here, "
+                                       "bitwise the graph's outputs)" if eager_wins == "aql" else
+                                       "issued eagerly (faster than the per-token HIP graph here)" if eager_wins else
+                                       "one HIP graph per token")),
                    "launches_per_layer": 0.0 if use_engine else len(groups),
                    "sibling_batching": "wq|wk|wv and w1|w3 share src1 -> one launch each" if batch else "off",
                    "collectives_per_layer": 0, "parallelism": "single GPU", "activations_finite": finite},
@@ -492,6 +526,8 @@ def main():
     result["launches_eager"] = {"tok_s": round(args.steps / elapsed_eager * 32 / args.layers, 2),
                                 "ms_per_step": round(elapsed_eager / args.steps * 1e3, 4),
                                 "launches_per_layer": len(groups)}
+    if aql_form is not None:
+        result["launches_aql"] = aql_form
     if engine is not None:
         result["engine"] = {k: v for k, v in engine.items() if k != "elapsed_s"}
     result["roofline"] = kernel_roofline(gh, L, launch_args, xs, stream, len(groups),

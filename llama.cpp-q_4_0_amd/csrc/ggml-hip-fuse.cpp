@@ -1130,6 +1130,22 @@ int ggml_hip_debug_aql_stats(long long *out) {
     return GGML_HIP_OK;
 }
 
+// not in the public header: every launch_k on `stream` through the launch recorder in `mode` (3: the own AQL queue,
+// ggml-hip-aql.cpp), 0 = back to eager HIP launches (drains first); for the tensor-free callers (bench.py's decode)
+int ggml_hip_debug_set_stream_launch_mode(void *stream, int mode) {
+    flush_deferred();
+    if (mode != 0 && mode != 3) return fail(GGML_HIP_ERR_INVALID, "mode must be 0 or 3");
+    hipStream_t s = resolve_stream(stream);
+    if (mode == 0) {
+        ghip::rec_enable(s, false);
+        ghip::rec_set_mode(1);
+        return GGML_HIP_OK;
+    }
+    ghip::rec_set_mode(3);
+    ghip::rec_enable(s, true);
+    return GGML_HIP_OK;
+}
+
 // not in the public header: a busy wait of ns nanoseconds after every eager launch (0 = none): the end-to-end
 // token time's sensitivity to the host's per-launch cost (tools/e2e_llama.py modes "-padN")
 int ggml_hip_debug_set_launch_pad(int ns) {

@@ -116,6 +116,7 @@ def _bind(L):
         "ggml_hip_chain_status": ([vp], i32),
         "ggml_hip_chain_destroy": ([vp], i32),
         "ggml_hip_chain_set_engine": ([vp, i32], i32),
+        "ggml_hip_debug_set_stream_launch_mode": ([vp, i32], i32),
         "ggml_hip_chain_engine_info": ([vp, vp, i32], i32),
         "ggml_hip_last_error": ([], cp),
         "ggml_hip_version": ([], cp),

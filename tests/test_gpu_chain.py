@@ -365,3 +365,24 @@ def test_engine_against_oracle():
             y_ref = O.mul_mat(wq[t][i], K, xin.reshape(1, K), nthreads=1)
             _, s_abs = block_terms(wq[t][i], xq, K)
             check_y(y, y_ref, s_abs, rtol=1e-3, atol_blocks=1e-6)
+
+
+def test_chain_through_aql_launch_mode_bitwise():
+    """The tensor-free launches of a stream routed through the own AQL queue (launch mode 3,
+    ggml_hip_debug_set_stream_launch_mode): the per-launch decode chain stays bitwise the separate calls',
+    over launches with fresh inputs (HIP fills / copies between them order against the queue)."""
+    L = ggml_hip.load()
+    L.ggml_hip_debug_set_stream_launch_mode.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    c = ChainCase(llama_layers(2), seed=12)
+    ch = ggml_hip.Chain(c.tasks(0))
+    s = L.ggml_hip_default_stream()
+    for rep in range(3):
+        c.randomize(120 + rep)
+        ggml_hip.check(L.ggml_hip_debug_set_stream_launch_mode(s, 3), "launch mode 3")
+        try:
+            ch.launch(s)
+        finally:
+            ggml_hip.check(L.ggml_hip_debug_set_stream_launch_mode(s, 0), "launch mode 0")
+        c.run_separate()
+        assert ch.status() == 0
+        assert_bitwise(c.outputs(0), c.outputs(1))

@@ -275,6 +275,8 @@ def main():
     ap.add_argument("--no-roofline-replays", action="store_true",
                     help="skip the per-position isolated replays of the roofline (profiling runs: the rocprof summary "
                          "then holds the timed replays' GEMVs only)")
+    ap.add_argument("--no-aql", action="store_true",
+                    help="decode: skip the form issued through the library's own AQL queue (launch mode 3)")
     ap.add_argument("--deadline", type=float, default=300.0,
                     help="N > 1: seconds after which a rank that has not finished aborts its communicator and exits "
                          "(rank 0 prints an error line); the self-launcher terminates its ranks 30 s later")
@@ -433,7 +435,9 @@ def main():
     # A third form: the same eager launches through the library's own AQL queue (launch mode 3, ggml-hip-aql.cpp:
     # 0.2-0.3 us of host time per dispatch, kernargs in VRAM, agent-scope fences between kernels); it must give the
     # graph's outputs bit for bit to count
-    aql_ok = hasattr(L, "ggml_hip_debug_set_stream_launch_mode") and not args.eager
+    # (not under a profiler: rocprofv3 wraps HSA queues, and this form writes its packets into its queue directly)
+    profiled = "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
+    aql_ok = hasattr(L, "ggml_hip_debug_set_stream_launch_mode") and not args.eager and not args.no_aql and not profiled
 
     def timed_aql():                  # the stream's launches through the queue for the whole timed block
         gh.check(L.ggml_hip_debug_set_stream_launch_mode(stream, 3))

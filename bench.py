@@ -844,6 +844,25 @@ def kernel_roofline(gh, L, launch_args, xs, stream, per_layer, ms_per_step, n_la
                 traced = eng[0][1] / eng[0][0] / 1e3
                 out["rocprof_check"]["engine_traced_avg_us"] = round(traced, 1)
                 out["rocprof_check"]["engine_untraced_step_us"] = round(engine_step_ms * 1e3, 1)
+            # the same check inside the traced run (tools/trace_steps.py): its own step, and the device span of its
+            # gap-free 128-launch windows against their summed durations
+            sp = newest_profile("_bench_rocprofv3_step_spans.json")
+            if sp and busy:
+                j = json.load(open(sp))
+                rc = out["rocprof_check"]
+                rc["spans_source"] = os.path.relpath(sp, ROOT)
+                if j.get("traced_ms_per_step"):
+                    rc["traced_step_us"] = round(j["traced_ms_per_step"] * 1e3, 1)
+                    rc["busy_le_traced_step"] = bool(busy <= j["traced_ms_per_step"] * 1e3)
+                gf = j.get("gap_free")
+                if gf:
+                    rc["device_bound_windows"] = j["gap_free_windows"]
+                    rc["window_sum_us_median"] = gf["sum_us_median"]
+                    rc["window_span_us_median"] = gf["span_us_median"]
+                    rc["window_sum_le_span"] = bool(gf["sum_us_median"] <= gf["span_us_median"])
+                rc["note"] = ("busy_le_step compares traced kernel durations with the UNtraced step; the tracer "
+                              "stamps every dispatch and its durations run ~2-5 % long, so the like-for-like checks "
+                              "are busy_le_traced_step and window_sum_le_span (both inside the traced run)")
         except Exception as e:       # a malformed summary must not cost the line
             out["rocprof_check"] = {"source": os.path.relpath(prof, ROOT), "error": str(e)}
     if engine_step_ms is not None:

@@ -34,6 +34,7 @@ if has prof; then    # the bench's own timed replays under the kernel tracer
   step prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- \
       python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-exact --no-roofline-replays --no-aql ${BENCH_ARGS:-}
   tail -1 "$O/prof.log" | cut -c1-300
+  python3 tools/trace_steps.py "$O/prof" "$O/prof.log" > "$O/step_spans.json" || true
 fi
 if has pmc; then     # decode GEMV HBM bytes: one counter per pass (gfx950: FETCH_SIZE is half the streamed bytes)
   for c in FETCH_SIZE WRITE_SIZE; do

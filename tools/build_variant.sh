@@ -16,5 +16,5 @@ done
 # same identity as the in-tree library (Makefile LDIDENT): SONAME libggml_hip.so, only ggml_* exported,
 # so a variant loaded by GGML_HIP_LIB is the one copy the shim's NEEDED libggml_hip.so resolves to
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../variants/libggml_hip_$name.so $objs \
-    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libggml_hip.so -Wl,--version-script,$PWD/exports.map
+    -L/opt/rocm/lib -lrccl -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libggml_hip.so -Wl,--version-script,$PWD/exports.map
 rm -rf ../variants/obj_$name

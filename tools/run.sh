@@ -81,6 +81,33 @@ if has e2e_aql; then # launch mode 3 (own AQL queue) against eager launches, int
       --modes fast,fast-aql,fast,fast-aql,exact,exact-aql --out "$O/e2e_aql.json"
   python3 -c "import json; r=json.load(open('$O/e2e_aql.json')); print({k: (v['decode_tok_s'], v.get('backend_host_ms_per_eval'), v.get('aql_per_eval')) for k, v in r.items() if k.startswith('offload')})"
 fi
+if has e2e_ab; then  # the in-tree library against variants/libggml_hip_$VARIANT.so, separate processes, interleaved
+  v=${VARIANT:-base}
+  for i in 1 2; do
+    step e2e_ab_base_$i 700 python tools/e2e_llama.py --decode 128 --no-cpu --modes ${AB_MODES:-fast} --out "$O/e2e_ab_base_$i.json"
+    GGML_HIP_LIB=$PWD/variants/libggml_hip_$v.so step e2e_ab_${v}_$i 700 python tools/e2e_llama.py --decode 128 --no-cpu \
+        --modes ${AB_MODES:-fast} --out "$O/e2e_ab_${v}_$i.json"
+  done
+  python3 -c "
+import json, glob
+for f in sorted(glob.glob('$O/e2e_ab_*.json')):
+    r = json.load(open(f)); print(f.split('/')[-1], {k: v['decode_tok_s'] for k, v in r.items() if k.startswith('offload')})"
+fi
+if has e2e_kstats; then  # e2e decode kernel durations, in-tree library and the variant (rocprofv3 kernel trace)
+  v=${VARIANT:-base}
+  step e2e_ks_base 600 rocprofv3 --kernel-trace --stats -d "$O/ks_base" -o run --output-format csv -- \
+      python3 tools/e2e_llama.py --decode 48 --no-cpu --modes fast
+  GGML_HIP_LIB=$PWD/variants/libggml_hip_$v.so step e2e_ks_$v 600 rocprofv3 --kernel-trace --stats -d "$O/ks_$v" -o run \
+      --output-format csv -- python3 tools/e2e_llama.py --decode 48 --no-cpu --modes fast
+fi
+if has kab; then      # decode GEMV launch times (tools/gemv_epi_ab.py), in-tree library vs variants/libggml_hip_$VARIANT.so
+  v=${VARIANT:-base}
+  for i in 1 2; do
+    step kab_base_$i 300 python tools/gemv_epi_ab.py 200 2
+    GGML_HIP_LIB=$PWD/variants/libggml_hip_$v.so step kab_${v}_$i 300 python tools/gemv_epi_ab.py 200 2
+  done
+  for f in "$O"/kab_*.log; do echo "## $f"; grep " us$" "$f"; done
+fi
 if has e2e_variant; then
   # a variant library through GGML_HIP_LIB, then the reference llama.cpp through the shim (the round-5 abort at
   # teardown): the process must exit 0 after llama_free / llama_free_model, with ONE libggml_hip mapped

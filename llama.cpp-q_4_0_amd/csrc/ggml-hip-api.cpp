@@ -363,13 +363,15 @@ int chain_task_n(ggml_hip_chain *c, int t, std::vector<char> &ran9, hipStream_t 
     if (c->ximg[t] && g9_images(k.nmat, k.W, k.M, k.K, c->N, img)) {
         const bool fold = chain_x9_on();
         const int u = c->prod_task[t];
-        if (!(fold && u >= 0 && ran9[u])) HIP_RET(ghip::gemm9_prep_x(k.x, k.K, c->N, c->ximg[t], s));
+        if (!(fold && u >= 0 && ran9[u] == 2)) HIP_RET(ghip::gemm9_prep_x(k.x, k.K, c->N, c->ximg[t], s));
         uint8_t *xo[4] = {nullptr, nullptr, nullptr, nullptr};
         int64_t ldy[4];
         for (int i = 0; i < k.nmat; i++) ldy[i] = k.M[i];
-        if (fold && c->out_img[t]) xo[c->out_mat[t]] = (uint8_t *)c->out_img[t];
+        // ran9: 2 = this launch's epilogue wrote its consumers' image, 1 = k_gemm9 without it (they prep their own)
+        const bool wr = fold && c->out_img[t] && ghip::gemm9_xo_ok(k.M[c->out_mat[t]], c->N);
+        if (wr) xo[c->out_mat[t]] = (uint8_t *)c->out_img[t];
         HIP_RET(ghip::gemm9_run_multi(k.nmat, img, k.M, k.K, c->ximg[t], c->N, (float *const *)k.y, ldy, s, xo));
-        ran9[t] = 1;
+        ran9[t] = wr ? 2 : 1;
         return GGML_HIP_OK;
     }
     ran9[t] = 0;

@@ -1226,6 +1226,13 @@ hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int
     return gemm9_run_multi(1, &wws, &M, K, xws, N, &y, &ldy, s);
 }
 
+// whether an epilogue can write an M-row output at N tokens as the next launch's x image (the tile epilogue's
+// 64-row granules, its 32-bit image offsets)
+bool gemm9_xo_ok(int64_t M, int64_t N) {
+    const int64_t Np = gemm9_np(N);
+    return M > 0 && M % 64 == 0 && N > 0 && x9_fits(M, Np) && (M / QK) * Np * 48 < ((int64_t)1 << 31);
+}
+
 hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int64_t K, const void *xws, int64_t N,
                            float *const *yv, const int64_t *ldyv, hipStream_t s, uint8_t *const *xo) {
     const int nb = (int)(K / QK);
@@ -1234,8 +1241,7 @@ hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *Mv, int
     G9Mats mats{};
     for (int i = 0; i < n && xo; i++) {
         if (!xo[i]) continue;
-        if (Mv[i] % 64 != 0 || ldyv[i] != Mv[i] || !x9_fits(Mv[i], Np) || (Mv[i] / QK) * Np * 48 >= ((int64_t)1 << 31))
-            return hipErrorInvalidValue;
+        if (ldyv[i] != Mv[i] || !gemm9_xo_ok(Mv[i], N)) return hipErrorInvalidValue;
         mats.xo[i] = xo[i];
     }
     mats.n = n;

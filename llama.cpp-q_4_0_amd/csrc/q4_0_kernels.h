@@ -112,7 +112,8 @@ hipError_t gemm9_prep_x(const float *x, int64_t K, int64_t N, void *xws, hipStre
 hipError_t gemm9_prep_w(const void *W, int64_t K, int64_t M, void *wws, hipStream_t s);
 // one launch over the row tiles of n (1..4) sibling weight images that share the x image; xo (optional, per
 // matrix, null entries allowed): the epilogue also writes matrix i's y as the x image of a next launch (K = M[i],
-// same N; bitwise gemm9_prep_x of y; M[i] % 64 == 0, ldy[i] == M[i], gemm9_x_bytes(M[i], N) bytes)
+// same N; bitwise gemm9_prep_x of y; gemm9_xo_ok(M[i], N), ldy[i] == M[i], gemm9_x_bytes(M[i], N) bytes)
+bool gemm9_xo_ok(int64_t M, int64_t N);
 hipError_t gemm9_run_multi(int n, const void *const *wws, const int64_t *M, int64_t K, const void *xws, int64_t N,
                            float *const *y, const int64_t *ldy, hipStream_t s, uint8_t *const *xo = nullptr);
 hipError_t gemm9_run(const void *wws, int64_t K, int64_t M, const void *xws, int64_t N, float *y, int64_t ldy,

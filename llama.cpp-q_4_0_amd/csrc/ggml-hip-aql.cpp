@@ -6,7 +6,10 @@
 // name).  Ordering with the HIP stream the backend also uses (copies, memsets): the first dispatch after any HIP
 // work waits for that stream on the host, and every backend HIP call drains the queue first (rec_flush through
 // GHIP_SYNC: a barrier packet with a completion signal, waited for on the host).  A kernel this path cannot take
-// (no code-object symbol, an argument layout it does not know) runs through hipLaunchKernel in order.
+// (no code-object symbol, an argument layout it does not know) runs through hipLaunchKernel in order.  The hidden
+// arguments filled are the dispatch geometry and the dynamic LDS size; the runtime-service pointers (hostcall /
+// printf buffer, device heap, multigrid sync) stay zero, so a kernel using device printf, malloc or assert must not
+// take this path (the library has none: tests/test_abi.py checks the sources).
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -112,12 +115,17 @@ bool init(Aql &a) {
     if (hsa_queue_create(a.gpu, 4096, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &a.q) != HSA_STATUS_SUCCESS)
         return false;
     PoolFind p;
-    if (hsa_amd_agent_iterate_memory_pools(a.gpu, find_vram, &p) != HSA_STATUS_SUCCESS || !p.have ||
-        hsa_amd_memory_pool_allocate(p.pool, SLOT * a.q->size, 0, (void **)&a.karg) != HSA_STATUS_SUCCESS)
-        return false;
-    if (hsa_amd_agents_allow_access(1, &a.cpu, nullptr, a.karg) != HSA_STATUS_SUCCESS) return false;
-    if (hsa_signal_create(1, 0, nullptr, &a.done) != HSA_STATUS_SUCCESS) return false;
-    return true;
+    bool ok = hsa_amd_agent_iterate_memory_pools(a.gpu, find_vram, &p) == HSA_STATUS_SUCCESS && p.have &&
+              hsa_amd_memory_pool_allocate(p.pool, SLOT * a.q->size, 0, (void **)&a.karg) == HSA_STATUS_SUCCESS;
+    ok = ok && hsa_amd_agents_allow_access(1, &a.cpu, nullptr, a.karg) == HSA_STATUS_SUCCESS;
+    ok = ok && hsa_signal_create(1, 0, nullptr, &a.done) == HSA_STATUS_SUCCESS;
+    if (!ok) {                            // a partial set-up is released: this process then launches through HIP
+        if (a.karg) (void)hsa_amd_memory_pool_free(a.karg);
+        a.karg = nullptr;
+        (void)hsa_queue_destroy(a.q);
+        a.q = nullptr;
+    }
+    return ok;
 }
 
 struct SymFind {

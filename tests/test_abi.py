@@ -47,6 +47,21 @@ def test_no_oracle_linkage():
     assert "libamdhip64" in deps and "librccl" in deps
 
 
+def test_device_code_uses_no_runtime_services():
+    """The AQL launch mode (csrc/ggml-hip-aql.cpp) fills only the dispatch-geometry hidden arguments: no kernel may
+    use device printf, malloc / free or assert, whose hostcall / heap pointers would stay zero there."""
+    import re
+    csrc = os.path.join(PKG, "csrc")
+    pat = re.compile(r"\b(printf|malloc|free|assert|__assert_fail)\s*\(")
+    for f in sorted(os.listdir(csrc)):
+        if not (f.endswith(".hip") or f in ("q4_0_device.h",)):
+            continue
+        for i, line in enumerate(open(os.path.join(csrc, f)), 1):
+            code = line.split("//")[0]
+            hits = [m for m in pat.findall(code) if m]
+            assert not hits, f"{f}:{i}: {line.strip()}"
+
+
 def test_ggml_tensor_mirror_layout():
     T = ggml_hip.GgmlTensor
     assert ctypes.sizeof(T) == 240

@@ -36,6 +36,17 @@ if has prof; then    # the bench's own timed replays under the kernel tracer
   tail -1 "$O/prof.log" | cut -c1-300
   python3 tools/trace_steps.py "$O/prof" "$O/prof.log" > "$O/step_spans.json" || true
 fi
+if has final; then   # round-end evidence: the traced run first, installed under profiles/ (on the box), then the
+  # bench, whose roofline.rocprof_check reads those files: the line and the committed profiles agree
+  R=${ROUND:-r06}
+  step prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-exact --no-roofline-replays --no-aql
+  python3 tools/trace_steps.py "$O/prof" "$O/prof.log" > "$O/step_spans.json"
+  cp "$O/prof/run_kernel_stats.csv" "profiles/${R}_bench_rocprofv3_kernel_stats.csv"
+  cp "$O/step_spans.json" "profiles/${R}_bench_rocprofv3_step_spans.json"
+  step bench 480 python bench.py
+  tail -1 "$O/bench.log" | cut -c1-400
+fi
 if has pmc; then     # decode GEMV HBM bytes: one counter per pass (gfx950: FETCH_SIZE is half the streamed bytes)
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmc_$c 300 rocprofv3 --pmc $c -d "$O/pmc/$c" -o run --output-format csv -- \
